@@ -1,0 +1,101 @@
+"""Pin the oracle (oracle/encoder_ref.py) against fixtures produced by the reference."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from chunkformer_amd.config import LARGE, SMALL
+from chunkformer_amd.weights import synthetic_features, synthetic_state_dict
+from oracle import encoder_ref as ref
+
+torch.set_num_threads(min(8, os.cpu_count() or 1))
+
+
+def _load(golden_dir, name):
+    return np.load(os.path.join(golden_dir, name))
+
+
+def test_calc_length_closed_form():
+    for T in range(-40, 5000):
+        assert ref.calc_length(T) == 1 + (T - 15) // 8
+
+
+def test_masks_bit_exact(golden_dir):
+    g = _load(golden_dir, "masks.npz")
+    for i in range(int(g["n_cases"])):
+        C, L, R = (int(v) for v in g[f"c{i}_clr"])
+        lens, offs = g[f"c{i}_lens"].tolist(), g[f"c{i}_offs"].tolist()
+        att, pad, nch = ref.masks_closed_form(lens, offs, C, L, R)
+        sa, sp = g[f"c{i}_att_shape"], g[f"c{i}_pad_shape"]
+        exp_att = np.unpackbits(g[f"c{i}_att"], axis=-1, count=int(sa[1])).astype(bool)
+        exp_pad = np.unpackbits(g[f"c{i}_pad"], axis=-1, count=int(sp[1])).astype(bool)
+        assert nch == g[f"c{i}_nchunks"].tolist()
+        np.testing.assert_array_equal(att, exp_att, err_msg=f"case {i}")
+        np.testing.assert_array_equal(pad, exp_pad, err_msg=f"case {i}")
+        assert [ref.calc_length(t) for t in lens] == g[f"c{i}_outlens"].tolist()
+
+
+@pytest.fixture(scope="module")
+def small(golden_dir):
+    g = _load(golden_dir, "small.npz")
+    sd = synthetic_state_dict(SMALL, int(g["seed"]))
+    dig = np.array([float(v.double().sum()) for v in sd.values()])
+    np.testing.assert_allclose(dig, g["sd_digest"], rtol=0, atol=0)
+    return g, sd
+
+
+@pytest.mark.parametrize("case", ["a", "b", "c", "d"])
+def test_masked_batch_matches_reference(small, case):
+    g, sd = small
+    lens = g[f"{case}_lens"].tolist()
+    C, L, R = (int(v) for v in g[f"{case}_clr"])
+    xs = synthetic_features(lens, int(g[f"{case}_seed"]))
+    out, olens, nch, _, _, _ = ref.forward_parallel_chunk(sd, SMALL, xs, lens, C, L, R)
+    assert nch == g[f"{case}_nchunks"].tolist()
+    assert olens.tolist() == g[f"{case}_outlens"].tolist()
+    np.testing.assert_allclose(out.numpy(), g[f"{case}_out"], atol=2e-5, rtol=0)
+    if case == "a":
+        np.testing.assert_allclose(ref.ctc_log_softmax(sd, out).numpy(), g["a_logp"], atol=5e-5, rtol=0)
+
+
+def test_cache_path_matches_reference(small):
+    g, sd = small
+    xs = synthetic_features([900], int(g["cache_seed"]))
+    out, _, _, ac, cc, off = ref.forward_parallel_chunk(
+        sd, SMALL, xs, [900], 16, 32, 32, torch.from_numpy(g["cache_att_in"]),
+        torch.from_numpy(g["cache_cnn_in"]), 48, [5])
+    np.testing.assert_allclose(out.numpy(), g["cache_out"], atol=2e-5, rtol=0)
+    np.testing.assert_allclose(ac.numpy(), g["cache_att_out"], atol=2e-5, rtol=0)
+    np.testing.assert_allclose(cc.numpy(), g["cache_cnn_out"], atol=2e-5, rtol=0)
+    assert off.tolist() == g["cache_offset_out"].tolist()
+
+
+@pytest.mark.parametrize("case", ["pc", "pf"])
+def test_padded_path_matches_reference(small, case):
+    g, sd = small
+    lens = g[f"{case}_lens"].tolist()
+    C, L, R = (int(v) for v in g[f"{case}_clr"])
+    xs = synthetic_features(lens, int(g[f"{case}_seed"]))
+    xp = torch.zeros(len(lens), max(lens), 80)
+    for i, t in enumerate(xs):
+        xp[i, : t.shape[0]] = t
+    out, masks = ref.forward_encoder(sd, SMALL, xp, lens, C, L, R)
+    np.testing.assert_array_equal(masks.numpy(), g[f"{case}_mask"])
+    np.testing.assert_allclose(out.numpy(), g[f"{case}_out"], atol=2e-5, rtol=0)
+
+
+def test_large_matches_reference(golden_dir):
+    g = _load(golden_dir, "large.npz")
+    sd = synthetic_state_dict(LARGE, int(g["seed"]))
+    lens = g["lens"].tolist()
+    xs = synthetic_features(lens, int(g["feat_seed"]))
+    out, olens, nch, _, _, _ = ref.forward_parallel_chunk(sd, LARGE, xs, lens, 64, 128, 128)
+    assert nch == g["nchunks"].tolist()
+    np.testing.assert_allclose(out.numpy(), g["out"], atol=1e-4, rtol=0)
+    logp = ref.ctc_log_softmax(sd, out)
+    top2 = g["top2"]
+    margin = top2[..., 0] - top2[..., 1]
+    ids = logp.argmax(-1).numpy()
+    sure = margin > 1e-4
+    np.testing.assert_array_equal(ids[sure], g["ids"][sure])
