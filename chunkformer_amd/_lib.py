@@ -1,0 +1,118 @@
+"""ctypes binding of libcfm.so (include/cfm.h).
+
+The library is the product: there is no Python/CPU fallback.  If the shared
+object is missing this module raises at import time, and every encoder call
+goes through it.  torch is imported first so that libcfm's libamdhip64.so.7
+dependency resolves to the HIP runtime torch already loaded (one runtime per
+process).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch  # noqa: F401  (load torch's HIP runtime before libcfm)
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("CFM_LIB", os.path.join(HERE, "_build", "libcfm.so"))
+
+if not os.path.exists(LIB_PATH):
+    raise ImportError(f"libcfm.so not found at {LIB_PATH}: run `python -m chunkformer_amd.build` "
+                      "(the HIP extension is required; there is no CPU fallback)")
+
+lib = ctypes.CDLL(LIB_PATH)
+
+P = ctypes.c_void_p
+I32 = ctypes.c_int32
+I64 = ctypes.c_int64
+SZ = ctypes.c_size_t
+PI32 = ctypes.POINTER(ctypes.c_int32)
+PI64 = ctypes.POINTER(ctypes.c_int64)
+
+CFM_OK, CFM_ERR_VALUE, CFM_ERR_ASSERT, CFM_ERR_RUNTIME = 0, 1, 2, 3
+DTYPE_F32, DTYPE_BF16 = 0, 1
+PLAN_HEADER = 16
+PLAN_REC = 8
+
+
+class CfmConfig(ctypes.Structure):
+    _fields_ = [("input_dim", I32), ("d_model", I32), ("n_heads", I32), ("ffn_dim", I32), ("num_blocks", I32),
+                ("kernel_size", I32), ("vocab", I32), ("norm_eps", ctypes.c_float), ("has_cmvn", I32),
+                ("compute_dtype", I32)]
+
+
+class CfmTensorView(ctypes.Structure):
+    _fields_ = [("name", ctypes.c_char_p), ("data", P), ("numel", I64)]
+
+
+def _sig(name, res, *args):
+    f = getattr(lib, name)
+    f.restype = res
+    f.argtypes = list(args)
+    return f
+
+
+cfm_version = _sig("cfm_version", ctypes.c_char_p)
+cfm_last_error = _sig("cfm_last_error", ctypes.c_char_p)
+cfm_model_create = _sig("cfm_model_create", I32, ctypes.POINTER(CfmConfig), ctypes.POINTER(CfmTensorView), I32, I32,
+                        ctypes.POINTER(P))
+cfm_model_destroy = _sig("cfm_model_destroy", None, P)
+cfm_model_set_option = _sig("cfm_model_set_option", I32, P, ctypes.c_char_p, I64)
+cfm_plan_masked = _sig("cfm_plan_masked", I32, P, P, I32, I32, I32, I32, P, P, PI32, P, PI64)
+cfm_plan_padded = _sig("cfm_plan_padded", I32, P, I32, I32, I32, I32, I32, PI32, P, PI64)
+cfm_workspace_bytes_masked = _sig("cfm_workspace_bytes_masked", SZ, P, I32, I32, I32, I32)
+cfm_workspace_bytes_padded = _sig("cfm_workspace_bytes_padded", SZ, P, I32, I32, I32, I32, I32)
+cfm_encode_masked = _sig("cfm_encode_masked", I32, P, P, P, P, P, P, I32, P, P, P, P, SZ, P)
+cfm_encode_padded = _sig("cfm_encode_padded", I32, P, P, P, P, P, P, SZ, P)
+cfm_masks_from_plan = _sig("cfm_masks_from_plan", I32, P, P, P, P, P)
+cfm_ctc_workspace_bytes = _sig("cfm_ctc_workspace_bytes", SZ, P, I32)
+cfm_ctc_logprobs = _sig("cfm_ctc_logprobs", I32, P, P, I32, P, P, P, SZ, P)
+
+EXPORTED = ["cfm_version", "cfm_last_error", "cfm_model_create", "cfm_model_destroy", "cfm_model_set_option",
+            "cfm_plan_masked", "cfm_plan_padded", "cfm_workspace_bytes_masked", "cfm_workspace_bytes_padded",
+            "cfm_encode_masked", "cfm_encode_padded", "cfm_masks_from_plan", "cfm_ctc_workspace_bytes",
+            "cfm_ctc_logprobs"]
+
+
+def check(status: int) -> None:
+    """Map a cfm_status to the reference's exception types (include/cfm.h)."""
+    if status == CFM_OK:
+        return
+    msg = (cfm_last_error() or b"").decode(errors="replace")
+    if status == CFM_ERR_VALUE:
+        raise ValueError(msg)
+    if status == CFM_ERR_ASSERT:
+        raise AssertionError(msg)
+    raise RuntimeError(msg)
+
+
+def ptr(t) -> int:
+    return 0 if t is None else t.data_ptr()
+
+
+def plan_masked(lens, offsets, C: int, L: int, R: int):
+    """Host planner (no GPU): returns (plan int32 CPU tensor, n_chunks list, out_lens list)."""
+    B = len(lens)
+    lens_t = torch.tensor([int(x) for x in lens], dtype=torch.int32)
+    offs_t = torch.tensor([int(x) for x in offsets], dtype=torch.int32) if offsets is not None else None
+    nch = torch.zeros(B, dtype=torch.int32)
+    olen = torch.zeros(B, dtype=torch.int32)
+    total = I32(0)
+    n = I64(0)
+    check(cfm_plan_masked(lens_t.data_ptr(), ptr(offs_t), B, C, L, R, nch.data_ptr(), olen.data_ptr(),
+                          ctypes.byref(total), None, ctypes.byref(n)))
+    plan = torch.zeros(n.value, dtype=torch.int32)
+    check(cfm_plan_masked(lens_t.data_ptr(), ptr(offs_t), B, C, L, R, None, None, ctypes.byref(total),
+                          plan.data_ptr(), ctypes.byref(n)))
+    return plan, nch.tolist(), olen.tolist()
+
+
+def plan_padded(lens, T: int, C: int, L: int, R: int):
+    B = len(lens)
+    lens_t = torch.tensor([int(x) for x in lens], dtype=torch.int32)
+    tout = I32(0)
+    n = I64(0)
+    check(cfm_plan_padded(lens_t.data_ptr(), B, T, C, L, R, ctypes.byref(tout), None, ctypes.byref(n)))
+    plan = torch.zeros(n.value, dtype=torch.int32)
+    check(cfm_plan_padded(lens_t.data_ptr(), B, T, C, L, R, ctypes.byref(tout), plan.data_ptr(), ctypes.byref(n)))
+    return plan, tout.value

@@ -1,0 +1,123 @@
+// Common device/host helpers for the gfx950 (CDNA4) ChunkFormer kernels.
+//
+// Element type T of every activation/weight stream is either `float` (parity
+// mode: exact-f32 MFMA v_mfma_f32_16x16x4_f32) or `bf16` (fast mode:
+// v_mfma_f32_16x16x32_bf16).  Accumulation, softmax and LayerNorm statistics
+// are always f32.  Both operand types share ONE fragment abstraction: a lane
+// holds 8 consecutive K elements of its row (A) / column (B); for bf16 that is
+// one 16x16x32 MFMA, for f32 eight 16x16x4 MFMAs (instruction e consumes
+// element e of every lane: k = 8*(lane>>4) + e).  Any consistent K permutation
+// is a valid contraction, so LDS images and address math are identical for
+// both types and only the byte width of a fragment differs (16 B vs 32 B).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef __bf16 bf16;
+typedef bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x8 __attribute__((ext_vector_type(8)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+#define CFM_DEV __device__ __forceinline__
+
+template <typename T> struct Frag;
+template <> struct Frag<float> { typedef f32x8 type; };
+template <> struct Frag<bf16> { typedef bf16x8 type; };
+
+CFM_DEV float to_f32(float x) { return x; }
+CFM_DEV float to_f32(bf16 x) { return (float)x; }
+template <typename T> CFM_DEV T from_f32(float x);
+template <> CFM_DEV float from_f32<float>(float x) { return x; }
+template <> CFM_DEV bf16 from_f32<bf16>(float x) { return (bf16)x; }
+
+// 16x16 output tile += A(16 x 32) * B(32 x 16) expressed on 8-element fragments
+CFM_DEV f32x4 mma16(const f32x8& a, const f32x8& b, f32x4 acc) {
+#pragma unroll
+  for (int e = 0; e < 8; ++e) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[e], b[e], acc, 0, 0, 0);
+  return acc;
+}
+CFM_DEV f32x4 mma16(const bf16x8& a, const bf16x8& b, f32x4 acc) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc, 0, 0, 0);
+}
+
+// load 8 consecutive elements (16 B for bf16, 32 B for f32)
+template <typename T> CFM_DEV typename Frag<T>::type ld8(const T* p) {
+  return *reinterpret_cast<const typename Frag<T>::type*>(p);
+}
+template <typename T> CFM_DEV void st8(T* p, const typename Frag<T>::type& v) {
+  *reinterpret_cast<typename Frag<T>::type*>(p) = v;
+}
+template <typename T> CFM_DEV typename Frag<T>::type zero8() {
+  typename Frag<T>::type z;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) z[e] = (T)0.0f;
+  return z;
+}
+
+CFM_DEV float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+CFM_DEV float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+// reductions inside aligned groups of 16 lanes (one MFMA 16x16 output row group)
+CFM_DEV float group16_max(float v) {
+#pragma unroll
+  for (int o = 8; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+CFM_DEV float group16_sum(float v) {
+#pragma unroll
+  for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+CFM_DEV float silu_f(float x) { return x / (1.0f + __expf(-x)); }
+CFM_DEV float sigmoid_f(float x) { return 1.0f / (1.0f + __expf(-x)); }
+
+// ----------------------------------------------------------------------------- plan records
+// Per packed chunk (masked batch), produced by the host planner (planner.cpp):
+enum {
+  PM_SRC_ROW = 0,   // first feature row of the chunk's window in the packed [sum T, 80] feats
+  PM_NVALID = 1,    // real feature rows in the window (rest is zero padding)
+  PM_ATT_LO = 2,    // attention window keys j in [lo, hi) are unmasked
+  PM_ATT_HI = 3,
+  PM_CONV_LO = 4,   // conv window columns j in [lo, hi) are unmasked (mask_pad)
+  PM_CONV_HI = 5,
+  PM_UTT = 6,
+  PM_CHUNK = 7,
+  PM_INTS = 8
+};
+
+// Attention block descriptor (one block of <=64 query rows x one head):
+enum {
+  AD_Q_ROW0 = 0,    // first query row in the Q / output buffers
+  AD_NQ = 1,        // query rows in this block (<= 64)
+  AD_KV_ROW0 = 2,   // KV stream row of window key j = 0 (may be negative: only keys in [lo,hi) are read)
+  AD_KEY_LO = 3,    // window keys j in [lo, hi) are unmasked, all others are -inf
+  AD_KEY_HI = 4,
+  AD_P_BASE = 5,    // rel-pos row of (query i, key j) is P_BASE - i + j
+  AD_Q_VALID = 6,   // query rows i >= Q_VALID are fully masked (output 0)
+  AD_PAD = 7,
+  AD_INTS = 8
+};
+
+// Depthwise-conv block descriptor (<= 64 output rows of one chunk / one padded segment)
+enum {
+  CD_OUT_ROW0 = 0,  // first output row
+  CD_NOUT = 1,      // output rows
+  CD_SRC_ROW0 = 2,  // input (GLU stream) row of window column j = 0; column j feeds output i = j - 7 .. j + 7
+  CD_J_LO = 3,      // window columns j in [lo, hi) are real, others are 0
+  CD_J_HI = 4,
+  CD_SEG_LO = 5,    // padded path: extra per-row segment bound (see conv_module.hip)
+  CD_SEG = 6,       // padded path: chunk length for per-row segments (0 = none)
+  CD_PAD = 7,
+  CD_INTS = 8
+};
+
+#define CFM_CHECK_LAUNCH() do { hipError_t _e = hipGetLastError(); if (_e != hipSuccess) return (int)_e; } while (0)

@@ -1,0 +1,72 @@
+// Internal launcher declarations (host side) for the gfx950 kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace cfm {
+
+enum { EPI_STORE = 0, EPI_STORE_F32 = 1, EPI_RESID = 2, EPI_QKV = 3, EPI_GLU = 4 };
+enum { ACT_NONE = 0, ACT_RELU = 1, ACT_SILU = 2 };
+
+struct EpiArgs {
+  const float* bias = nullptr;   // [N] f32 or null
+  float alpha = 1.f;
+  void* out = nullptr;           // STORE/STORE_F32/GLU output, QKV: q buffer [M, d]
+  void* out2 = nullptr;          // QKV: KV stream [rows, H, 2*dk]
+  int ldo = 0;                   // output row stride (elements)
+  int row_off = 0;               // STORE*/GLU/QKV(kv): output row offset
+  float* x = nullptr;            // RESID: f32 residual stream
+  int ldx = 0;
+  const uint8_t* rowmask = nullptr;  // RESID: per-row 0/1 multiplier (null = all 1)
+  int d = 0;                     // QKV: model dim
+};
+
+template <typename T>
+int gemm(int epi, int act, const T* A, int lda, const T* W, int ldw, int M, int N, int K, const EpiArgs& ep,
+         hipStream_t st);
+
+// LayerNorm over d (eps) of f32 rows -> T rows; optional 0/1 row mask on the output.
+template <typename T>
+int layernorm(const float* x, int M, int d, const float* w, const float* b, float eps, T* out,
+              const uint8_t* rowmask, hipStream_t st);
+// y = LN1(x) written back to x (f32); then out = LN2(y) as T (LN2 may be null: out = y as T).
+template <typename T>
+int layernorm2(float* x, int M, int d, const float* w1, const float* b1, const float* w2, const float* b2,
+               float eps, T* out, hipStream_t st);
+// same, with the second output in f32 (final after_norm)
+int layernorm2_f32(float* x, int M, int d, const float* w1, const float* b1, const float* w2, const float* b2,
+                   float eps, float* out, hipStream_t st);
+
+// chunk attention (attention.hip)
+template <typename T>
+int chunk_attention(const T* q, const T* kv, int kv_rows, const T* P, int p_rows, const float* pos_u,
+                    const float* pos_v, const int32_t* desc, int nblk, int H, T* out, hipStream_t st);
+
+// conv module: depthwise k=15 + bias + LayerNorm + SiLU (conv_module.hip)
+template <typename T>
+int conv_dw_ln_silu(const T* glu, const int32_t* desc, int nblk, int d, const float* wdw_t /*[15][d]*/,
+                    const float* bdw, const float* lnw, const float* lnb, float eps, T* out, hipStream_t st);
+
+// front-end (frontend.hip): meta rows give (src_row, nvalid) per window at PM_SRC_ROW / PM_NVALID
+template <typename T>
+int frontend_conv0_dw(const float* feats, const int32_t* meta, int meta_stride, int nwin, int W,
+                      const float* cmvn_mean, const float* cmvn_istd, const float* w0, const float* b0,
+                      const float* w1, const float* b1, int d, T* out, hipStream_t st);
+template <typename T>
+int frontend_dw2(const T* in, int nwin, int T2, int d, const float* w, const float* b, T* out, hipStream_t st);
+
+// misc (misc.hip)
+template <typename T>
+int pos_table(int d, int p_rows, int anchor, T* out, hipStream_t st);
+template <typename T>
+int att_cache_in(const float* cache, int L, int row_elems, T* kv, hipStream_t st);
+template <typename T>
+int att_cache_out(const T* kv, int start_row, int L, int row_elems, float* cache, hipStream_t st);
+template <typename T>
+int cnn_cache_in(const float* cache /*[d][7]*/, int d, int lorder, T* glu, hipStream_t st);
+template <typename T>
+int cnn_cache_out(const T* glu, int start_row, int d, int lorder, float* cache, hipStream_t st);
+int masks_from_plan(const int32_t* meta, int n, int C, int L, int R, uint8_t* att, uint8_t* pad, hipStream_t st);
+int log_softmax_rows(float* logits, int M, int V, int write_logp, int32_t* ids, hipStream_t st);
+
+}  // namespace cfm

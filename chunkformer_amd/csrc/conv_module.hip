@@ -1,0 +1,114 @@
+// Convolution module middle: overlapping-chunk window -> mask -> depthwise
+// conv k=15 (valid) -> LayerNorm(channels) -> SiLU.
+//
+// Reference: ChunkConvolutionModule.forward_parallel_chunk (convolution.py:224-249)
+// and, with other descriptors, the dynamic-chunk padded `forward`
+// (convolution.py:133-186).  pointwise_conv1+GLU runs in the GEMM epilogue and
+// writes a flat GLU stream; pointwise_conv2 (+ output mask) is the next GEMM.
+//
+// Descriptor (cfm_common.h CD_*): output row i of the block reads stream rows
+// SRC_ROW0 + i + t, t = 0..14, i.e. window columns j = i + t; columns outside
+// [J_LO, J_HI) are zero (torch.where(mask_pad, x, 0) / zero padding).
+// One wave per output row, lane l owns channels [l*VPL, l*VPL+VPL); the LN
+// statistics are wave reductions.  Depthwise weights are stored tap-major
+// [15][d] so every tap is one coalesced vector load.
+#include "cfm_common.h"
+#include "cfm_kernels.h"
+
+namespace cfm {
+
+template <typename T, int VPL> struct VecIO;
+template <int VPL> struct VecIO<float, VPL> {
+  static CFM_DEV void load(const float* p, float (&v)[VPL]) {
+#pragma unroll
+    for (int e = 0; e < VPL; e += 2) {
+      typedef float f2 __attribute__((ext_vector_type(2)));
+      const f2 t = *reinterpret_cast<const f2*>(p + e);
+      v[e] = t[0]; v[e + 1] = t[1];
+    }
+  }
+  static CFM_DEV void store(float* p, const float (&v)[VPL]) {
+#pragma unroll
+    for (int e = 0; e < VPL; e += 2) {
+      typedef float f2 __attribute__((ext_vector_type(2)));
+      *reinterpret_cast<f2*>(p + e) = (f2){v[e], v[e + 1]};
+    }
+  }
+};
+template <int VPL> struct VecIO<bf16, VPL> {
+  static CFM_DEV void load(const bf16* p, float (&v)[VPL]) {
+#pragma unroll
+    for (int e = 0; e < VPL; e += 2) {
+      typedef bf16 b2 __attribute__((ext_vector_type(2)));
+      const b2 t = *reinterpret_cast<const b2*>(p + e);
+      v[e] = (float)t[0]; v[e + 1] = (float)t[1];
+    }
+  }
+  static CFM_DEV void store(bf16* p, const float (&v)[VPL]) {
+#pragma unroll
+    for (int e = 0; e < VPL; e += 2) {
+      typedef bf16 b2 __attribute__((ext_vector_type(2)));
+      *reinterpret_cast<b2*>(p + e) = (b2){(bf16)v[e], (bf16)v[e + 1]};
+    }
+  }
+};
+
+template <typename T, int VPL>
+__global__ __launch_bounds__(256) void conv_dw_ln_silu_kernel(const T* __restrict__ glu, const int32_t* __restrict__ desc,
+                                                              const float* __restrict__ wdw, const float* __restrict__ bdw,
+                                                              const float* __restrict__ lnw, const float* __restrict__ lnb,
+                                                              float eps, T* __restrict__ out) {
+  constexpr int d = VPL * 64;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int32_t* D = desc + (size_t)blockIdx.x * CD_INTS;
+  const int out_row0 = D[CD_OUT_ROW0], nout = D[CD_NOUT], src0 = D[CD_SRC_ROW0];
+  const int jlo = D[CD_J_LO], jhi = D[CD_J_HI];
+  const int c0 = lane * VPL;
+  float bias[VPL];
+#pragma unroll
+  for (int e = 0; e < VPL; ++e) bias[e] = bdw[c0 + e];
+  for (int i = blockIdx.y * 4 + w; i < nout; i += 4 * gridDim.y) {
+    float acc[VPL];
+#pragma unroll
+    for (int e = 0; e < VPL; ++e) acc[e] = bias[e];
+    const int tlo = max(0, jlo - i), thi = min(15, jhi - i);
+    for (int t = tlo; t < thi; ++t) {
+      float xv[VPL], wv[VPL];
+      VecIO<T, VPL>::load(glu + (size_t)(src0 + i + t) * d + c0, xv);
+      VecIO<float, VPL>::load(wdw + t * d + c0, wv);
+#pragma unroll
+      for (int e = 0; e < VPL; ++e) acc[e] = fmaf(xv[e], wv[e], acc[e]);
+    }
+    float s = 0.f;
+#pragma unroll
+    for (int e = 0; e < VPL; ++e) s += acc[e];
+    const float mean = wave_sum(s) / d;
+    float q = 0.f;
+#pragma unroll
+    for (int e = 0; e < VPL; ++e) { const float t = acc[e] - mean; q += t * t; }
+    const float rstd = rsqrtf(wave_sum(q) / d + eps);
+#pragma unroll
+    for (int e = 0; e < VPL; ++e) acc[e] = silu_f((acc[e] - mean) * rstd * lnw[c0 + e] + lnb[c0 + e]);
+    VecIO<T, VPL>::store(out + (size_t)(out_row0 + i) * d + c0, acc);
+  }
+}
+
+template <typename T>
+int conv_dw_ln_silu(const T* glu, const int32_t* desc, int nblk, int d, const float* wdw_t, const float* bdw,
+                    const float* lnw, const float* lnb, float eps, T* out, hipStream_t st) {
+  if (nblk <= 0) return 0;
+  const dim3 grid(nblk, 4);   // 4 x 4 waves stride over the (<= 64) rows of a block
+  if (d == 128) hipLaunchKernelGGL((conv_dw_ln_silu_kernel<T, 2>), grid, dim3(256), 0, st, glu, desc, wdw_t, bdw, lnw, lnb, eps, out);
+  else if (d == 256) hipLaunchKernelGGL((conv_dw_ln_silu_kernel<T, 4>), grid, dim3(256), 0, st, glu, desc, wdw_t, bdw, lnw, lnb, eps, out);
+  else if (d == 512) hipLaunchKernelGGL((conv_dw_ln_silu_kernel<T, 8>), grid, dim3(256), 0, st, glu, desc, wdw_t, bdw, lnw, lnb, eps, out);
+  else return (int)hipErrorInvalidValue;
+  CFM_CHECK_LAUNCH();
+  return 0;
+}
+
+template int conv_dw_ln_silu<float>(const float*, const int32_t*, int, int, const float*, const float*, const float*,
+                                    const float*, float, float*, hipStream_t);
+template int conv_dw_ln_silu<bf16>(const bf16*, const int32_t*, int, int, const float*, const float*, const float*,
+                                   const float*, float, bf16*, hipStream_t);
+
+}  // namespace cfm

@@ -1,0 +1,516 @@
+// Model handle, weight repacking and the per-call orchestration of the encoder.
+//
+// ModelT<T>::encode runs, on one stream and without allocation or host sync:
+//   front-end (frontend.hip + 3 GEMMs, in window groups) -> x [rows, d] f32
+//   P_l = pos_emb . W_pos_l^T for every layer (attention.py:481-483)
+//   12 x ChunkFormerEncoderLayer (encoder_layer.py:155-248 masked / 62-153 padded):
+//     LN -> FFN_mac (GEMM SiLU, GEMM resid x0.5) -> LN -> QKV GEMM -> chunk attention
+//     -> out-proj GEMM (resid) -> LN -> pw1 GEMM + GLU -> dw/LN/SiLU -> pw2 GEMM (masked resid)
+//     -> LN -> FFN (x0.5) -> norm_final fused with the next layer's first LN / after_norm
+#include <cmath>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../../include/cfm.h"
+#include "cfm_common.h"
+#include "cfm_kernels.h"
+#include "plan.h"
+#include "status.h"
+
+namespace cfm {
+
+static thread_local std::string g_err;
+cfm_status set_error(cfm_status s, const std::string& msg) {
+  g_err = msg;
+  return s;
+}
+
+#define HIPC(x)                                                                               \
+  do {                                                                                        \
+    hipError_t _e = (x);                                                                      \
+    if (_e != hipSuccess) return set_error(CFM_ERR_RUNTIME, std::string(#x ": ") + hipGetErrorString(_e)); \
+  } while (0)
+#define KCHK(x)                                                                               \
+  do {                                                                                        \
+    int _e = (x);                                                                             \
+    if (_e) return set_error(CFM_ERR_RUNTIME, std::string(#x ": ") + hipGetErrorString((hipError_t)_e)); \
+  } while (0)
+
+static size_t align_up(size_t x, size_t a = 256) { return (x + a - 1) / a * a; }
+
+struct Carver {
+  char* base;
+  size_t off = 0;
+  explicit Carver(void* b) : base((char*)b) {}
+  template <typename U> U* take(size_t n) {
+    U* p = (U*)(base ? base + off : nullptr);
+    off += align_up(n * sizeof(U));
+    return p;
+  }
+};
+
+struct LayerW {
+  void *ff1m, *ff2m, *ff1, *ff2, *qkv, *pos, *wo, *pw1, *pw2;   // T matrices [N][K]
+  float *b_ff1m, *b_ff2m, *b_ff1, *b_ff2, *b_qkv, *b_o, *b_pw1, *b_pw2;
+  float *pu, *pv, *dw_t, *b_dw, *cn_w, *cn_b;
+  float *ln_ffm_w, *ln_ffm_b, *ln_mha_w, *ln_mha_b, *ln_conv_w, *ln_conv_b, *ln_ff_w, *ln_ff_b, *ln_fin_w, *ln_fin_b;
+};
+
+struct FrontW {
+  float *cm = nullptr, *ci = nullptr, *w0, *b0, *w1, *b1, *w2, *b2, *b_pw1, *b_pw2, *b_out;
+  void *pw1, *pw2, *wout;
+  float *an_w, *an_b;
+  void* ctc_w = nullptr;
+  float* ctc_b = nullptr;
+};
+
+}  // namespace cfm
+
+struct cfm_model {
+  cfm_config cfg;
+  int device = 0;
+  void* dev_mem = nullptr;
+  std::vector<cfm::LayerW> layers;
+  cfm::FrontW fe;
+  int max_layers = -1;
+  virtual ~cfm_model() {
+    if (dev_mem) { (void)hipSetDevice(device); (void)hipFree(dev_mem); }
+  }
+  virtual cfm_status encode(const float* feats, const int32_t* plan_dev, const int32_t* plan_hdr, const float* aci,
+                            const float* cci, int trunc, float* aco, float* cco, float* out, void* ws, size_t wsb,
+                            hipStream_t st) const = 0;
+  virtual cfm_status ctc(const float* enc, int rows, float* logp, int32_t* ids, void* ws, size_t wsb,
+                         hipStream_t st) const = 0;
+  virtual size_t ws_bytes(const int32_t* hdr) const = 0;
+  virtual size_t ctc_ws_bytes(int rows) const = 0;
+};
+
+namespace cfm {
+
+template <typename T>
+struct ModelT : public cfm_model {
+  // front-end window group size: bounds the [G, T2, 19, d] intermediates
+  int fe_group(const int32_t* h) const {
+    const int W = h[PH_W];
+    const int T1 = (W - 3) / 2 + 1, T2 = (T1 - 3) / 2 + 1;
+    const size_t per = (size_t)T2 * 19 * cfg.d_model * sizeof(T);
+    const size_t cap = (size_t)768 << 20;   // 768 MiB per intermediate buffer
+    int g = (int)std::max<size_t>(1, cap / per);
+    return std::min(g, h[PH_NWIN]);
+  }
+
+  struct WS {
+    float* x;
+    T *h, *hid, *q, *kv, *ao, *glu, *cv, *P, *pos, *feA, *feB;
+  };
+
+  WS carve(void* base, const int32_t* h, size_t* total) const {
+    const int d = cfg.d_model, ff = cfg.ffn_dim, nb = cfg.num_blocks;
+    const size_t rows = h[PH_ROWS];
+    const size_t prow_pad = (h[PH_PROWS] + 127) / 128 * 128;
+    const int W = h[PH_W];
+    const int T1 = (W - 3) / 2 + 1, T2 = (T1 - 3) / 2 + 1;
+    const size_t G = fe_group(h);
+    Carver c(base);
+    WS w;
+    w.x = c.take<float>(rows * d);
+    w.h = c.take<T>(rows * d);
+    w.hid = c.take<T>(rows * ff);
+    w.q = c.take<T>(rows * d);
+    w.kv = c.take<T>((size_t)h[PH_KVROWS] * 2 * d);
+    w.ao = c.take<T>(rows * d);
+    w.glu = c.take<T>((size_t)h[PH_GLUROWS] * d);
+    w.cv = c.take<T>(rows * d);
+    w.P = c.take<T>((size_t)nb * prow_pad * d);
+    w.pos = c.take<T>(prow_pad * d);
+    w.feA = c.take<T>(G * T2 * 19 * d);
+    w.feB = c.take<T>(G * T2 * 19 * d);
+    if (total) *total = c.off;
+    return w;
+  }
+
+  size_t ws_bytes(const int32_t* hdr) const override {
+    size_t t = 0;
+    carve(nullptr, hdr, &t);
+    return t + 4096;
+  }
+  size_t ctc_ws_bytes(int rows) const override {
+    return align_up((size_t)rows * cfg.vocab * sizeof(float)) + align_up((size_t)rows * cfg.d_model * sizeof(T)) + 4096;
+  }
+
+  cfm_status encode(const float* feats, const int32_t* plan_dev, const int32_t* hh, const float* aci, const float* cci,
+                    int trunc, float* aco, float* cco, float* out, void* ws, size_t wsb,
+                    hipStream_t st) const override {
+    const int d = cfg.d_model, ff = cfg.ffn_dim, H = cfg.n_heads;
+    const float eps = cfg.norm_eps;
+    const int rows = hh[PH_ROWS], C = hh[PH_C], L = hh[PH_L];
+    const int nwin = hh[PH_NWIN], Wn = hh[PH_W], tout = hh[PH_TOUT];
+    const int p_rows = hh[PH_PROWS], kv_rows = hh[PH_KVROWS], glu_rows = hh[PH_GLUROWS];
+    const int kvoff = hh[PH_KVOFF], gluoff = hh[PH_GLUOFF];
+    const bool masked = hh[PH_KIND] == 1;
+    const size_t prow_pad = (p_rows + 127) / 128 * 128;
+    if (wsb < ws_bytes(hh)) return set_error(CFM_ERR_VALUE, "workspace too small");
+    if (!masked && (aci || cci)) return set_error(CFM_ERR_VALUE, "caches are only defined for the masked batch path");
+    WS w = carve(ws, hh, nullptr);
+    const int32_t* meta = plan_dev + plan_meta_off(hh);
+    const int32_t* attd = plan_dev + plan_att_off(hh);
+    const int32_t* convd = plan_dev + plan_conv_off(hh);
+    const uint8_t* rmask = reinterpret_cast<const uint8_t*>(plan_dev + plan_mask_off(hh));
+    const int T1 = (Wn - 3) / 2 + 1, T2 = (T1 - 3) / 2 + 1, T3 = (T2 - 3) / 2 + 1;
+    if (T3 != tout) return set_error(CFM_ERR_RUNTIME, "plan / front-end geometry mismatch");
+
+    // ---------------- front-end
+    const int G = fe_group(hh);
+    for (int g0 = 0; g0 < nwin; g0 += G) {
+      const int ng = std::min(G, nwin - g0);
+      KCHK(frontend_conv0_dw<T>(feats, meta + (size_t)g0 * PLAN_REC, PLAN_REC, ng, Wn, fe.cm, fe.ci, fe.w0, fe.b0,
+                                fe.w1, fe.b1, d, w.feA, st));
+      EpiArgs e1; e1.bias = fe.b_pw1; e1.out = w.feB; e1.ldo = d;
+      KCHK(gemm<T>(EPI_STORE, ACT_RELU, w.feA, d, (const T*)fe.pw1, d, ng * T2 * 19, d, d, e1, st));
+      KCHK(frontend_dw2<T>(w.feB, ng, T2, d, fe.w2, fe.b2, w.feA, st));
+      EpiArgs e2; e2.bias = fe.b_pw2; e2.out = w.feB; e2.ldo = d;
+      KCHK(gemm<T>(EPI_STORE, ACT_RELU, w.feA, d, (const T*)fe.pw2, d, ng * T3 * 9, d, d, e2, st));
+      EpiArgs e3; e3.bias = fe.b_out; e3.out = w.x; e3.ldo = d; e3.row_off = g0 * tout; e3.alpha = std::sqrt((float)d);
+      KCHK(gemm<T>(EPI_STORE_F32, ACT_NONE, w.feB, 9 * d, (const T*)fe.wout, 9 * d, ng * T3, d, 9 * d, e3, st));
+    }
+    // ---------------- relative positions: P_l = pos . W_pos_l^T
+    const int nl = (max_layers >= 0 && max_layers < cfg.num_blocks) ? max_layers : cfg.num_blocks;
+    KCHK(pos_table<T>(d, p_rows, hh[PH_PANCHOR], w.pos, st));
+    for (int l = 0; l < nl; ++l) {
+      EpiArgs e; e.out = w.P + (size_t)l * prow_pad * d; e.ldo = d;
+      KCHK(gemm<T>(EPI_STORE, ACT_NONE, w.pos, d, (const T*)layers[l].pos, d, p_rows, d, d, e, st));
+    }
+    // ---------------- stream padding rows (cache slots and right zero padding)
+    if (kvoff > 0) HIPC(hipMemsetAsync(w.kv, 0, (size_t)kvoff * 2 * d * sizeof(T), st));
+    if (kv_rows > kvoff + rows)
+      HIPC(hipMemsetAsync(w.kv + (size_t)(kvoff + rows) * 2 * d, 0, (size_t)(kv_rows - kvoff - rows) * 2 * d * sizeof(T), st));
+    if (gluoff > 0) HIPC(hipMemsetAsync(w.glu, 0, (size_t)gluoff * d * sizeof(T), st));
+    if (glu_rows > gluoff + rows)
+      HIPC(hipMemsetAsync(w.glu + (size_t)(gluoff + rows) * d, 0, (size_t)(glu_rows - gluoff - rows) * d * sizeof(T), st));
+
+    const int natt = hh[PH_NATT], nconv = hh[PH_NCONV];
+    const int cache_start = std::min(trunc, rows);   // new cache = stream[:trunc + L][-L:] (attention.py:467)
+    if (nl == 0) {
+      KCHK(layernorm2_f32(w.x, rows, d, fe.an_w, fe.an_b, nullptr, nullptr, eps, out, st));
+      return CFM_OK;
+    }
+    KCHK(layernorm<T>(w.x, rows, d, layers[0].ln_ffm_w, layers[0].ln_ffm_b, eps, w.h, nullptr, st));
+    for (int l = 0; l < nl; ++l) {
+      const LayerW& Lw = layers[l];
+      // macaron FFN (x 0.5)
+      { EpiArgs e; e.bias = Lw.b_ff1m; e.out = w.hid; e.ldo = ff;
+        KCHK(gemm<T>(EPI_STORE, ACT_SILU, w.h, d, (const T*)Lw.ff1m, d, rows, ff, d, e, st)); }
+      { EpiArgs e; e.bias = Lw.b_ff2m; e.x = w.x; e.ldx = d; e.alpha = 0.5f;
+        KCHK(gemm<T>(EPI_RESID, ACT_NONE, w.hid, ff, (const T*)Lw.ff2m, ff, rows, d, ff, e, st)); }
+      // MHSA
+      KCHK(layernorm<T>(w.x, rows, d, Lw.ln_mha_w, Lw.ln_mha_b, eps, w.h, nullptr, st));
+      if (aci) KCHK(att_cache_in<T>(aci + (size_t)l * L * 2 * d, L, 2 * d, w.kv, st));
+      { EpiArgs e; e.bias = Lw.b_qkv; e.out = w.q; e.out2 = w.kv; e.row_off = kvoff; e.d = d;
+        KCHK(gemm<T>(EPI_QKV, ACT_NONE, w.h, d, (const T*)Lw.qkv, d, rows, 3 * d, d, e, st)); }
+      if (aci && aco) KCHK(att_cache_out<T>(w.kv, cache_start, L, 2 * d, aco + (size_t)l * L * 2 * d, st));
+      KCHK(chunk_attention<T>(w.q, w.kv, kv_rows, w.P + (size_t)l * prow_pad * d, p_rows, Lw.pu, Lw.pv, attd, natt, H,
+                              w.ao, st));
+      { EpiArgs e; e.bias = Lw.b_o; e.x = w.x; e.ldx = d;
+        KCHK(gemm<T>(EPI_RESID, ACT_NONE, w.ao, d, (const T*)Lw.wo, d, rows, d, d, e, st)); }
+      // convolution module
+      KCHK(layernorm<T>(w.x, rows, d, Lw.ln_conv_w, Lw.ln_conv_b, eps, w.h, masked ? nullptr : rmask, st));
+      if (cci) KCHK(cnn_cache_in<T>(cci + (size_t)l * d * 7, d, 7, w.glu, st));
+      { EpiArgs e; e.bias = Lw.b_pw1; e.out = w.glu; e.ldo = d; e.row_off = gluoff;
+        KCHK(gemm<T>(EPI_GLU, ACT_NONE, w.h, d, (const T*)Lw.pw1, d, rows, 2 * d, d, e, st)); }
+      if (cci && cco) KCHK(cnn_cache_out<T>(w.glu, cache_start, d, 7, cco + (size_t)l * d * 7, st));
+      KCHK(conv_dw_ln_silu<T>(w.glu, convd, nconv, d, Lw.dw_t, Lw.b_dw, Lw.cn_w, Lw.cn_b, eps, w.cv, st));
+      { EpiArgs e; e.bias = Lw.b_pw2; e.x = w.x; e.ldx = d; e.rowmask = rmask;
+        KCHK(gemm<T>(EPI_RESID, ACT_NONE, w.cv, d, (const T*)Lw.pw2, d, rows, d, d, e, st)); }
+      // FFN (x 0.5)
+      KCHK(layernorm<T>(w.x, rows, d, Lw.ln_ff_w, Lw.ln_ff_b, eps, w.h, nullptr, st));
+      { EpiArgs e; e.bias = Lw.b_ff1; e.out = w.hid; e.ldo = ff;
+        KCHK(gemm<T>(EPI_STORE, ACT_SILU, w.h, d, (const T*)Lw.ff1, d, rows, ff, d, e, st)); }
+      { EpiArgs e; e.bias = Lw.b_ff2; e.x = w.x; e.ldx = d; e.alpha = 0.5f;
+        KCHK(gemm<T>(EPI_RESID, ACT_NONE, w.hid, ff, (const T*)Lw.ff2, ff, rows, d, ff, e, st)); }
+      // norm_final (+ next layer's macaron LN, or after_norm)
+      if (l + 1 < nl)
+        KCHK(layernorm2<T>(w.x, rows, d, Lw.ln_fin_w, Lw.ln_fin_b, layers[l + 1].ln_ffm_w, layers[l + 1].ln_ffm_b, eps,
+                           w.h, st));
+      else
+        KCHK(layernorm2_f32(w.x, rows, d, Lw.ln_fin_w, Lw.ln_fin_b, fe.an_w, fe.an_b, eps, out, st));
+    }
+    return CFM_OK;
+  }
+
+  cfm_status ctc(const float* enc, int rows, float* logp, int32_t* ids, void* ws, size_t wsb,
+                 hipStream_t st) const override {
+    if (!fe.ctc_w) return set_error(CFM_ERR_ASSERT, "model has no CTC head (vocab == 0)");
+    if (wsb < ctc_ws_bytes(rows)) return set_error(CFM_ERR_VALUE, "ctc workspace too small");
+    const int d = cfg.d_model, V = cfg.vocab;
+    Carver c(ws);
+    float* logits = c.take<float>((size_t)rows * V);
+    T* a = c.take<T>((size_t)rows * d);
+    const T* A;
+    if constexpr (sizeof(T) == 4) {
+      A = reinterpret_cast<const T*>(enc);
+    } else {
+      KCHK(att_cache_in<T>(enc, rows, d, a, st));   // f32 -> T row copy
+      A = a;
+    }
+    float* dst = logp ? logp : logits;
+    EpiArgs e; e.bias = fe.ctc_b; e.out = dst; e.ldo = V;
+    KCHK(gemm<T>(EPI_STORE_F32, ACT_NONE, A, d, (const T*)fe.ctc_w, d, rows, V, d, e, st));
+    KCHK(log_softmax_rows(dst, rows, V, logp ? 1 : 0, ids, st));
+    return CFM_OK;
+  }
+};
+
+// ----------------------------------------------------------------------------- weight packing
+struct HostW {
+  std::map<std::string, std::pair<const float*, int64_t>> m;
+  const float* get(const std::string& k, int64_t numel) const {
+    auto it = m.find(k);
+    if (it == m.end()) throw std::string("missing weight " + k);
+    if (it->second.second != numel)
+      throw std::string("weight " + k + ": numel " + std::to_string(it->second.second) + " != " + std::to_string(numel));
+    return it->second.first;
+  }
+  bool has(const std::string& k) const { return m.count(k) > 0; }
+};
+
+template <typename T>
+static cfm_status build_model(const cfm_config& cfg, const HostW& hw, int device, cfm_model** out) {
+  auto* M = new ModelT<T>();
+  std::unique_ptr<cfm_model> guard(M);
+  M->cfg = cfg;
+  M->device = device;
+  const int d = cfg.d_model, ff = cfg.ffn_dim, H = cfg.n_heads, nb = cfg.num_blocks, V = cfg.vocab;
+  // host staging image of the whole device block
+  struct Item { size_t off; size_t bytes; };
+  std::vector<char> img;
+  auto reserve = [&](size_t bytes) {
+    size_t off = align_up(img.size());
+    img.resize(off + align_up(bytes));
+    return off;
+  };
+  std::vector<std::pair<size_t, void**>> fix;   // (offset, pointer slot) patched after allocation
+  auto put_f32 = [&](const float* src, size_t n, float** slot) {
+    size_t off = reserve(n * 4);
+    std::memcpy(img.data() + off, src, n * 4);
+    fix.push_back({off, (void**)slot});
+  };
+  auto put_T = [&](const std::vector<float>& src, void** slot) {
+    size_t off = reserve(src.size() * sizeof(T));
+    T* p = reinterpret_cast<T*>(img.data() + off);
+    for (size_t i = 0; i < src.size(); ++i) {
+      if constexpr (sizeof(T) == 4) p[i] = src[i];
+      else {   // round-to-nearest-even f32 -> bf16 (host)
+        uint32_t u;
+        std::memcpy(&u, &src[i], 4);
+        uint16_t r;
+        if ((u & 0x7f800000u) == 0x7f800000u) r = (uint16_t)((u >> 16) | ((u & 0xffff) ? 0x40 : 0));
+        else r = (uint16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+        std::memcpy(&p[i], &r, 2);
+      }
+    }
+    fix.push_back({off, slot});
+  };
+  auto vec = [&](const std::string& k, int64_t n) { const float* s = hw.get(k, n); return std::vector<float>(s, s + n); };
+  try {
+    const std::string E = "encoder.";
+    FrontW& F = M->fe;
+    if (cfg.has_cmvn) {
+      put_f32(hw.get(E + "global_cmvn.mean", cfg.input_dim), cfg.input_dim, &F.cm);
+      put_f32(hw.get(E + "global_cmvn.istd", cfg.input_dim), cfg.input_dim, &F.ci);
+    }
+    put_f32(hw.get(E + "embed.conv.0.weight", (int64_t)d * 9), (size_t)d * 9, &F.w0);
+    put_f32(hw.get(E + "embed.conv.0.bias", d), d, &F.b0);
+    put_f32(hw.get(E + "embed.conv.2.weight", (int64_t)d * 9), (size_t)d * 9, &F.w1);
+    put_f32(hw.get(E + "embed.conv.2.bias", d), d, &F.b1);
+    put_T(vec(E + "embed.conv.3.weight", (int64_t)d * d), &F.pw1);
+    put_f32(hw.get(E + "embed.conv.3.bias", d), d, &F.b_pw1);
+    put_f32(hw.get(E + "embed.conv.5.weight", (int64_t)d * 9), (size_t)d * 9, &F.w2);
+    put_f32(hw.get(E + "embed.conv.5.bias", d), d, &F.b2);
+    put_T(vec(E + "embed.conv.6.weight", (int64_t)d * d), &F.pw2);
+    put_f32(hw.get(E + "embed.conv.6.bias", d), d, &F.b_pw2);
+    {   // out Linear columns (c*9 + f) -> channels-last (f*d + c)
+      const float* s = hw.get(E + "embed.out.weight", (int64_t)d * 9 * d);
+      std::vector<float> w((size_t)d * 9 * d);
+      for (int o = 0; o < d; ++o)
+        for (int c = 0; c < d; ++c)
+          for (int f = 0; f < 9; ++f) w[(size_t)o * 9 * d + f * d + c] = s[(size_t)o * 9 * d + c * 9 + f];
+      put_T(w, &F.wout);
+    }
+    put_f32(hw.get(E + "embed.out.bias", d), d, &F.b_out);
+    put_f32(hw.get(E + "after_norm.weight", d), d, &F.an_w);
+    put_f32(hw.get(E + "after_norm.bias", d), d, &F.an_b);
+    if (V > 0) {
+      put_T(vec("ctc.ctc_lo.weight", (int64_t)V * d), &F.ctc_w);
+      put_f32(hw.get("ctc.ctc_lo.bias", V), V, &F.ctc_b);
+    }
+    M->layers.resize(nb);
+    for (int l = 0; l < nb; ++l) {
+      LayerW& Lw = M->layers[l];
+      const std::string p = E + "encoders." + std::to_string(l) + ".";
+      put_T(vec(p + "feed_forward_macaron.w_1.weight", (int64_t)ff * d), &Lw.ff1m);
+      put_f32(hw.get(p + "feed_forward_macaron.w_1.bias", ff), ff, &Lw.b_ff1m);
+      put_T(vec(p + "feed_forward_macaron.w_2.weight", (int64_t)d * ff), &Lw.ff2m);
+      put_f32(hw.get(p + "feed_forward_macaron.w_2.bias", d), d, &Lw.b_ff2m);
+      put_T(vec(p + "feed_forward.w_1.weight", (int64_t)ff * d), &Lw.ff1);
+      put_f32(hw.get(p + "feed_forward.w_1.bias", ff), ff, &Lw.b_ff1);
+      put_T(vec(p + "feed_forward.w_2.weight", (int64_t)d * ff), &Lw.ff2);
+      put_f32(hw.get(p + "feed_forward.w_2.bias", d), d, &Lw.b_ff2);
+      {
+        std::vector<float> w, b;
+        for (const char* nm : {"linear_q", "linear_k", "linear_v"}) {
+          auto wv = vec(p + "self_attn." + nm + ".weight", (int64_t)d * d);
+          auto bv = vec(p + "self_attn." + nm + ".bias", d);
+          w.insert(w.end(), wv.begin(), wv.end());
+          b.insert(b.end(), bv.begin(), bv.end());
+        }
+        put_T(w, &Lw.qkv);
+        put_f32(b.data(), b.size(), &Lw.b_qkv);
+      }
+      put_T(vec(p + "self_attn.linear_pos.weight", (int64_t)d * d), &Lw.pos);
+      put_T(vec(p + "self_attn.linear_out.weight", (int64_t)d * d), &Lw.wo);
+      put_f32(hw.get(p + "self_attn.linear_out.bias", d), d, &Lw.b_o);
+      put_f32(hw.get(p + "self_attn.pos_bias_u", (int64_t)H * 64), (size_t)H * 64, &Lw.pu);
+      put_f32(hw.get(p + "self_attn.pos_bias_v", (int64_t)H * 64), (size_t)H * 64, &Lw.pv);
+      {   // pointwise_conv1 rows interleaved per 16: [a(16t..16t+15) | gate(d+16t..)] for the fused GLU
+        const float* s = hw.get(p + "conv_module.pointwise_conv1.weight", (int64_t)2 * d * d);
+        const float* sb = hw.get(p + "conv_module.pointwise_conv1.bias", 2 * d);
+        std::vector<float> w((size_t)2 * d * d), b(2 * d);
+        for (int t = 0; t < d / 16; ++t)
+          for (int r = 0; r < 16; ++r) {
+            const int ra = 16 * t + r, rg = d + 16 * t + r;
+            std::memcpy(&w[(size_t)(32 * t + r) * d], s + (size_t)ra * d, 4 * d);
+            std::memcpy(&w[(size_t)(32 * t + 16 + r) * d], s + (size_t)rg * d, 4 * d);
+            b[32 * t + r] = sb[ra];
+            b[32 * t + 16 + r] = sb[rg];
+          }
+        put_T(w, &Lw.pw1);
+        put_f32(b.data(), b.size(), &Lw.b_pw1);
+      }
+      {   // depthwise [d][1][15] -> tap-major [15][d]
+        const float* s = hw.get(p + "conv_module.depthwise_conv.weight", (int64_t)d * 15);
+        std::vector<float> w((size_t)15 * d);
+        for (int c = 0; c < d; ++c)
+          for (int t = 0; t < 15; ++t) w[(size_t)t * d + c] = s[c * 15 + t];
+        put_f32(w.data(), w.size(), &Lw.dw_t);
+      }
+      put_f32(hw.get(p + "conv_module.depthwise_conv.bias", d), d, &Lw.b_dw);
+      put_f32(hw.get(p + "conv_module.norm.weight", d), d, &Lw.cn_w);
+      put_f32(hw.get(p + "conv_module.norm.bias", d), d, &Lw.cn_b);
+      put_T(vec(p + "conv_module.pointwise_conv2.weight", (int64_t)d * d), &Lw.pw2);
+      put_f32(hw.get(p + "conv_module.pointwise_conv2.bias", d), d, &Lw.b_pw2);
+      const std::pair<const char*, float**> lns[] = {
+          {"norm_ff_macaron.weight", &Lw.ln_ffm_w}, {"norm_ff_macaron.bias", &Lw.ln_ffm_b},
+          {"norm_mha.weight", &Lw.ln_mha_w},        {"norm_mha.bias", &Lw.ln_mha_b},
+          {"norm_conv.weight", &Lw.ln_conv_w},      {"norm_conv.bias", &Lw.ln_conv_b},
+          {"norm_ff.weight", &Lw.ln_ff_w},          {"norm_ff.bias", &Lw.ln_ff_b},
+          {"norm_final.weight", &Lw.ln_fin_w},      {"norm_final.bias", &Lw.ln_fin_b}};
+      for (auto& kv : lns) put_f32(hw.get(p + kv.first, d), d, kv.second);
+    }
+  } catch (const std::string& e) {
+    return set_error(CFM_ERR_VALUE, e);
+  }
+  HIPC(hipSetDevice(device));
+  HIPC(hipMalloc(&M->dev_mem, img.size()));
+  HIPC(hipMemcpy(M->dev_mem, img.data(), img.size(), hipMemcpyHostToDevice));
+  for (auto& f : fix) *f.second = (char*)M->dev_mem + f.first;
+  *out = guard.release();
+  return CFM_OK;
+}
+
+}  // namespace cfm
+
+using namespace cfm;
+
+extern "C" {
+
+const char* cfm_version(void) { return "chunkformer_amd 0.1 (gfx950)"; }
+const char* cfm_last_error(void) { return g_err.c_str(); }
+
+cfm_status cfm_model_create(const cfm_config* cfg, const cfm_tensor_view* weights, int32_t n, int32_t device,
+                            cfm_model** out) {
+  if (!cfg || !out) return set_error(CFM_ERR_VALUE, "null argument");
+  *out = nullptr;
+  if (cfg->input_dim != 80) return set_error(CFM_ERR_ASSERT, "front-end kernel supports input_dim == 80");
+  if (cfg->d_model != 128 && cfg->d_model != 256 && cfg->d_model != 512)
+    return set_error(CFM_ERR_ASSERT, "d_model must be 128, 256 or 512");
+  if (cfg->n_heads <= 0 || cfg->d_model != 64 * cfg->n_heads) return set_error(CFM_ERR_ASSERT, "head_dim must be 64");
+  if (cfg->ffn_dim % 128) return set_error(CFM_ERR_ASSERT, "ffn_dim must be a multiple of 128");
+  if (cfg->kernel_size != 15) return set_error(CFM_ERR_ASSERT, "cnn_module_kernel must be 15");
+  if (cfg->num_blocks <= 0 || cfg->vocab < 0) return set_error(CFM_ERR_VALUE, "bad num_blocks / vocab");
+  HostW hw;
+  for (int i = 0; i < n; ++i) hw.m[weights[i].name] = {weights[i].data, weights[i].numel};
+  if (cfg->compute_dtype == CFM_DTYPE_F32) return build_model<float>(*cfg, hw, device, out);
+  if (cfg->compute_dtype == CFM_DTYPE_BF16) return build_model<bf16>(*cfg, hw, device, out);
+  return set_error(CFM_ERR_VALUE, "unknown compute dtype");
+}
+
+void cfm_model_destroy(cfm_model* m) { delete m; }
+
+cfm_status cfm_model_set_option(cfm_model* m, const char* key, int64_t value) {
+  if (!m || !key) return set_error(CFM_ERR_VALUE, "null argument");
+  if (!std::strcmp(key, "max_layers")) { m->max_layers = (int)value; return CFM_OK; }
+  return set_error(CFM_ERR_VALUE, std::string("unknown option ") + key);
+}
+
+size_t cfm_workspace_bytes_masked(const cfm_model* m, int32_t N, int32_t C, int32_t L, int32_t R) {
+  if (!m || N <= 0 || C <= 0) return 0;
+  int32_t h[PH_HEADER] = {0};
+  const int rows = N * C;
+  h[PH_KIND] = 1; h[PH_NWIN] = N; h[PH_ROWS] = rows; h[PH_C] = C; h[PH_L] = L; h[PH_R] = R;
+  h[PH_W] = (C - 1) * 8 + 15; h[PH_TOUT] = C; h[PH_PROWS] = L + 2 * C + R - 1;
+  h[PH_KVROWS] = L + rows + R; h[PH_GLUROWS] = rows + 14;
+  return m->ws_bytes(h);
+}
+
+size_t cfm_workspace_bytes_padded(const cfm_model* m, int32_t B, int32_t T, int32_t C, int32_t L, int32_t R) {
+  if (!m || B <= 0) return 0;
+  const int Tp = calc_length(T);
+  if (Tp <= 0) return 0;
+  if (C <= 0) { C = Tp; L = 0; R = 0; }
+  int32_t h[PH_HEADER] = {0};
+  const int rows = B * Tp;
+  h[PH_KIND] = 2; h[PH_NWIN] = B; h[PH_ROWS] = rows; h[PH_C] = C; h[PH_L] = L; h[PH_R] = R;
+  h[PH_W] = T; h[PH_TOUT] = Tp; h[PH_PROWS] = L + 2 * C + R - 1; h[PH_KVROWS] = rows; h[PH_GLUROWS] = rows;
+  return m->ws_bytes(h);
+}
+
+cfm_status cfm_encode_masked(const cfm_model* m, const float* feats, const int32_t* h, const int32_t* plan_dev,
+                             const float* aci, const float* cci, int32_t trunc, float* aco, float* cco, float* out,
+                             void* ws, size_t wsb, cfm_stream stream) {
+  if (!m || !feats || !h || !plan_dev || !out) return set_error(CFM_ERR_VALUE, "null argument");
+  if (h[PH_KIND] != 1) return set_error(CFM_ERR_VALUE, "not a masked-batch plan");
+  if ((aci == nullptr) != (cci == nullptr)) return set_error(CFM_ERR_VALUE, "att_cache and cnn_cache must be given together");
+  HIPC(hipSetDevice(m->device));
+  return m->encode(feats, plan_dev, h, aci, cci, trunc, aco, cco, out, ws, wsb, (hipStream_t)stream);
+}
+
+cfm_status cfm_encode_padded(const cfm_model* m, const float* xs, const int32_t* h, const int32_t* plan_dev, float* out,
+                             void* ws, size_t wsb, cfm_stream stream) {
+  if (!m || !xs || !h || !plan_dev || !out) return set_error(CFM_ERR_VALUE, "null argument");
+  if (h[PH_KIND] != 2) return set_error(CFM_ERR_VALUE, "not a padded-batch plan");
+  HIPC(hipSetDevice(m->device));
+  return m->encode(xs, plan_dev, h, nullptr, nullptr, 0, nullptr, nullptr, out, ws, wsb, (hipStream_t)stream);
+}
+
+cfm_status cfm_masks_from_plan(const int32_t* h, const int32_t* plan_dev, uint8_t* att, uint8_t* pad,
+                               cfm_stream stream) {
+  if (!h || !plan_dev || !att || !pad) return set_error(CFM_ERR_VALUE, "null argument");
+  if (h[PH_KIND] != 1) return set_error(CFM_ERR_VALUE, "not a masked-batch plan");
+  KCHK(masks_from_plan(plan_dev + PH_HEADER, h[PH_NWIN], h[PH_C], h[PH_L], h[PH_R], att, pad, (hipStream_t)stream));
+  return CFM_OK;
+}
+
+size_t cfm_ctc_workspace_bytes(const cfm_model* m, int32_t rows) { return m ? m->ctc_ws_bytes(rows) : 0; }
+
+cfm_status cfm_ctc_logprobs(const cfm_model* m, const float* enc, int32_t rows, float* logp, int32_t* ids, void* ws,
+                            size_t wsb, cfm_stream stream) {
+  if (!m || !enc) return set_error(CFM_ERR_VALUE, "null argument");
+  if (rows <= 0) return CFM_OK;
+  HIPC(hipSetDevice(m->device));
+  return m->ctc(enc, rows, logp, ids, ws, wsb, (hipStream_t)stream);
+}
+
+}  // extern "C"

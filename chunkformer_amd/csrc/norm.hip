@@ -1,0 +1,145 @@
+// LayerNorm kernels (pre-norm of every sub-block, norm_final, after_norm).
+//
+// Reference: nn.LayerNorm(eps=1e-5) at encoder_layer.py:46-57 and encoder.py:119.
+// One wave per row; lane l owns elements [l*VPL, l*VPL + VPL) with VPL = d/64, so
+// a row is one coalesced 16/32-B-per-lane load.  Statistics are two-pass in
+// registers (mean, then mean of squared deviations = torch's biased variance).
+// `layernorm2` fuses norm_final of layer i with the first pre-norm of layer i+1
+// (or with after_norm): the row is read once and written twice.
+#include "cfm_common.h"
+#include "cfm_kernels.h"
+
+namespace cfm {
+
+template <int VPL>
+CFM_DEV void ln_row(float (&v)[VPL], int d, const float* w, const float* b, float eps, int lane) {
+  float s = 0.f;
+#pragma unroll
+  for (int e = 0; e < VPL; ++e) s += v[e];
+  const float mean = wave_sum(s) / d;
+  float q = 0.f;
+#pragma unroll
+  for (int e = 0; e < VPL; ++e) {
+    const float t = v[e] - mean;
+    q += t * t;
+  }
+  const float rstd = rsqrtf(wave_sum(q) / d + eps);
+#pragma unroll
+  for (int e = 0; e < VPL; ++e) {
+    const int c = lane * VPL + e;
+    v[e] = (v[e] - mean) * rstd * w[c] + b[c];
+  }
+}
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef bf16 bf16x4 __attribute__((ext_vector_type(4)));
+// VPL is 2 (d=128), 4 (d=256) or 8 (d=512): vector width min(VPL, 4) elements
+template <int VPL>
+CFM_DEV void load_row(const float* p, float (&v)[VPL]) {
+  if constexpr (VPL == 2) {
+    const f32x2 t = *reinterpret_cast<const f32x2*>(p);
+    v[0] = t[0]; v[1] = t[1];
+  } else {
+#pragma unroll
+    for (int e = 0; e < VPL; e += 4) {
+      const f32x4 t = *reinterpret_cast<const f32x4*>(p + e);
+      v[e] = t[0]; v[e + 1] = t[1]; v[e + 2] = t[2]; v[e + 3] = t[3];
+    }
+  }
+}
+template <int VPL>
+CFM_DEV void store_row(float* p, const float (&v)[VPL]) {
+  if constexpr (VPL == 2) {
+    *reinterpret_cast<f32x2*>(p) = (f32x2){v[0], v[1]};
+  } else {
+#pragma unroll
+    for (int e = 0; e < VPL; e += 4) *reinterpret_cast<f32x4*>(p + e) = (f32x4){v[e], v[e + 1], v[e + 2], v[e + 3]};
+  }
+}
+template <int VPL>
+CFM_DEV void store_row(bf16* p, const float (&v)[VPL]) {
+  if constexpr (VPL == 2) {
+    *reinterpret_cast<bf16x2*>(p) = (bf16x2){(bf16)v[0], (bf16)v[1]};
+  } else {
+#pragma unroll
+    for (int e = 0; e < VPL; e += 4)
+      *reinterpret_cast<bf16x4*>(p + e) = (bf16x4){(bf16)v[e], (bf16)v[e + 1], (bf16)v[e + 2], (bf16)v[e + 3]};
+  }
+}
+
+template <typename T, int VPL>
+__global__ __launch_bounds__(256) void ln_kernel(const float* __restrict__ x, int M, const float* __restrict__ w,
+                                                 const float* __restrict__ b, float eps, T* __restrict__ out,
+                                                 const uint8_t* __restrict__ rowmask) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  constexpr int d = VPL * 64;
+  float v[VPL];
+  load_row<VPL>(x + (size_t)row * d + lane * VPL, v);
+  ln_row<VPL>(v, d, w, b, eps, lane);
+  if (rowmask && !rowmask[row]) {
+#pragma unroll
+    for (int e = 0; e < VPL; ++e) v[e] = 0.f;
+  }
+  store_row<VPL>(out + (size_t)row * d + lane * VPL, v);
+}
+
+template <typename TO, int VPL>
+__global__ __launch_bounds__(256) void ln2_kernel(float* __restrict__ x, int M, const float* __restrict__ w1,
+                                                  const float* __restrict__ b1, const float* __restrict__ w2,
+                                                  const float* __restrict__ b2, float eps, TO* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  constexpr int d = VPL * 64;
+  float v[VPL];
+  float* xp = x + (size_t)row * d + lane * VPL;
+  load_row<VPL>(xp, v);
+  ln_row<VPL>(v, d, w1, b1, eps, lane);
+  store_row<VPL>(xp, v);
+  if (w2) ln_row<VPL>(v, d, w2, b2, eps, lane);
+  store_row<VPL>(out + (size_t)row * d + lane * VPL, v);
+}
+
+template <typename T>
+int layernorm(const float* x, int M, int d, const float* w, const float* b, float eps, T* out,
+              const uint8_t* rowmask, hipStream_t st) {
+  if (M <= 0) return 0;
+  if (d == 128) hipLaunchKernelGGL((ln_kernel<T, 2>), dim3((M + 3) / 4), dim3(256), 0, st, x, M, w, b, eps, out, rowmask);
+  else if (d == 256) hipLaunchKernelGGL((ln_kernel<T, 4>), dim3((M + 3) / 4), dim3(256), 0, st, x, M, w, b, eps, out, rowmask);
+  else if (d == 512) hipLaunchKernelGGL((ln_kernel<T, 8>), dim3((M + 3) / 4), dim3(256), 0, st, x, M, w, b, eps, out, rowmask);
+  else return (int)hipErrorInvalidValue;
+  CFM_CHECK_LAUNCH();
+  return 0;
+}
+
+template <typename T>
+static int ln2_launch(float* x, int M, int d, const float* w1, const float* b1, const float* w2, const float* b2,
+                      float eps, T* out, hipStream_t st) {
+  if (M <= 0) return 0;
+  if (d == 128) hipLaunchKernelGGL((ln2_kernel<T, 2>), dim3((M + 3) / 4), dim3(256), 0, st, x, M, w1, b1, w2, b2, eps, out);
+  else if (d == 256) hipLaunchKernelGGL((ln2_kernel<T, 4>), dim3((M + 3) / 4), dim3(256), 0, st, x, M, w1, b1, w2, b2, eps, out);
+  else if (d == 512) hipLaunchKernelGGL((ln2_kernel<T, 8>), dim3((M + 3) / 4), dim3(256), 0, st, x, M, w1, b1, w2, b2, eps, out);
+  else return (int)hipErrorInvalidValue;
+  CFM_CHECK_LAUNCH();
+  return 0;
+}
+
+template <typename T>
+int layernorm2(float* x, int M, int d, const float* w1, const float* b1, const float* w2, const float* b2, float eps,
+               T* out, hipStream_t st) {
+  return ln2_launch<T>(x, M, d, w1, b1, w2, b2, eps, out, st);
+}
+int layernorm2_f32(float* x, int M, int d, const float* w1, const float* b1, const float* w2, const float* b2,
+                   float eps, float* out, hipStream_t st) {
+  return ln2_launch<float>(x, M, d, w1, b1, w2, b2, eps, out, st);
+}
+
+template int layernorm<float>(const float*, int, int, const float*, const float*, float, float*, const uint8_t*, hipStream_t);
+template int layernorm<bf16>(const float*, int, int, const float*, const float*, float, bf16*, const uint8_t*, hipStream_t);
+template int layernorm2<float>(float*, int, int, const float*, const float*, const float*, const float*, float, float*, hipStream_t);
+template int layernorm2<bf16>(float*, int, int, const float*, const float*, const float*, const float*, float, bf16*, hipStream_t);
+
+}  // namespace cfm

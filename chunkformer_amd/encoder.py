@@ -1,0 +1,208 @@
+"""Host-side mirror of the reference `ChunkFormerEncoder` (chunkformer/modules/encoder.py).
+
+Same method names, argument meaning, return tuples and error types as the
+reference; every tensor op of the hot path runs in libcfm.so (HIP, gfx950):
+
+  forward_parallel_chunk  encoder.py:503-681   -> cfm_plan_masked + cfm_encode_masked
+  forward_encoder         encoder.py:220-274   -> cfm_plan_padded + cfm_encode_padded
+  forward                 encoder.py:461-501   (eval branch: negative sizes -> 0/0/0)
+  ctc_log_softmax/argmax  ctc.py:73-91          -> cfm_ctc_logprobs
+
+Python only moves pointers: it builds the host plan (C++ planner), uploads it,
+allocates outputs/workspace with torch on the current device and launches on
+torch's current stream.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Dict, List, Optional, Tuple
+
+import torch
+
+from . import _lib
+from .config import EncoderConfig
+from .weights import check_state_dict
+
+_DTYPES = {"fp32": _lib.DTYPE_F32, "float32": _lib.DTYPE_F32, "bf16": _lib.DTYPE_BF16, "bfloat16": _lib.DTYPE_BF16}
+
+
+def calc_length(T: int) -> int:
+    """subsampling.py:270-288 (integer form)."""
+    return 1 + (int(T) - 15) // 8
+
+
+class ChunkFormerEncoder:
+    subsampling_rate = 8
+    right_context = 14
+
+    def __init__(self, cfg: EncoderConfig, state_dict: Dict[str, torch.Tensor], device=None, dtype: str = "bf16"):
+        cfg.validate()
+        check_state_dict(cfg, state_dict)
+        if not torch.cuda.is_available():
+            raise RuntimeError("chunkformer_amd needs a ROCm GPU (MI355X); there is no CPU fallback")
+        self.cfg = cfg
+        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        if dtype not in _DTYPES:
+            raise ValueError(f"dtype must be one of {list(_DTYPES)}")
+        self.dtype = "bf16" if _DTYPES[dtype] == _lib.DTYPE_BF16 else "fp32"
+        self.num_blocks = cfg.num_blocks
+        self.attention_heads = cfg.n_heads
+        self._output_size = cfg.d_model
+        self.cnn_module_kernel = cfg.kernel_size
+        c = _lib.CfmConfig(cfg.input_dim, cfg.d_model, cfg.n_heads, cfg.ffn_dim, cfg.num_blocks, cfg.kernel_size,
+                           cfg.vocab, cfg.norm_eps, int(cfg.cmvn), _DTYPES[dtype])
+        keep = []
+        views = (_lib.CfmTensorView * len(state_dict))()
+        for i, (k, v) in enumerate(state_dict.items()):
+            t = v.detach().to("cpu", torch.float32).contiguous()
+            keep.append(t)
+            views[i] = _lib.CfmTensorView(k.encode(), t.data_ptr(), t.numel())
+        h = ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            _lib.check(_lib.cfm_model_create(ctypes.byref(c), views, len(state_dict), self.device.index or 0,
+                                             ctypes.byref(h)))
+        self._h = h
+        self._ws: Optional[torch.Tensor] = None
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            _lib.cfm_model_destroy(h)
+            self._h = None
+
+    def output_size(self) -> int:
+        return self._output_size
+
+    def set_option(self, key: str, value: int) -> None:
+        _lib.check(_lib.cfm_model_set_option(self._h, key.encode(), int(value)))
+
+    # ------------------------------------------------------------------ helpers
+    def _workspace(self, nbytes: int) -> torch.Tensor:
+        if self._ws is None or self._ws.numel() < nbytes:
+            self._ws = None
+            self._ws = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
+        return self._ws
+
+    def _stream(self) -> int:
+        return torch.cuda.current_stream(self.device).cuda_stream
+
+    def _upload(self, plan: torch.Tensor) -> torch.Tensor:
+        return plan.pin_memory().to(self.device, non_blocking=True)
+
+    # ------------------------------------------------------------------ masked batch
+    @torch.no_grad()
+    def forward_parallel_chunk(self, xs, xs_origin_lens, chunk_size: int = -1, left_context_size: int = -1,
+                               right_context_size: int = -1, att_cache: torch.Tensor = torch.zeros((0, 0, 0)),
+                               cnn_cache: torch.Tensor = torch.zeros((0, 0)), truncated_context_size: int = 0,
+                               offset: torch.Tensor = torch.zeros(0)):
+        """encoder.py:503-681.  Returns (xs [N, C, d], xs_lens [B] int32, n_chunks, r_att_cache,
+        r_cnn_cache, offset); `offset` is updated in place (+= xs_lens) like the reference."""
+        B = len(xs)
+        C, L, R = int(chunk_size), int(left_context_size), int(right_context_size)
+        dev = self.device
+        if offset.shape[0] == 0:
+            offset = torch.zeros(B, dtype=torch.long, device=xs_origin_lens.device)
+        lens = [int(t) for t in xs_origin_lens.tolist()]
+        offs = [int(o) for o in offset.tolist()]
+        plan, n_chunks, out_lens = _lib.plan_masked(lens, offs, C, L, R)
+        N = sum(n_chunks)
+        d = self.cfg.d_model
+        feats = torch.cat([x.to(dev, torch.float32).reshape(-1, self.cfg.input_dim)[: int(t)]
+                           for x, t in zip(xs, lens)], 0).contiguous()
+        if feats.shape[0] == 0:
+            feats = torch.zeros(1, self.cfg.input_dim, device=dev)
+        plan_dev = self._upload(plan)
+        out = torch.empty(N * C, d, dtype=torch.float32, device=dev)
+        has_cache = att_cache.size(0) > 0
+        aci = cci = aco = cco = None
+        if has_cache:
+            nb = self.num_blocks
+            aci = att_cache.to(dev, torch.float32).contiguous()
+            cci = cnn_cache.to(dev, torch.float32).contiguous()
+            if tuple(aci.shape) != (nb, L, self.cfg.n_heads, 2 * self.cfg.head_dim):
+                raise ValueError(f"att_cache shape {tuple(aci.shape)} != {(nb, L, self.cfg.n_heads, 2 * self.cfg.head_dim)}")
+            if tuple(cci.shape) != (nb, d, self.cfg.conv_lorder):
+                raise ValueError(f"cnn_cache shape {tuple(cci.shape)} != {(nb, d, self.cfg.conv_lorder)}")
+            aco = torch.empty_like(aci)
+            cco = torch.empty_like(cci)
+        ws_bytes = _lib.cfm_workspace_bytes_masked(self._h, N, C, L, R)
+        ws = self._workspace(ws_bytes)
+        _lib.check(_lib.cfm_encode_masked(self._h, feats.data_ptr(), plan.data_ptr(), plan_dev.data_ptr(),
+                                          _lib.ptr(aci), _lib.ptr(cci), int(truncated_context_size), _lib.ptr(aco),
+                                          _lib.ptr(cco), out.data_ptr(), ws.data_ptr(), ws_bytes, self._stream()))
+        xs_lens = torch.tensor(out_lens, dtype=torch.int32, device=xs_origin_lens.device)
+        offset += xs_lens.to(offset.device)
+        if has_cache:
+            r_att, r_cnn = aco, cco
+        else:
+            r_att = torch.zeros(self.num_blocks, 0, 0, 0, device=dev)
+            r_cnn = torch.zeros(self.num_blocks, 0, 0, device=dev)
+        self._last_plan = (plan, plan_dev)   # keep the uploaded plan alive until the stream consumed it
+        return out.view(N, C, d), xs_lens, n_chunks, r_att, r_cnn, offset
+
+    @torch.no_grad()
+    def masks(self, xs_origin_lens, chunk_size: int, left_context_size: int, right_context_size: int,
+              offset: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+        """att_mask [N,1,L+C+R] and mask_pad [N,1,C+14] exactly as encoder.py:627-645 builds them."""
+        lens = [int(t) for t in xs_origin_lens.tolist()]
+        offs = [0] * len(lens) if offset is None or offset.shape[0] == 0 else [int(o) for o in offset.tolist()]
+        C, L, R = chunk_size, left_context_size, right_context_size
+        plan, n_chunks, _ = _lib.plan_masked(lens, offs, C, L, R)
+        N = sum(n_chunks)
+        plan_dev = self._upload(plan)
+        att = torch.empty(N, L + C + R, dtype=torch.uint8, device=self.device)
+        pad = torch.empty(N, C + 14, dtype=torch.uint8, device=self.device)
+        _lib.check(_lib.cfm_masks_from_plan(plan.data_ptr(), plan_dev.data_ptr(), att.data_ptr(), pad.data_ptr(),
+                                            self._stream()))
+        torch.cuda.current_stream(self.device).synchronize()
+        return att.bool().unsqueeze(1), pad.bool().unsqueeze(1)
+
+    # ------------------------------------------------------------------ padded batch
+    @torch.no_grad()
+    def forward_encoder(self, xs: torch.Tensor, xs_lens: torch.Tensor, chunk_size: int = 0,
+                        left_context_size: int = 0, right_context_size: int = 0):
+        """encoder.py:220-274: padded [B, T, 80] -> ([B, T', d], masks [B, 1, T'] bool)."""
+        B, T, F = xs.shape
+        if F != self.cfg.input_dim:
+            raise RuntimeError(f"expected {self.cfg.input_dim} input features, got {F}")
+        lens = [int(t) for t in xs_lens.tolist()]
+        plan, Tp = _lib.plan_padded(lens, T, int(chunk_size), int(left_context_size), int(right_context_size))
+        dev = self.device
+        x = xs.to(dev, torch.float32).contiguous()
+        plan_dev = self._upload(plan)
+        out = torch.empty(B, Tp, self.cfg.d_model, dtype=torch.float32, device=dev)
+        ws_bytes = _lib.cfm_workspace_bytes_padded(self._h, B, T, int(chunk_size), int(left_context_size),
+                                                   int(right_context_size))
+        ws = self._workspace(ws_bytes)
+        _lib.check(_lib.cfm_encode_padded(self._h, x.data_ptr(), plan.data_ptr(), plan_dev.data_ptr(), out.data_ptr(),
+                                          ws.data_ptr(), ws_bytes, self._stream()))
+        self._last_plan = (plan, plan_dev)
+        sub = torch.tensor([calc_length(t) for t in lens], device=dev)
+        masks = (torch.arange(Tp, device=dev)[None, :] < sub[:, None]).unsqueeze(1)
+        return out, masks
+
+    def forward(self, xs, xs_lens, chunk_size: int = 0, left_context_size: int = -1, right_context_size: int = -1,
+                **kwargs):
+        """encoder.py:461-501 (eval branch)."""
+        if chunk_size < 0 or left_context_size < 0 or right_context_size < 0:
+            chunk_size, left_context_size, right_context_size = 0, 0, 0
+        return self.forward_encoder(xs, xs_lens, chunk_size, left_context_size, right_context_size)
+
+    __call__ = forward
+
+    # ------------------------------------------------------------------ CTC head
+    @torch.no_grad()
+    def ctc_log_softmax(self, hs: torch.Tensor, want_logp: bool = True, want_ids: bool = True):
+        """ctc.py:73-81 log_softmax(ctc_lo(hs)) and its argmax over the vocabulary (int32)."""
+        if self.cfg.vocab <= 0:
+            raise AssertionError("model has no CTC head")
+        shape = hs.shape[:-1]
+        enc = hs.reshape(-1, self.cfg.d_model).to(self.device, torch.float32).contiguous()
+        rows = enc.shape[0]
+        logp = torch.empty(rows, self.cfg.vocab, dtype=torch.float32, device=self.device) if want_logp else None
+        ids = torch.empty(rows, dtype=torch.int32, device=self.device) if want_ids else None
+        nbytes = _lib.cfm_ctc_workspace_bytes(self._h, rows)
+        ws = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
+        _lib.check(_lib.cfm_ctc_logprobs(self._h, enc.data_ptr(), rows, _lib.ptr(logp), _lib.ptr(ids), ws.data_ptr(),
+                                         nbytes, self._stream()))
+        return (logp.view(*shape, -1) if logp is not None else None), (ids.view(*shape) if ids is not None else None)

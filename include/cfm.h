@@ -1,0 +1,138 @@
+/*
+ * cfm.h — C-ABI of the MI355X-native ChunkFormer encoder hot path (libcfm.so).
+ *
+ * Drop-in boundary for the reference's `ChunkFormerEncoder` method set
+ * (ishine/chunkformer, chunkformer/modules/encoder.py).  The reference has no
+ * FFI of its own: it is plain Python method calls on nn.Modules, so each entry
+ * point below names the reference method it replaces; the Python mirror
+ * (chunkformer_amd/encoder.py) binds them with ctypes exactly as the
+ * reference's callers call the module.
+ *
+ * Conventions
+ *   - every pointer named *_dev / buffer argument is DEVICE memory owned by the
+ *     caller (torch tensors in the Python mirror); host arrays are named *_host
+ *     or documented as host;
+ *   - all device work is stream-ordered on `stream` (a hipStream_t);
+ *   - cfm_encode_* and cfm_ctc_* perform no allocation and no host
+ *     synchronisation, so they can be captured into a HIP graph;
+ *   - one model handle per device, one host thread per device (one
+ *     torch.distributed rank per GPU);
+ *   - status codes map to the reference's exception types:
+ *       CFM_ERR_VALUE   -> ValueError      (bad argument / size)
+ *       CFM_ERR_ASSERT  -> AssertionError  (unsupported configuration, encoder.py:94-96,116)
+ *       CFM_ERR_RUNTIME -> RuntimeError    (HIP failure, shape mismatch)
+ *     cfm_last_error() returns the thread-local message of the last failure.
+ */
+#ifndef CFM_H
+#define CFM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum { CFM_OK = 0, CFM_ERR_VALUE = 1, CFM_ERR_ASSERT = 2, CFM_ERR_RUNTIME = 3 } cfm_status;
+typedef enum { CFM_DTYPE_F32 = 0, CFM_DTYPE_BF16 = 1 } cfm_dtype;
+
+/* encoder_conf subset (encoder.py:36-70) + CTC output_dim (init_model.py:73) */
+typedef struct {
+  int32_t input_dim;      /* 80 */
+  int32_t d_model;        /* output_size: 128, 256 or 512 */
+  int32_t n_heads;        /* attention_heads (head dim must be 64) */
+  int32_t ffn_dim;        /* linear_units */
+  int32_t num_blocks;
+  int32_t kernel_size;    /* cnn_module_kernel (15) */
+  int32_t vocab;          /* CTC output_dim, 0 = no CTC head */
+  float norm_eps;         /* 1e-5 */
+  int32_t has_cmvn;       /* global_cmvn present */
+  int32_t compute_dtype;  /* cfm_dtype: F32 = exact-f32 MFMA parity mode, BF16 = bf16 MFMA, f32 accumulate */
+} cfm_config;
+
+/* one state_dict tensor, by reference key name, host f32 contiguous */
+typedef struct {
+  const char* name;
+  const float* data;
+  int64_t numel;
+} cfm_tensor_view;
+
+typedef struct cfm_model cfm_model;
+typedef void* cfm_stream; /* hipStream_t */
+
+const char* cfm_version(void);
+const char* cfm_last_error(void);
+
+/* Build a model on `device` from reference state_dict tensors (replaces
+ * init_speech_model + load_checkpoint for the encoder, init_model.py:61-145,
+ * checkpoint.py:26-41).  Weights are repacked into device layouts owned by the
+ * handle.  Missing / mis-shaped keys -> CFM_ERR_VALUE. */
+cfm_status cfm_model_create(const cfm_config* cfg, const cfm_tensor_view* weights, int32_t n_weights,
+                            int32_t device, cfm_model** out);
+void cfm_model_destroy(cfm_model* m);
+/* test/diagnostic knobs: "max_layers" (run only the first N blocks, -1 = all) */
+cfm_status cfm_model_set_option(cfm_model* m, const char* key, int64_t value);
+
+/* ------------------------------------------------------------------ plans
+ * A plan is an int32 blob computed on the HOST (no GPU needed) and uploaded by
+ * the caller; it carries the packer's integer work (chunk windows, masks as
+ * [lo, hi) ranges, kernel block descriptors, per-row validity).
+ *
+ * cfm_plan_masked: the masked-batch packer of forward_parallel_chunk
+ * (encoder.py:534-604 + masks 625-645), bit-exact.  Per utterance: lens[b]
+ * fbank frames, offsets[b] carried offset (encoder.py:565-594).  Outputs
+ * n_chunks[b], out_lens[b] = calc_length(lens[b]) (subsampling.py:270-288),
+ * *total_chunks.  Call with plan == NULL to get *plan_ints, then again with a
+ * buffer of that many int32. */
+cfm_status cfm_plan_masked(const int32_t* lens_host, const int32_t* offsets_host, int32_t B, int32_t chunk_size,
+                           int32_t left_context, int32_t right_context, int32_t* n_chunks_host,
+                           int32_t* out_lens_host, int32_t* total_chunks, int32_t* plan_host, int64_t* plan_ints);
+
+/* cfm_plan_padded: padded-batch geometry of forward_encoder (encoder.py:220-274,
+ * attention.py:334-386, convolution.py:148-167).  chunk_size <= 0 -> full
+ * attention.  *t_out = calc_length(T). */
+cfm_status cfm_plan_padded(const int32_t* lens_host, int32_t B, int32_t T, int32_t chunk_size, int32_t left_context,
+                           int32_t right_context, int32_t* t_out, int32_t* plan_host, int64_t* plan_ints);
+
+/* ------------------------------------------------------------------ encoder
+ * cfm_encode_masked replaces ChunkFormerEncoder.forward_parallel_chunk
+ * (encoder.py:503-681).  feats_dev: the B utterances' fbank concatenated
+ * [sum T_b, 80] f32.  att_cache_in / cnn_cache_in: [nb, L, H, 2*dk] / [nb, d, 7]
+ * f32 or NULL (no cache: zeros, and no new cache is produced).  With caches,
+ * the new caches (attention.py:466-467, convolution.py:228-230) are written to
+ * att_cache_out / cnn_cache_out (may alias the inputs).  out_dev: [N*C, d] f32
+ * after after_norm.  workspace: cfm_workspace_bytes_masked() bytes.  plan_host is the
+ * host copy of the plan (only its header is read: launch geometry), plan_dev the
+ * same blob in device memory (read by the kernels). */
+size_t cfm_workspace_bytes_masked(const cfm_model* m, int32_t total_chunks, int32_t chunk_size, int32_t left_context,
+                                  int32_t right_context);
+cfm_status cfm_encode_masked(const cfm_model* m, const float* feats_dev, const int32_t* plan_host,
+                             const int32_t* plan_dev, const float* att_cache_in, const float* cnn_cache_in, int32_t truncated_context_size,
+                             float* att_cache_out, float* cnn_cache_out, float* out_dev, void* workspace,
+                             size_t workspace_bytes, cfm_stream stream);
+
+/* cfm_encode_padded replaces ChunkFormerEncoder.forward_encoder (encoder.py:220-274)
+ * and therefore ChunkFormerModel.encode (chunkformer_model.py:256-274).
+ * xs_dev: [B, T, 80] f32 padded batch; out_dev: [B, T', d] f32. */
+size_t cfm_workspace_bytes_padded(const cfm_model* m, int32_t B, int32_t T, int32_t chunk_size, int32_t left_context,
+                                  int32_t right_context);
+cfm_status cfm_encode_padded(const cfm_model* m, const float* xs_dev, const int32_t* plan_host, const int32_t* plan_dev,
+                             float* out_dev, void* workspace, size_t workspace_bytes, cfm_stream stream);
+
+/* Materialise att_mask [N, L+C+R] and mask_pad [N, C+14] (0/1 bytes) of a masked
+ * plan: the exact tensors encoder.py:627-645 builds. */
+cfm_status cfm_masks_from_plan(const int32_t* plan_host, const int32_t* plan_dev, uint8_t* att_mask_dev,
+                               uint8_t* mask_pad_dev, cfm_stream stream);
+
+/* ------------------------------------------------------------------ CTC head
+ * CTC.log_softmax (ctc.py:73-81) + argmax (chunkformer_model.py:437-438, 526-527)
+ * over enc_dev [rows, d].  logp_dev [rows, V] may be NULL (ids only: logits go to
+ * the workspace); ids_dev [rows] int32 may be NULL. */
+size_t cfm_ctc_workspace_bytes(const cfm_model* m, int32_t rows);
+cfm_status cfm_ctc_logprobs(const cfm_model* m, const float* enc_dev, int32_t rows, float* logp_dev, int32_t* ids_dev,
+                            void* workspace, size_t workspace_bytes, cfm_stream stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CFM_H */

@@ -1,0 +1,161 @@
+"""GPU parity: libcfm.so (HIP, gfx950) against the reference-generated golden fixtures
+and the oracle, through the C-ABI (chunkformer_amd.encoder mirror).
+
+Tolerances:
+  masks / n_chunks / lens : bit-exact
+  fp32 mode               : max-abs <= FP32_ATOL on encoder output and CTC log-probs
+  bf16 mode               : rel-L2 <= 2e-2 and CTC argmax agreement >= 99%
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+FP32_ATOL = 1e-4
+BF16_RELL2 = 2e-2
+
+
+def _rel_l2(a, b):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))
+
+
+@pytest.fixture(scope="module")
+def cfm():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import chunkformer_amd.encoder as enc
+    return enc
+
+
+@pytest.fixture(scope="module")
+def small_g(golden_dir):
+    return np.load(os.path.join(golden_dir, "small.npz"))
+
+
+@pytest.fixture(scope="module")
+def small_models(cfm, small_g):
+    from chunkformer_amd.config import SMALL
+    from chunkformer_amd.weights import synthetic_state_dict
+    sd = synthetic_state_dict(SMALL, int(small_g["seed"]))
+    return {dt: cfm.ChunkFormerEncoder(SMALL, sd, dtype=dt) for dt in ("fp32", "bf16")}
+
+
+def test_masks_bit_exact(cfm, small_models, golden_dir):
+    g = np.load(os.path.join(golden_dir, "masks.npz"))
+    enc = small_models["fp32"]
+    for i in range(int(g["n_cases"])):
+        C, L, R = (int(v) for v in g[f"c{i}_clr"])
+        lens = torch.from_numpy(g[f"c{i}_lens"])
+        offs = torch.from_numpy(g[f"c{i}_offs"].astype(np.int64))
+        att, pad = enc.masks(lens, C, L, R, offs)
+        sa, sp = g[f"c{i}_att_shape"], g[f"c{i}_pad_shape"]
+        exp_att = np.unpackbits(g[f"c{i}_att"], axis=-1, count=int(sa[1])).astype(bool)
+        exp_pad = np.unpackbits(g[f"c{i}_pad"], axis=-1, count=int(sp[1])).astype(bool)
+        np.testing.assert_array_equal(att[:, 0].cpu().numpy(), exp_att, err_msg=f"case {i}")
+        np.testing.assert_array_equal(pad[:, 0].cpu().numpy(), exp_pad, err_msg=f"case {i}")
+
+
+@pytest.mark.parametrize("case", ["a", "b", "c", "d"])
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_masked_batch(cfm, small_models, small_g, case, dtype):
+    from chunkformer_amd.weights import synthetic_features
+    g = small_g
+    enc = small_models[dtype]
+    lens = g[f"{case}_lens"].tolist()
+    C, L, R = (int(v) for v in g[f"{case}_clr"])
+    xs = synthetic_features(lens, int(g[f"{case}_seed"]))
+    out, olens, nch, ra, rc, off = enc.forward_parallel_chunk(xs, torch.tensor(lens, dtype=torch.int32), C, L, R)
+    assert nch == g[f"{case}_nchunks"].tolist()
+    assert olens.tolist() == g[f"{case}_outlens"].tolist()
+    assert off.tolist() == g[f"{case}_outlens"].tolist()
+    assert tuple(ra.shape) == (2, 0, 0, 0) and tuple(rc.shape) == (2, 0, 0)
+    o = out.cpu().numpy()
+    exp = g[f"{case}_out"]
+    assert np.isfinite(o).all()
+    if dtype == "fp32":
+        np.testing.assert_allclose(o, exp, atol=FP32_ATOL, rtol=0)
+    else:
+        assert _rel_l2(o, exp) <= BF16_RELL2
+    if case == "a":
+        logp, ids = enc.ctc_log_softmax(out)
+        lp = logp.cpu().numpy()
+        if dtype == "fp32":
+            np.testing.assert_allclose(lp, g["a_logp"], atol=FP32_ATOL * 5, rtol=0)
+        agree = (ids.cpu().numpy() == g["a_logp"].argmax(-1)).mean()
+        assert agree >= (0.999 if dtype == "fp32" else 0.99)
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_cache_path(cfm, small_models, small_g, dtype):
+    from chunkformer_amd.weights import synthetic_features
+    g = small_g
+    enc = small_models[dtype]
+    xs = synthetic_features([900], int(g["cache_seed"]))
+    off = torch.tensor([5], dtype=torch.int32)
+    out, _, _, ac, cc, off2 = enc.forward_parallel_chunk(
+        xs, torch.tensor([900], dtype=torch.int32), 16, 32, 32, torch.from_numpy(g["cache_att_in"]),
+        torch.from_numpy(g["cache_cnn_in"]), 48, off)
+    assert off2.tolist() == g["cache_offset_out"].tolist()
+    for got, exp in ((out, g["cache_out"]), (ac, g["cache_att_out"]), (cc, g["cache_cnn_out"])):
+        got = got.cpu().numpy()
+        if dtype == "fp32":
+            np.testing.assert_allclose(got, exp, atol=FP32_ATOL, rtol=0)
+        else:
+            assert _rel_l2(got, exp) <= BF16_RELL2
+
+
+@pytest.mark.parametrize("case", ["pc", "pf"])
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_padded_path(cfm, small_models, small_g, case, dtype):
+    from chunkformer_amd.weights import synthetic_features
+    g = small_g
+    enc = small_models[dtype]
+    lens = g[f"{case}_lens"].tolist()
+    C, L, R = (int(v) for v in g[f"{case}_clr"])
+    xs = synthetic_features(lens, int(g[f"{case}_seed"]))
+    xp = torch.zeros(len(lens), max(lens), 80)
+    for i, t in enumerate(xs):
+        xp[i, : t.shape[0]] = t
+    out, masks = enc.forward_encoder(xp, torch.tensor(lens), C, L, R)
+    np.testing.assert_array_equal(masks.cpu().numpy(), g[f"{case}_mask"])
+    o = out.cpu().numpy()
+    if dtype == "fp32":
+        np.testing.assert_allclose(o, g[f"{case}_out"], atol=FP32_ATOL, rtol=0)
+    else:
+        assert _rel_l2(o, g[f"{case}_out"]) <= BF16_RELL2
+
+
+@pytest.fixture(scope="module")
+def large(cfm, golden_dir):
+    from chunkformer_amd.config import LARGE
+    from chunkformer_amd.weights import synthetic_state_dict
+    g = np.load(os.path.join(golden_dir, "large.npz"))
+    sd = synthetic_state_dict(LARGE, int(g["seed"]))
+    return g, {dt: cfm.ChunkFormerEncoder(LARGE, sd, dtype=dt) for dt in ("fp32", "bf16")}
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_large_12L(cfm, large, dtype):
+    from chunkformer_amd.weights import synthetic_features
+    g, models = large
+    enc = models[dtype]
+    lens = g["lens"].tolist()
+    xs = synthetic_features(lens, int(g["feat_seed"]))
+    out, olens, nch, _, _, _ = enc.forward_parallel_chunk(xs, torch.tensor(lens, dtype=torch.int32), 64, 128, 128)
+    assert nch == g["nchunks"].tolist()
+    o = out.cpu().numpy()
+    _, ids = enc.ctc_log_softmax(out, want_logp=False)
+    ids = ids.cpu().numpy()
+    margin = g["top2"][..., 0] - g["top2"][..., 1]
+    if dtype == "fp32":
+        np.testing.assert_allclose(o, g["out"], atol=FP32_ATOL * 5, rtol=0)
+        sure = margin > 1e-3
+        np.testing.assert_array_equal(ids[sure], g["ids"][sure])
+    else:
+        assert _rel_l2(o, g["out"]) <= BF16_RELL2
+        assert (ids == g["ids"]).mean() >= 0.99
