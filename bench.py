@@ -1,0 +1,225 @@
+"""Benchmark: audio-frames/s through the ChunkFormer encoder (masked batch) on MI355X.
+
+    python bench.py --gpus N --steps K --warmup W            (N>1: launched by torch.distributed.run)
+
+Workload (BASELINE.json configs[1]): chunkformer-large (12 layers, d=512,
+8 heads, ff=2048, conv k=15, V=5000) with seeded synthetic weights, a 240-min masked
+batch PER GPU of synthetic N(0,1) 80-dim fbank: utterance lengths log-uniform in
+[1 s, 30 min] from torch.Generator seed 0 (B=70, N=2,845 chunks at one GPU),
+chunk 64 / left 128 / right 128.  For N GPUs the generator draws N x 240 min and the
+utterances are LPT-sharded over the ranks by chunk count (no data-path collective:
+weak scaling); after timing, CTC ids are all-gathered over RCCL and timed separately.
+
+A step = ChunkFormerEncoder.forward_parallel_chunk over the rank's whole batch:
+host packer (C++ planner) + plan upload + front-end + 12 blocks + after_norm, with
+the features already resident in HBM.  value = all ranks' fbank frames / max-over-
+ranks step time.
+
+roofline: the dominant kernel is the FFN w_1 GEMM ([64N, 512] x [512, 2048], bf16
+MFMA); its per-launch time is measured live with HIP events on the launch stream
+(libcfm in-stream profiler) over the timed steps.  cpu_baseline: the CPU oracle
+(oracle/encoder_ref.py, torch fp32) on a bounded sample of the same workload.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from chunkformer_amd import _lib  # noqa: E402
+from chunkformer_amd.config import LARGE  # noqa: E402
+from chunkformer_amd.distributed import chunks_of, gather_ids, init_from_env, lpt_shard  # noqa: E402
+from chunkformer_amd.encoder import ChunkFormerEncoder  # noqa: E402
+from chunkformer_amd.weights import synthetic_state_dict  # noqa: E402
+
+METRIC = "audio-frames/sec (80-dim fbank) through encoder, chunkformer-large chunk=64, 1/2/4/8 GPU"
+PEAK_TFLOPS = {"bf16": 2500.0, "fp32": 157.3}   # MI355X dense MFMA peaks (MI355X_MICROARCH.md)
+C, L, R = 64, 128, 128
+
+
+def workload_lengths(total_frames: int, seed: int = 0):
+    """SURVEY §8d generator: log-uniform 1 s .. 30 min until the target is reached."""
+    g = torch.Generator().manual_seed(seed)
+    lens, tot = [], 0
+    lo, hi = math.log(100), math.log(180000)
+    while tot < total_frames:
+        T = int(math.exp(lo + float(torch.rand(1, generator=g)) * (hi - lo)))
+        T = min(T, total_frames - tot)
+        lens.append(T)
+        tot += T
+    return lens
+
+
+def flops_per_chunk(cfg) -> float:
+    """Algorithmic FLOPs of one 64-frame chunk."""
+    d, ff, k = cfg.d_model, cfg.ffn_dim, cfg.kernel_size
+    front = 2 * (d * (4 * C + 3) * 39 * 9 + d * (2 * C + 1) * 19 * 9 + d * d * (2 * C + 1) * 19 + d * C * 9 * 9
+                 + d * d * C * 9 + C * 9 * d * d)
+    layer = 2 * (2 * 2 * C * d * ff + 4 * C * d * d + 2 * C * d * d + C * d * d + C * d * k
+                 + C * d * (L + C + R) + C * d * (L + 2 * C + R - 1) + C * d * (L + C + R))
+    return front + cfg.num_blocks * layer
+
+
+def cpu_baseline(lens_all, budget_s: float = 12.0):
+    """Time the CPU oracle (torch fp32) on consecutive utterance groups until the budget."""
+    from chunkformer_amd.weights import synthetic_features
+    from oracle import encoder_ref as ref
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    sd = synthetic_state_dict(LARGE, 0)
+    frames, t_tot, groups, i = 0, 0.0, 0, 0
+    while t_tot < budget_s and i < len(lens_all):
+        grp = []
+        while i < len(lens_all) and sum(grp) < 30000:
+            grp.append(min(lens_all[i], 60000))
+            i += 1
+        xs = synthetic_features(grp, 1000 + groups)
+        t0 = time.perf_counter()
+        ref.forward_parallel_chunk(sd, LARGE, xs, grp, C, L, R)
+        t_tot += time.perf_counter() - t0
+        frames += sum(grp)
+        groups += 1
+    return {"value": round(frames / t_tot, 1), "unit": "audio-frames/s", "cores": threads, "kind": "port",
+            "sample": f"{groups} masked-batch calls of the oracle (oracle/encoder_ref.py, torch fp32 CPU) over the "
+                      f"workload's first utterances (capped at 60k frames each), {frames} frames in {t_tot:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--minutes", type=float, default=240.0, help="audio minutes per GPU")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-breakdown", action="store_true")
+    args = ap.parse_args()
+
+    rank, world, local = init_from_env()
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    per_gpu = int(args.minutes * 60 * 100)
+    lens_all = workload_lengths(per_gpu * world, seed=0)
+    shards = lpt_shard(lens_all, world, C) if world > 1 else [list(range(len(lens_all)))]
+    mine = shards[rank]
+    lens = [lens_all[i] for i in mine]
+    g = torch.Generator(device=dev).manual_seed(1234 + rank)
+    xs = [torch.randn(t, 80, generator=g, device=dev) for t in lens]
+    xs_lens = torch.tensor(lens, dtype=torch.int32)
+    n_chunks = sum(chunks_of(t, C) for t in lens)
+
+    enc = ChunkFormerEncoder(LARGE, synthetic_state_dict(LARGE, 0), device=dev, dtype=args.dtype)
+
+    def step():
+        return enc.forward_parallel_chunk(xs, xs_lens, C, L, R)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    ffn1_bit = 1 << _lib.PROFILE_CLASSES.index("ffn_w1_gemm")
+    enc.set_option("profile_reset", 1)
+    enc.set_option("profile", ffn1_bit)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    enc.set_option("profile", 0)
+    prof = _lib.profile_read(enc._h)
+    t = torch.tensor([dt], dtype=torch.float64, device=dev)
+    frames = torch.tensor([float(sum(lens))], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dist.all_reduce(frames, op=dist.ReduceOp.SUM)
+    dt_max = float(t.item())
+    total_frames = float(frames.item())
+    value = total_frames * args.steps / dt_max
+
+    # ---- dominant kernel: FFN w_1 GEMM, per-launch time from in-stream HIP events
+    ms1, n1 = prof["ffn_w1_gemm"]
+    rows = n_chunks * C
+    fl_launch = 2.0 * rows * LARGE.ffn_dim * LARGE.d_model
+    avg_s = (ms1 / max(n1, 1)) / 1e3
+    achieved = fl_launch / avg_s / 1e12 if n1 else None
+    peak = PEAK_TFLOPS[args.dtype]
+    step_flops = n_chunks * flops_per_chunk(LARGE) + LARGE.num_blocks * 2 * (L + 2 * C + R - 1) * LARGE.d_model ** 2
+
+    # ---- CTC head + the one collective (timed separately; not part of `value`)
+    enc_out = out[0]
+    torch.cuda.synchronize()
+    tc = time.perf_counter()
+    _, ids = enc.ctc_log_softmax(enc_out, want_logp=False)
+    torch.cuda.synchronize()
+    ctc_ms = (time.perf_counter() - tc) * 1e3
+    gather_ms = None
+    if world > 1:
+        out_lens = [max(0, int(v)) for v in out[1].tolist()]
+        segs = ids.view(-1, C).split(out[2], 0)
+        flat = torch.cat([s.reshape(-1)[:ol] for s, ol in zip(segs, out_lens)])
+        dist.barrier()
+        torch.cuda.synchronize()
+        tg = time.perf_counter()
+        gather_ids(flat, out_lens, shards)
+        torch.cuda.synchronize()
+        gather_ms = (time.perf_counter() - tg) * 1e3
+
+    breakdown = None
+    if not args.no_breakdown:
+        enc.set_option("profile_reset", 1)
+        enc.set_option("profile", (1 << len(_lib.PROFILE_CLASSES)) - 1)
+        step()
+        torch.cuda.synchronize()
+        enc.set_option("profile", 0)
+        breakdown = {k: round(v[0], 3) for k, v in _lib.profile_read(enc._h).items() if v[1]}
+
+    if rank == 0:
+        res = {
+            "metric": METRIC,
+            "value": round(value, 1),
+            "unit": "audio-frames/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(dt_max / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": args.dtype,
+            "data": "synthetic (N(0,1) 80-dim fbank, seeded random chunkformer-large weights; no checkpoint offline)",
+            "config": {"workload": f"masked batch, {args.minutes:g} min of audio per GPU (log-uniform 1 s-30 min "
+                                   f"utterances, seed 0), forward_parallel_chunk C=64 L=128 R=128",
+                       "utterances_rank0": len(lens), "chunks_rank0": n_chunks, "frames_total": int(total_frames),
+                       "parallelism": f"dp{world} (LPT utterance sharding)"},
+            "roofline": {"bound": "mfma", "kernel": "ffn_w1_gemm (gemm_kernel<bf16,EPI_STORE,SiLU>)"
+                         if args.dtype == "bf16" else "ffn_w1_gemm (gemm_kernel<float,EPI_STORE,SiLU>)",
+                         "achieved": round(achieved, 1) if achieved else None, "peak": peak, "unit": "TFLOP/s",
+                         "frac": round(achieved / peak, 4) if achieved else None, "traffic": None,
+                         "flops_per_launch": fl_launch, "avg_launch_ms": round(avg_s * 1e3, 4), "launches": n1},
+            "step_tflops_algorithmic": round(step_flops / (dt_max / args.steps) / 1e12, 1),
+            "ctc_ms": round(ctc_ms, 3),
+            "allgather_ids_ms": round(gather_ms, 3) if gather_ms is not None else None,
+            "breakdown_ms": breakdown,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            res["cpu_baseline"] = cpu_baseline(lens_all)
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -65,13 +65,29 @@ cfm_workspace_bytes_padded = _sig("cfm_workspace_bytes_padded", SZ, P, I32, I32,
 cfm_encode_masked = _sig("cfm_encode_masked", I32, P, P, P, P, P, P, I32, P, P, P, P, SZ, P)
 cfm_encode_padded = _sig("cfm_encode_padded", I32, P, P, P, P, P, P, SZ, P)
 cfm_masks_from_plan = _sig("cfm_masks_from_plan", I32, P, P, P, P, P)
+cfm_profile_read = _sig("cfm_profile_read", I32, P, P, P, P, I32)
 cfm_ctc_workspace_bytes = _sig("cfm_ctc_workspace_bytes", SZ, P, I32)
 cfm_ctc_logprobs = _sig("cfm_ctc_logprobs", I32, P, P, I32, P, P, P, SZ, P)
 
 EXPORTED = ["cfm_version", "cfm_last_error", "cfm_model_create", "cfm_model_destroy", "cfm_model_set_option",
             "cfm_plan_masked", "cfm_plan_padded", "cfm_workspace_bytes_masked", "cfm_workspace_bytes_padded",
-            "cfm_encode_masked", "cfm_encode_padded", "cfm_masks_from_plan", "cfm_ctc_workspace_bytes",
+            "cfm_encode_masked", "cfm_encode_padded", "cfm_masks_from_plan", "cfm_profile_read", "cfm_ctc_workspace_bytes",
             "cfm_ctc_logprobs"]
+
+
+def profile_read(h):
+    """{kernel class: (total_ms, launches)} accumulated by the in-stream event profiler."""
+    cap = 32
+    names = (ctypes.c_char_p * cap)()
+    ms = (ctypes.c_double * cap)()
+    n = (ctypes.c_int64 * cap)()
+    k = cfm_profile_read(h, ctypes.cast(names, P), ctypes.cast(ms, P), ctypes.cast(n, P), cap)
+    return {names[i].decode(): (ms[i], n[i]) for i in range(min(k, cap))}
+
+
+PROFILE_CLASSES = ["frontend_conv0_dw", "frontend_pw_gemm", "frontend_dw2", "pos_gemm", "layernorm", "ffn_w1_gemm",
+                   "ffn_w2_gemm", "qkv_gemm", "chunk_attention", "out_proj_gemm", "pw1_glu_gemm", "conv_dw_ln_silu",
+                   "pw2_gemm", "cache_copy", "ctc"]
 
 
 def check(status: int) -> None:

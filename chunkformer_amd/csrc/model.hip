@@ -39,6 +39,15 @@ cfm_status set_error(cfm_status s, const std::string& msg) {
     if (_e) return set_error(CFM_ERR_RUNTIME, std::string(#x ": ") + hipGetErrorString((hipError_t)_e)); \
   } while (0)
 
+// time one launch (class CLS) with events when that class is enabled in prof_mask
+#define PROF(CLS, X)                      \
+  do {                                    \
+    hipEvent_t _pb;                       \
+    prof_begin(CLS, st, &_pb);            \
+    KCHK(X);                              \
+    prof_end(CLS, st, _pb);               \
+  } while (0)
+
 static size_t align_up(size_t x, size_t a = 256) { return (x + a - 1) / a * a; }
 
 struct Carver {
@@ -69,6 +78,16 @@ struct FrontW {
 
 }  // namespace cfm
 
+// Kernel classes timed by the optional in-stream profiler (HIP events around launches)
+enum {
+  PC_FE_CONV = 0, PC_FE_GEMM, PC_FE_DW2, PC_POS, PC_LN, PC_FFN1, PC_FFN2, PC_QKV, PC_ATTN, PC_OPROJ, PC_PW1,
+  PC_CONV, PC_PW2, PC_CACHE, PC_CTC, PC_N
+};
+static const char* const PC_NAMES[PC_N] = {
+    "frontend_conv0_dw", "frontend_pw_gemm", "frontend_dw2", "pos_gemm", "layernorm", "ffn_w1_gemm", "ffn_w2_gemm",
+    "qkv_gemm", "chunk_attention", "out_proj_gemm", "pw1_glu_gemm", "conv_dw_ln_silu", "pw2_gemm", "cache_copy",
+    "ctc"};
+
 struct cfm_model {
   cfm_config cfg;
   int device = 0;
@@ -76,8 +95,52 @@ struct cfm_model {
   std::vector<cfm::LayerW> layers;
   cfm::FrontW fe;
   int max_layers = -1;
+  // profiler: bitmask of PC_* classes to bracket with events on the launch stream
+  uint32_t prof_mask = 0;
+  mutable std::vector<hipEvent_t> ev_pool;
+  mutable std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> ev_live;
+  mutable double prof_ms[PC_N] = {0};
+  mutable int64_t prof_n[PC_N] = {0};
+  hipEvent_t ev_get() const {
+    if (ev_pool.empty()) {
+      hipEvent_t e;
+      if (hipEventCreate(&e) != hipSuccess) return nullptr;
+      return e;
+    }
+    hipEvent_t e = ev_pool.back();
+    ev_pool.pop_back();
+    return e;
+  }
+  void prof_begin(int cls, hipStream_t st, hipEvent_t* b) const {
+    *b = nullptr;
+    if (!(prof_mask >> cls & 1u)) return;
+    *b = ev_get();
+    if (*b) (void)hipEventRecord(*b, st);
+  }
+  void prof_end(int cls, hipStream_t st, hipEvent_t b) const {
+    if (!b) return;
+    hipEvent_t e = ev_get();
+    if (!e) return;
+    (void)hipEventRecord(e, st);
+    ev_live.push_back({cls, {b, e}});
+  }
+  void prof_collect() const {   // host-synchronising: only from cfm_profile_read
+    for (auto& it : ev_live) {
+      float ms = 0.f;
+      if (hipEventSynchronize(it.second.second) == hipSuccess &&
+          hipEventElapsedTime(&ms, it.second.first, it.second.second) == hipSuccess) {
+        prof_ms[it.first] += ms;
+        prof_n[it.first] += 1;
+      }
+      ev_pool.push_back(it.second.first);
+      ev_pool.push_back(it.second.second);
+    }
+    ev_live.clear();
+  }
   virtual ~cfm_model() {
     if (dev_mem) { (void)hipSetDevice(device); (void)hipFree(dev_mem); }
+    for (auto& it : ev_live) { (void)hipEventDestroy(it.second.first); (void)hipEventDestroy(it.second.second); }
+    for (auto e : ev_pool) (void)hipEventDestroy(e);
   }
   virtual cfm_status encode(const float* feats, const int32_t* plan_dev, const int32_t* plan_hdr, const float* aci,
                             const float* cci, int trunc, float* aco, float* cco, float* out, void* ws, size_t wsb,
@@ -166,22 +229,22 @@ struct ModelT : public cfm_model {
     const int G = fe_group(hh);
     for (int g0 = 0; g0 < nwin; g0 += G) {
       const int ng = std::min(G, nwin - g0);
-      KCHK(frontend_conv0_dw<T>(feats, meta + (size_t)g0 * PLAN_REC, PLAN_REC, ng, Wn, fe.cm, fe.ci, fe.w0, fe.b0,
+      PROF(PC_FE_CONV, frontend_conv0_dw<T>(feats, meta + (size_t)g0 * PLAN_REC, PLAN_REC, ng, Wn, fe.cm, fe.ci, fe.w0, fe.b0,
                                 fe.w1, fe.b1, d, w.feA, st));
       EpiArgs e1; e1.bias = fe.b_pw1; e1.out = w.feB; e1.ldo = d;
-      KCHK(gemm<T>(EPI_STORE, ACT_RELU, w.feA, d, (const T*)fe.pw1, d, ng * T2 * 19, d, d, e1, st));
-      KCHK(frontend_dw2<T>(w.feB, ng, T2, d, fe.w2, fe.b2, w.feA, st));
+      PROF(PC_FE_GEMM, gemm<T>(EPI_STORE, ACT_RELU, w.feA, d, (const T*)fe.pw1, d, ng * T2 * 19, d, d, e1, st));
+      PROF(PC_FE_DW2, frontend_dw2<T>(w.feB, ng, T2, d, fe.w2, fe.b2, w.feA, st));
       EpiArgs e2; e2.bias = fe.b_pw2; e2.out = w.feB; e2.ldo = d;
-      KCHK(gemm<T>(EPI_STORE, ACT_RELU, w.feA, d, (const T*)fe.pw2, d, ng * T3 * 9, d, d, e2, st));
+      PROF(PC_FE_GEMM, gemm<T>(EPI_STORE, ACT_RELU, w.feA, d, (const T*)fe.pw2, d, ng * T3 * 9, d, d, e2, st));
       EpiArgs e3; e3.bias = fe.b_out; e3.out = w.x; e3.ldo = d; e3.row_off = g0 * tout; e3.alpha = std::sqrt((float)d);
-      KCHK(gemm<T>(EPI_STORE_F32, ACT_NONE, w.feB, 9 * d, (const T*)fe.wout, 9 * d, ng * T3, d, 9 * d, e3, st));
+      PROF(PC_FE_GEMM, gemm<T>(EPI_STORE_F32, ACT_NONE, w.feB, 9 * d, (const T*)fe.wout, 9 * d, ng * T3, d, 9 * d, e3, st));
     }
     // ---------------- relative positions: P_l = pos . W_pos_l^T
     const int nl = (max_layers >= 0 && max_layers < cfg.num_blocks) ? max_layers : cfg.num_blocks;
-    KCHK(pos_table<T>(d, p_rows, hh[PH_PANCHOR], w.pos, st));
+    PROF(PC_POS, pos_table<T>(d, p_rows, hh[PH_PANCHOR], w.pos, st));
     for (int l = 0; l < nl; ++l) {
       EpiArgs e; e.out = w.P + (size_t)l * prow_pad * d; e.ldo = d;
-      KCHK(gemm<T>(EPI_STORE, ACT_NONE, w.pos, d, (const T*)layers[l].pos, d, p_rows, d, d, e, st));
+      PROF(PC_POS, gemm<T>(EPI_STORE, ACT_NONE, w.pos, d, (const T*)layers[l].pos, d, p_rows, d, d, e, st));
     }
     // ---------------- stream padding rows (cache slots and right zero padding)
     if (kvoff > 0) HIPC(hipMemsetAsync(w.kv, 0, (size_t)kvoff * 2 * d * sizeof(T), st));
@@ -194,48 +257,48 @@ struct ModelT : public cfm_model {
     const int natt = hh[PH_NATT], nconv = hh[PH_NCONV];
     const int cache_start = std::min(trunc, rows);   // new cache = stream[:trunc + L][-L:] (attention.py:467)
     if (nl == 0) {
-      KCHK(layernorm2_f32(w.x, rows, d, fe.an_w, fe.an_b, nullptr, nullptr, eps, out, st));
+      PROF(PC_LN, layernorm2_f32(w.x, rows, d, fe.an_w, fe.an_b, nullptr, nullptr, eps, out, st));
       return CFM_OK;
     }
-    KCHK(layernorm<T>(w.x, rows, d, layers[0].ln_ffm_w, layers[0].ln_ffm_b, eps, w.h, nullptr, st));
+    PROF(PC_LN, layernorm<T>(w.x, rows, d, layers[0].ln_ffm_w, layers[0].ln_ffm_b, eps, w.h, nullptr, st));
     for (int l = 0; l < nl; ++l) {
       const LayerW& Lw = layers[l];
       // macaron FFN (x 0.5)
       { EpiArgs e; e.bias = Lw.b_ff1m; e.out = w.hid; e.ldo = ff;
-        KCHK(gemm<T>(EPI_STORE, ACT_SILU, w.h, d, (const T*)Lw.ff1m, d, rows, ff, d, e, st)); }
+        PROF(PC_FFN1, gemm<T>(EPI_STORE, ACT_SILU, w.h, d, (const T*)Lw.ff1m, d, rows, ff, d, e, st)); }
       { EpiArgs e; e.bias = Lw.b_ff2m; e.x = w.x; e.ldx = d; e.alpha = 0.5f;
-        KCHK(gemm<T>(EPI_RESID, ACT_NONE, w.hid, ff, (const T*)Lw.ff2m, ff, rows, d, ff, e, st)); }
+        PROF(PC_FFN2, gemm<T>(EPI_RESID, ACT_NONE, w.hid, ff, (const T*)Lw.ff2m, ff, rows, d, ff, e, st)); }
       // MHSA
-      KCHK(layernorm<T>(w.x, rows, d, Lw.ln_mha_w, Lw.ln_mha_b, eps, w.h, nullptr, st));
-      if (aci) KCHK(att_cache_in<T>(aci + (size_t)l * L * 2 * d, L, 2 * d, w.kv, st));
+      PROF(PC_LN, layernorm<T>(w.x, rows, d, Lw.ln_mha_w, Lw.ln_mha_b, eps, w.h, nullptr, st));
+      if (aci) PROF(PC_CACHE, att_cache_in<T>(aci + (size_t)l * L * 2 * d, L, 2 * d, w.kv, st));
       { EpiArgs e; e.bias = Lw.b_qkv; e.out = w.q; e.out2 = w.kv; e.row_off = kvoff; e.d = d;
-        KCHK(gemm<T>(EPI_QKV, ACT_NONE, w.h, d, (const T*)Lw.qkv, d, rows, 3 * d, d, e, st)); }
-      if (aci && aco) KCHK(att_cache_out<T>(w.kv, cache_start, L, 2 * d, aco + (size_t)l * L * 2 * d, st));
-      KCHK(chunk_attention<T>(w.q, w.kv, kv_rows, w.P + (size_t)l * prow_pad * d, p_rows, Lw.pu, Lw.pv, attd, natt, H,
+        PROF(PC_QKV, gemm<T>(EPI_QKV, ACT_NONE, w.h, d, (const T*)Lw.qkv, d, rows, 3 * d, d, e, st)); }
+      if (aci && aco) PROF(PC_CACHE, att_cache_out<T>(w.kv, cache_start, L, 2 * d, aco + (size_t)l * L * 2 * d, st));
+      PROF(PC_ATTN, chunk_attention<T>(w.q, w.kv, kv_rows, w.P + (size_t)l * prow_pad * d, p_rows, Lw.pu, Lw.pv, attd, natt, H,
                               w.ao, st));
       { EpiArgs e; e.bias = Lw.b_o; e.x = w.x; e.ldx = d;
-        KCHK(gemm<T>(EPI_RESID, ACT_NONE, w.ao, d, (const T*)Lw.wo, d, rows, d, d, e, st)); }
+        PROF(PC_OPROJ, gemm<T>(EPI_RESID, ACT_NONE, w.ao, d, (const T*)Lw.wo, d, rows, d, d, e, st)); }
       // convolution module
-      KCHK(layernorm<T>(w.x, rows, d, Lw.ln_conv_w, Lw.ln_conv_b, eps, w.h, masked ? nullptr : rmask, st));
-      if (cci) KCHK(cnn_cache_in<T>(cci + (size_t)l * d * 7, d, 7, w.glu, st));
+      PROF(PC_LN, layernorm<T>(w.x, rows, d, Lw.ln_conv_w, Lw.ln_conv_b, eps, w.h, masked ? nullptr : rmask, st));
+      if (cci) PROF(PC_CACHE, cnn_cache_in<T>(cci + (size_t)l * d * 7, d, 7, w.glu, st));
       { EpiArgs e; e.bias = Lw.b_pw1; e.out = w.glu; e.ldo = d; e.row_off = gluoff;
-        KCHK(gemm<T>(EPI_GLU, ACT_NONE, w.h, d, (const T*)Lw.pw1, d, rows, 2 * d, d, e, st)); }
-      if (cci && cco) KCHK(cnn_cache_out<T>(w.glu, cache_start, d, 7, cco + (size_t)l * d * 7, st));
-      KCHK(conv_dw_ln_silu<T>(w.glu, convd, nconv, d, Lw.dw_t, Lw.b_dw, Lw.cn_w, Lw.cn_b, eps, w.cv, st));
+        PROF(PC_PW1, gemm<T>(EPI_GLU, ACT_NONE, w.h, d, (const T*)Lw.pw1, d, rows, 2 * d, d, e, st)); }
+      if (cci && cco) PROF(PC_CACHE, cnn_cache_out<T>(w.glu, cache_start, d, 7, cco + (size_t)l * d * 7, st));
+      PROF(PC_CONV, conv_dw_ln_silu<T>(w.glu, convd, nconv, d, Lw.dw_t, Lw.b_dw, Lw.cn_w, Lw.cn_b, eps, w.cv, st));
       { EpiArgs e; e.bias = Lw.b_pw2; e.x = w.x; e.ldx = d; e.rowmask = rmask;
-        KCHK(gemm<T>(EPI_RESID, ACT_NONE, w.cv, d, (const T*)Lw.pw2, d, rows, d, d, e, st)); }
+        PROF(PC_PW2, gemm<T>(EPI_RESID, ACT_NONE, w.cv, d, (const T*)Lw.pw2, d, rows, d, d, e, st)); }
       // FFN (x 0.5)
-      KCHK(layernorm<T>(w.x, rows, d, Lw.ln_ff_w, Lw.ln_ff_b, eps, w.h, nullptr, st));
+      PROF(PC_LN, layernorm<T>(w.x, rows, d, Lw.ln_ff_w, Lw.ln_ff_b, eps, w.h, nullptr, st));
       { EpiArgs e; e.bias = Lw.b_ff1; e.out = w.hid; e.ldo = ff;
-        KCHK(gemm<T>(EPI_STORE, ACT_SILU, w.h, d, (const T*)Lw.ff1, d, rows, ff, d, e, st)); }
+        PROF(PC_FFN1, gemm<T>(EPI_STORE, ACT_SILU, w.h, d, (const T*)Lw.ff1, d, rows, ff, d, e, st)); }
       { EpiArgs e; e.bias = Lw.b_ff2; e.x = w.x; e.ldx = d; e.alpha = 0.5f;
-        KCHK(gemm<T>(EPI_RESID, ACT_NONE, w.hid, ff, (const T*)Lw.ff2, ff, rows, d, ff, e, st)); }
+        PROF(PC_FFN2, gemm<T>(EPI_RESID, ACT_NONE, w.hid, ff, (const T*)Lw.ff2, ff, rows, d, ff, e, st)); }
       // norm_final (+ next layer's macaron LN, or after_norm)
       if (l + 1 < nl)
-        KCHK(layernorm2<T>(w.x, rows, d, Lw.ln_fin_w, Lw.ln_fin_b, layers[l + 1].ln_ffm_w, layers[l + 1].ln_ffm_b, eps,
+        PROF(PC_LN, layernorm2<T>(w.x, rows, d, Lw.ln_fin_w, Lw.ln_fin_b, layers[l + 1].ln_ffm_w, layers[l + 1].ln_ffm_b, eps,
                            w.h, st));
       else
-        KCHK(layernorm2_f32(w.x, rows, d, Lw.ln_fin_w, Lw.ln_fin_b, fe.an_w, fe.an_b, eps, out, st));
+        PROF(PC_LN, layernorm2_f32(w.x, rows, d, Lw.ln_fin_w, Lw.ln_fin_b, fe.an_w, fe.an_b, eps, out, st));
     }
     return CFM_OK;
   }
@@ -257,8 +320,8 @@ struct ModelT : public cfm_model {
     }
     float* dst = logp ? logp : logits;
     EpiArgs e; e.bias = fe.ctc_b; e.out = dst; e.ldo = V;
-    KCHK(gemm<T>(EPI_STORE_F32, ACT_NONE, A, d, (const T*)fe.ctc_w, d, rows, V, d, e, st));
-    KCHK(log_softmax_rows(dst, rows, V, logp ? 1 : 0, ids, st));
+    PROF(PC_CTC, gemm<T>(EPI_STORE_F32, ACT_NONE, A, d, (const T*)fe.ctc_w, d, rows, V, d, e, st));
+    PROF(PC_CTC, log_softmax_rows(dst, rows, V, logp ? 1 : 0, ids, st));
     return CFM_OK;
   }
 };
@@ -452,6 +515,12 @@ void cfm_model_destroy(cfm_model* m) { delete m; }
 cfm_status cfm_model_set_option(cfm_model* m, const char* key, int64_t value) {
   if (!m || !key) return set_error(CFM_ERR_VALUE, "null argument");
   if (!std::strcmp(key, "max_layers")) { m->max_layers = (int)value; return CFM_OK; }
+  if (!std::strcmp(key, "profile")) { m->prof_mask = (uint32_t)value; return CFM_OK; }
+  if (!std::strcmp(key, "profile_reset")) {
+    m->prof_collect();
+    for (int i = 0; i < PC_N; ++i) { m->prof_ms[i] = 0; m->prof_n[i] = 0; }
+    return CFM_OK;
+  }
   return set_error(CFM_ERR_VALUE, std::string("unknown option ") + key);
 }
 
@@ -501,6 +570,18 @@ cfm_status cfm_masks_from_plan(const int32_t* h, const int32_t* plan_dev, uint8_
   if (h[PH_KIND] != 1) return set_error(CFM_ERR_VALUE, "not a masked-batch plan");
   KCHK(masks_from_plan(plan_dev + PH_HEADER, h[PH_NWIN], h[PH_C], h[PH_L], h[PH_R], att, pad, (hipStream_t)stream));
   return CFM_OK;
+}
+
+int32_t cfm_profile_read(const cfm_model* m, const char** names, double* total_ms, int64_t* launches, int32_t cap) {
+  if (!m) return 0;
+  m->prof_collect();
+  const int n = std::min<int>(cap, PC_N);
+  for (int i = 0; i < n; ++i) {
+    if (names) names[i] = PC_NAMES[i];
+    if (total_ms) total_ms[i] = m->prof_ms[i];
+    if (launches) launches[i] = m->prof_n[i];
+  }
+  return PC_N;
 }
 
 size_t cfm_ctc_workspace_bytes(const cfm_model* m, int32_t rows) { return m ? m->ctc_ws_bytes(rows) : 0; }

@@ -70,8 +70,17 @@ const char* cfm_last_error(void);
 cfm_status cfm_model_create(const cfm_config* cfg, const cfm_tensor_view* weights, int32_t n_weights,
                             int32_t device, cfm_model** out);
 void cfm_model_destroy(cfm_model* m);
-/* test/diagnostic knobs: "max_layers" (run only the first N blocks, -1 = all) */
+/* diagnostic knobs:
+ *   "max_layers"    run only the first N blocks (-1 = all)
+ *   "profile"       bitmask of kernel classes to bracket with HIP events on the launch
+ *                   stream (bit i = class i of cfm_profile_read); 0 = off
+ *   "profile_reset" clear the accumulated profile */
 cfm_status cfm_model_set_option(cfm_model* m, const char* key, int64_t value);
+/* Per kernel class: name, accumulated milliseconds and launch count of the
+ * event-bracketed launches since the last reset.  Host-synchronising (waits for
+ * the recorded events); never call it inside graph capture.  Returns the number
+ * of classes (fills at most `cap`). */
+int32_t cfm_profile_read(const cfm_model* m, const char** names, double* total_ms, int64_t* launches, int32_t cap);
 
 /* ------------------------------------------------------------------ plans
  * A plan is an int32 blob computed on the HOST (no GPU needed) and uploaded by
