@@ -68,6 +68,10 @@ cfm_masks_from_plan = _sig("cfm_masks_from_plan", I32, P, P, P, P, P)
 cfm_profile_read = _sig("cfm_profile_read", I32, P, P, P, P, I32)
 cfm_ctc_workspace_bytes = _sig("cfm_ctc_workspace_bytes", SZ, P, I32)
 cfm_ctc_logprobs = _sig("cfm_ctc_logprobs", I32, P, P, I32, P, P, P, SZ, P)
+# include/cfm_ops.h
+cfm_op_gemm = _sig("cfm_op_gemm", I32, I32, I32, I32, P, I32, P, I32, I32, I32, I32, P, ctypes.c_float, P, I32, I32, P,
+                   I32, P, I32, P, I32, P)
+EXPORTED_OPS = ["cfm_op_gemm"]
 
 EXPORTED = ["cfm_version", "cfm_last_error", "cfm_model_create", "cfm_model_destroy", "cfm_model_set_option",
             "cfm_plan_masked", "cfm_plan_padded", "cfm_workspace_bytes_masked", "cfm_workspace_bytes_padded",

@@ -25,6 +25,8 @@ template <typename T>
 int gemm(int epi, int act, const T* A, int lda, const T* W, int ldw, int M, int N, int K, const EpiArgs& ep,
          hipStream_t st);
 
+void gemm_force_small_tiles(int v);
+
 // LayerNorm over d (eps) of f32 rows -> T rows; optional 0/1 row mask on the output.
 template <typename T>
 int layernorm(const float* x, int M, int d, const float* w, const float* b, float eps, T* out,

@@ -15,6 +15,7 @@
 #include <vector>
 
 #include "../../include/cfm.h"
+#include "../../include/cfm_ops.h"
 #include "cfm_common.h"
 #include "cfm_kernels.h"
 #include "plan.h"
@@ -582,6 +583,24 @@ int32_t cfm_profile_read(const cfm_model* m, const char** names, double* total_m
     if (launches) launches[i] = m->prof_n[i];
   }
   return PC_N;
+}
+
+cfm_status cfm_op_gemm(int32_t dtype, int32_t epi, int32_t act, const void* A, int32_t lda, const void* W, int32_t ldw,
+                       int32_t M, int32_t N, int32_t K, const float* bias, float alpha, void* out, int32_t ldo,
+                       int32_t row_off, void* out2, int32_t d, float* x, int32_t ldx, const uint8_t* rowmask,
+                       int32_t small_tiles, cfm_stream stream) {
+  EpiArgs e;
+  e.bias = bias; e.alpha = alpha; e.out = out; e.out2 = out2; e.ldo = ldo; e.row_off = row_off; e.x = x; e.ldx = ldx;
+  e.rowmask = rowmask; e.d = d;
+  gemm_force_small_tiles(small_tiles);
+  int r;
+  if (dtype == CFM_DTYPE_F32)
+    r = gemm<float>(epi, act, (const float*)A, lda, (const float*)W, ldw, M, N, K, e, (hipStream_t)stream);
+  else
+    r = gemm<bf16>(epi, act, (const bf16*)A, lda, (const bf16*)W, ldw, M, N, K, e, (hipStream_t)stream);
+  gemm_force_small_tiles(0);
+  if (r) return set_error(CFM_ERR_RUNTIME, std::string("gemm: ") + hipGetErrorString((hipError_t)r));
+  return CFM_OK;
 }
 
 size_t cfm_ctc_workspace_bytes(const cfm_model* m, int32_t rows) { return m ? m->ctc_ws_bytes(rows) : 0; }

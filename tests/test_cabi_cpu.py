@@ -19,12 +19,13 @@ def lib():
 
 
 def test_exports_every_declared_symbol(lib):
-    hdr = open(os.path.join(ROOT, "include", "cfm.h")).read()
-    declared = set(re.findall(r"\b(cfm_[a-z_]+)\s*\(", hdr))
-    assert declared, "no declarations parsed"
-    for name in sorted(declared):
-        assert hasattr(lib.lib, name), f"libcfm.so does not export {name}"
-    assert set(lib.EXPORTED) == declared
+    for h, exported in (("cfm.h", lib.EXPORTED), ("cfm_ops.h", lib.EXPORTED_OPS)):
+        hdr = open(os.path.join(ROOT, "include", h)).read()
+        declared = set(re.findall(r"\b(cfm_[a-z_]+)\s*\(", hdr))
+        assert declared, "no declarations parsed"
+        for name in sorted(declared):
+            assert hasattr(lib.lib, name), f"libcfm.so does not export {name}"
+        assert set(exported) == declared
 
 
 def test_version(lib):

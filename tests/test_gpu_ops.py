@@ -1,0 +1,113 @@
+"""Kernel-level GPU parity: the projection GEMM (every epilogue, both tile paths, bf16
+and exact-f32) against a torch fp32 reference of the same op (cfm_op_gemm, include/cfm_ops.h)."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def L():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from chunkformer_amd import _lib
+    return _lib
+
+
+def _run(L, dtype, epi, act, A, W, bias, alpha=1.0, out=None, ldo=0, row_off=0, out2=None, d=0, x=None,
+         rowmask=None, small=0):
+    M, K = A.shape
+    N = W.shape[0]
+    st = torch.cuda.current_stream().cuda_stream
+    L.check(L.cfm_op_gemm(dtype, epi, act, A.data_ptr(), K, W.data_ptr(), K, M, N, K, L.ptr(bias), alpha,
+                          L.ptr(out), ldo, row_off, L.ptr(out2), d, L.ptr(x), N if x is not None else 0,
+                          L.ptr(rowmask), small, st))
+    torch.cuda.synchronize()
+
+
+def _ref(A, W, bias):
+    r = A.float() @ W.float().t()
+    return r + bias if bias is not None else r
+
+
+def _close(got, exp, tol):
+    err = (got.float() - exp).abs().max().item()
+    scale = exp.abs().max().item() + 1e-6
+    assert err <= tol * scale, f"max err {err} vs scale {scale}"
+
+
+SHAPES = [(1000, 512, 512), (700, 2048, 512), (513, 512, 2048), (256, 256, 4608), (300, 48, 128),
+          (70001, 512, 512), (33000, 2048, 512)]   # the last two run the persistent multi-tile path
+MODES = [("bf16", 0), ("bf16", 1), ("fp32", 0)]
+
+
+@pytest.mark.parametrize("M,N,K", SHAPES)
+@pytest.mark.parametrize("mode", MODES)
+@pytest.mark.parametrize("act", [0, 1, 2])
+def test_gemm_store(L, M, N, K, mode, act):
+    dt, small = mode
+    tdt = torch.bfloat16 if dt == "bf16" else torch.float32
+    g = torch.Generator(device="cuda").manual_seed(M + N + K)
+    A = (torch.randn(M, K, device="cuda", generator=g) * 0.5).to(tdt)
+    W = (torch.randn(N, K, device="cuda", generator=g) / K ** 0.5).to(tdt)
+    bias = torch.randn(N, device="cuda", generator=g)
+    out = torch.full((M + 3, N), float("nan"), device="cuda", dtype=tdt)
+    _run(L, L.DTYPE_BF16 if dt == "bf16" else L.DTYPE_F32, 0, act, A, W, bias, out=out, ldo=N, row_off=3, small=small)
+    r = _ref(A, W, bias)
+    r = torch.relu(r) if act == 1 else (torch.nn.functional.silu(r) if act == 2 else r)
+    _close(out[3:], r, 1e-2 if dt == "bf16" else 1e-5)
+    assert torch.isnan(out[:3].float()).all()
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_gemm_store_f32_and_resid(L, mode):
+    dt, small = mode
+    tdt = torch.bfloat16 if dt == "bf16" else torch.float32
+    code = L.DTYPE_BF16 if dt == "bf16" else L.DTYPE_F32
+    M, N, K = 777, 512, 4608
+    g = torch.Generator(device="cuda").manual_seed(5)
+    A = (torch.randn(M, K, device="cuda", generator=g) * 0.5).to(tdt)
+    W = (torch.randn(N, K, device="cuda", generator=g) / K ** 0.5).to(tdt)
+    bias = torch.randn(N, device="cuda", generator=g)
+    out = torch.empty(M, N, device="cuda")
+    _run(L, code, 1, 0, A, W, bias, alpha=22.627, out=out, ldo=N, small=small)
+    _close(out, 22.627 * _ref(A, W, bias), 1e-3 if dt == "bf16" else 1e-5)
+    x0 = torch.randn(M, N, device="cuda", generator=g)
+    x = x0.clone()
+    rm = (torch.rand(M, device="cuda", generator=g) > 0.3).to(torch.uint8)
+    _run(L, code, 2, 0, A, W, bias, alpha=0.5, x=x, rowmask=rm, small=small)
+    _close(x, x0 + 0.5 * _ref(A, W, bias) * rm.float()[:, None], 1e-3 if dt == "bf16" else 1e-5)
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_gemm_qkv_and_glu(L, mode):
+    dt, small = mode
+    tdt = torch.bfloat16 if dt == "bf16" else torch.float32
+    code = L.DTYPE_BF16 if dt == "bf16" else L.DTYPE_F32
+    d, M, Lc = 512, 900, 5
+    g = torch.Generator(device="cuda").manual_seed(9)
+    A = (torch.randn(M, d, device="cuda", generator=g) * 0.5).to(tdt)
+    W = (torch.randn(3 * d, d, device="cuda", generator=g) / d ** 0.5).to(tdt)
+    bias = torch.randn(3 * d, device="cuda", generator=g)
+    q = torch.empty(M, d, device="cuda", dtype=tdt)
+    kv = torch.zeros(M + Lc + 2, 2 * d, device="cuda", dtype=tdt)
+    _run(L, code, 3, 0, A, W, bias, out=q, out2=kv, row_off=Lc, d=d, small=small)
+    r = _ref(A, W, bias)
+    tol = 1e-2 if dt == "bf16" else 1e-5
+    _close(q, r[:, :d], tol)
+    kvr = kv[Lc: Lc + M].view(M, d // 64, 2, 64)
+    _close(kvr[:, :, 0].reshape(M, d), r[:, d: 2 * d], tol)
+    _close(kvr[:, :, 1].reshape(M, d), r[:, 2 * d:], tol)
+    assert (kv[:Lc] == 0).all() and (kv[Lc + M:] == 0).all()
+    # GLU with [a16 | gate16] interleaved weights
+    W1 = (torch.randn(2 * d, d, device="cuda", generator=g) / d ** 0.5).to(tdt)
+    b1 = torch.randn(2 * d, device="cuda", generator=g)
+    idx = torch.arange(2 * d, device="cuda").view(d // 16, 2, 16)
+    perm = torch.stack([idx[:, 0] // 2 * 0 + torch.arange(d // 16, device="cuda")[:, None] * 16
+                        + torch.arange(16, device="cuda")[None, :],
+                        d + torch.arange(d // 16, device="cuda")[:, None] * 16 + torch.arange(16, device="cuda")[None, :]],
+                       1).reshape(-1)
+    out = torch.empty(M + 7, d, device="cuda", dtype=tdt)
+    _run(L, code, 4, 0, A, W1[perm].contiguous(), b1[perm].contiguous(), out=out, ldo=d, row_off=7, small=small)
+    r = _ref(A, W1, b1)
+    _close(out[7:], r[:, :d] * torch.sigmoid(r[:, d:]), tol)
