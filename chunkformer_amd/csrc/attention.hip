@@ -194,4 +194,278 @@ template int chunk_attention<float>(const float*, const float*, int, const float
 template int chunk_attention<bf16>(const bf16*, const bf16*, int, const bf16*, int, const float*, const float*,
                                    const int32_t*, int, int, bf16*, hipStream_t);
 
+
+
+// =====================================================================================
+// Fast path (bf16, masked batch): one block = one head x a run of NCH consecutive chunks.
+//
+// The packed chunk stream makes consecutive chunks' key windows overlap by W - C rows, so a
+// block slides along the stream: K and V^T live in an LDS ring of 384 rows (the window of
+// the current chunk plus the next chunk's C new rows, register-prefetched during compute),
+// and the head's relative-position rows P (<= 383) are staged once per block.  Per wave (16
+// queries) everything is computed TRANSPOSED (keys / P rows on the MFMA row axis, queries
+// on lanes): S^T = K . (q+u)^T, band^T = P . (q+v)^T, then O^T = V^T . P^T uses the score
+// registers directly as the B operand (their key order is a fixed permutation, matched by
+// the V^T fragment), so probabilities never round-trip through LDS.  The rel_shift skew is
+// a per-wave bf16 scratch write + diagonal read (reference: matrix_bd is bf16 under autocast).
+// Softmax is exact (not online): all <= 320 scores of a query stay in registers.
+// =====================================================================================
+namespace {
+constexpr int RING = 384;                       // ring rows (>= W + C)
+constexpr int NCH = 8;                          // chunks per block
+constexpr int KR_BYTES = RING * 128;            // K ring [384][64] bf16, 16-B chunks swizzled
+constexpr int P_BYTES_ = RING * 128;            // P rows [384][64] bf16, swizzled
+constexpr int VT_PITCH_B = (RING + 8) * 2;      // V^T [64 dims][384 (+8)] bf16
+constexpr int VT_BYTES_ = 64 * VT_PITCH_B;
+constexpr int SCR_PITCH = 50;                   // bf16 per query row of the skew scratch (48-wide band)
+constexpr int SCR_BYTES = 16 * SCR_PITCH * 2;   // per wave
+constexpr int RING_LDS = KR_BYTES + P_BYTES_ + VT_BYTES_ + 8 * SCR_BYTES + 512;
+}  // namespace
+
+CFM_DEV int sw128(int row, int ch) { return row * 128 + ((ch ^ ((row >> 1) & 7)) << 4); }
+
+__global__ __launch_bounds__(512, 1) void chunk_attention_ring_kernel(
+    const bf16* __restrict__ Q, const bf16* __restrict__ KV, int kv_rows, const bf16* __restrict__ P, int p_rows,
+    const float* __restrict__ pos_u, const float* __restrict__ pos_v, const int32_t* __restrict__ desc, int n_chunks,
+    int H, int C, int W, bf16* __restrict__ out, int diag) {
+  __shared__ __attribute__((aligned(16))) char smem[RING_LDS];
+  char* kr = smem;
+  char* pl = smem + KR_BYTES;
+  char* vt = pl + P_BYTES_;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int fr = lane & 15, g = lane >> 4;
+  // waves 0-3 work on chunk c, waves 4-7 on chunk c+1 (both windows live in the ring: W + C <= RING)
+  const int half = w >> 2, wq = w & 3;
+  bf16* scr = reinterpret_cast<bf16*>(vt + VT_BYTES_ + w * SCR_BYTES);
+  float* uv = reinterpret_cast<float*>(vt + VT_BYTES_ + 8 * SCR_BYTES);   // [2][64]: pos_bias_u / v of head h
+  const int h = blockIdx.y;
+  const int d = H * 64;
+  const int c0 = blockIdx.x * NCH, c1 = min(c0 + NCH, n_chunks);
+  if (c0 >= c1) return;
+
+  // ---- zero the K / V^T rings (rows past a window's end are read as masked keys: p = 0 must not meet NaN)
+  for (int idx = tid; idx < (KR_BYTES + P_BYTES_ + VT_BYTES_) / 16; idx += 512)
+    reinterpret_cast<u32x4*>(smem)[idx] = (u32x4){0u, 0u, 0u, 0u};
+  if (tid < 128) uv[tid] = (tid < 64 ? pos_u : pos_v)[h * 64 + (tid & 63)];
+  __syncthreads();
+  // ---- stage P rows and the first pair's windows (rows [kv0, kv0 + W + C))
+  for (int idx = tid; idx < p_rows * 8; idx += 512) {
+    const int r = idx >> 3, ch = idx & 7;
+    *reinterpret_cast<u32x4*>(pl + sw128(r, ch)) = *reinterpret_cast<const u32x4*>(P + (size_t)r * d + h * 64 + ch * 8);
+  }
+  // staging unit = two consecutive (even-aligned) flat rows x one 16-B chunk of K and V: the K halves
+  // go to the swizzled K ring, the V halves are interleaved into 8 bf16x2 words of V^T (conflict-free:
+  // the 64 lanes of a wave take 64 consecutive row pairs of one chunk)
+  typedef bf16 bf16x2_ __attribute__((ext_vector_type(2)));
+  auto stage_pair = [&](int frow, int ch, const u32x4& k0, const u32x4& v0, const u32x4& k1, const u32x4& v1) {
+    const int rr = frow % RING;   // even; rr + 1 < RING
+    *reinterpret_cast<u32x4*>(kr + sw128(rr, ch)) = k0;
+    *reinterpret_cast<u32x4*>(kr + sw128(rr + 1, ch)) = k1;
+    const bf16x8 a = __builtin_bit_cast(bf16x8, v0), b = __builtin_bit_cast(bf16x8, v1);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) *reinterpret_cast<bf16x2_*>(vt + (ch * 8 + e) * VT_PITCH_B + rr * 2) = (bf16x2_){a[e], b[e]};
+  };
+  auto load_pair = [&](int frow, int ch, u32x4& k0, u32x4& v0, u32x4& k1, u32x4& v1) {
+    const bf16* s0 = KV + (size_t)min(frow, kv_rows - 1) * (2 * d) + h * 128 + ch * 8;
+    const bf16* s1 = KV + (size_t)min(frow + 1, kv_rows - 1) * (2 * d) + h * 128 + ch * 8;
+    k0 = *reinterpret_cast<const u32x4*>(s0);
+    v0 = *reinterpret_cast<const u32x4*>(s0 + 64);
+    k1 = *reinterpret_cast<const u32x4*>(s1);
+    v1 = *reinterpret_cast<const u32x4*>(s1 + 64);
+  };
+  const int kvb = desc[(size_t)c0 * AD_INTS + AD_KV_ROW0];   // chunk c's window starts at kvb + (c - c0) * C
+  {
+    const int npairs = (W + (c0 + 1 < c1 ? C : 0)) / 2;
+    for (int idx = tid; idx < npairs * 8; idx += 512) {
+      const int pr = idx % npairs, ch = idx / npairs;
+      u32x4 k0, v0, k1, v1;
+      load_pair(kvb + 2 * pr, ch, k0, v0, k1, v1);
+      stage_pair(kvb + 2 * pr, ch, k0, v0, k1, v1);
+    }
+  }
+  __syncthreads();
+
+  const float scale = 0.125f;
+  const int i0 = wq * 16;
+  for (int cp = c0; cp < c1; cp += 2) {
+    const int kvp = kvb + (cp - c0) * C;
+    const int c = cp + half;
+    const bool active = c < c1 && i0 < C && diag != 1;
+    // ---- query fragment loads first (their wait must not cover the prefetch below)
+    bf16x8 qraw[2];
+    const int32_t* D = desc + (size_t)min(c, c1 - 1) * AD_INTS;
+    const int q_row0 = D[AD_Q_ROW0];
+    if (active) {
+      const bf16* qp = Q + (size_t)(q_row0 + i0 + fr) * d + h * 64;
+      qraw[0] = *reinterpret_cast<const bf16x8*>(qp + 8 * g);
+      qraw[1] = *reinterpret_cast<const bf16x8*>(qp + 32 + 8 * g);
+    }
+    // ---- prefetch the next pair's 2C new window rows [kvp + W + C, kvp + W + 3C) into registers
+    const int n_new = max(0, min(2 * C, (min(cp + 4, c1) - (cp + 2)) * C));
+    const int pf_pairs = n_new / 2;
+    u32x4 pk0[2], pv0[2], pk1[2], pv1[2];
+    int pf_row[2], pf_ch[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int idx = tid + 512 * q;
+      pf_row[q] = -1;
+      if (pf_pairs > 0 && idx < pf_pairs * 8) {
+        pf_ch[q] = idx / pf_pairs;
+        pf_row[q] = kvp + W + C + 2 * (idx % pf_pairs);
+        load_pair(pf_row[q], pf_ch[q], pk0[q], pv0[q], pk1[q], pv1[q]);
+      }
+    }
+    if (active) {
+      const int kv0 = D[AD_KV_ROW0];
+      const int key_lo = D[AD_KEY_LO], key_hi = D[AD_KEY_HI], p_base = D[AD_P_BASE], q_valid = D[AD_Q_VALID];
+      const int rb = kv0 % RING;   // ring row of window key 0
+      auto ring = [&](int j) { const int r = rb + j; return r >= RING ? r - RING : r; };
+      // ---- query fragments (B operands): lane (fr, g) = query i0+fr, dims 32s + 8g .. +7
+      bf16x8 qu[2], qv[2];
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const f32x4 u0 = *reinterpret_cast<const f32x4*>(uv + s * 32 + 8 * g);
+        const f32x4 u1 = *reinterpret_cast<const f32x4*>(uv + s * 32 + 8 * g + 4);
+        const f32x4 v0_ = *reinterpret_cast<const f32x4*>(uv + 64 + s * 32 + 8 * g);
+        const f32x4 v1_ = *reinterpret_cast<const f32x4*>(uv + 64 + s * 32 + 8 * g + 4);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float qf = (float)qraw[s][e];
+          qu[s][e] = (bf16)(qf + (e < 4 ? u0[e] : u1[e - 4]));
+          qv[s][e] = (bf16)(qf + (e < 4 ? v0_[e] : v1_[e - 4]));
+        }
+      }
+      const int jb = key_lo & ~15;
+      f32x4 S[5][4];
+      float mx = -INFINITY;
+#pragma unroll
+      for (int t = 0; t < 5; ++t) {
+        const int j0 = jb + 64 * t;
+        if (j0 >= key_hi) {
+#pragma unroll
+          for (int st = 0; st < 4; ++st) S[t][st] = (f32x4){-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+          continue;
+        }
+        // S^T[key 16st + 4g + rr][query fr]
+#pragma unroll
+        for (int st = 0; st < 4; ++st) {
+          const int rr_ = ring(j0 + 16 * st + fr);
+          f32x4 a = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int s = 0; s < 2; ++s)
+            a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<const bf16x8*>(kr + sw128(rr_, 4 * s + g)), qu[s],
+                                                        a, 0, 0, 0);
+          S[t][st] = a;
+        }
+        // band^T[P row kb + 16pt + 4g + rr][query fr] -> scratch[query][band pos], in two 32-key halves
+        // (3 P subtiles each, keeps the per-wave scratch at 16 x 48 bf16)
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+          const int kb = p_base - i0 - 15 + j0 + 32 * hh;
+#pragma unroll
+          for (int pt = 0; pt < 3; ++pt) {
+            const int prow = min(max(kb + 16 * pt + fr, 0), p_rows - 1);
+            f32x4 a = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int s = 0; s < 2; ++s)
+              a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<const bf16x8*>(pl + sw128(prow, 4 * s + g)),
+                                                          qv[s], a, 0, 0, 0);
+            typedef bf16 bf16x4 __attribute__((ext_vector_type(4)));
+            *reinterpret_cast<bf16x4*>(scr + fr * SCR_PITCH + 16 * pt + 4 * g) =
+                (bf16x4){(bf16)a[0], (bf16)a[1], (bf16)a[2], (bf16)a[3]};
+          }
+          // skewed read: score(query fr, key j0+32hh+16st+4g+rr) += band[fr][16st + 4g + rr + 15 - fr]
+#pragma unroll
+          for (int st2 = 0; st2 < 2; ++st2) {
+            const int st = 2 * hh + st2;
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr) {
+              const int jj = 16 * st2 + 4 * g + rr;
+              const float bdv = (float)scr[fr * SCR_PITCH + jj + 15 - fr];
+              float sv = (S[t][st][rr] + bdv) * scale;
+              const int j = j0 + 32 * hh + jj;
+              if (j < key_lo || j >= key_hi) sv = -INFINITY;
+              S[t][st][rr] = sv;
+              mx = fmaxf(mx, sv);
+            }
+          }
+        }
+      }
+      // ---- exact softmax per query (lanes fr, fr+16, fr+32, fr+48 share a query)
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      if (mx == -INFINITY) mx = 0.f;   // fully masked query: every p = 0, output 0 (reference: NaN -> 0)
+      float l = 0.f;
+#pragma unroll
+      for (int t = 0; t < 5; ++t)
+#pragma unroll
+        for (int st = 0; st < 4; ++st)
+#pragma unroll
+          for (int rr = 0; rr < 4; ++rr) {
+            const float p = __expf(S[t][st][rr] - mx);
+            S[t][st][rr] = p;
+            l += p;
+          }
+      l += __shfl_xor(l, 16, 64);
+      l += __shfl_xor(l, 32, 64);
+      // ---- O^T[dim 16nt + 4g + rr][query fr] = sum_keys V^T . P^T (key order permuted, same for both)
+      f32x4 O[4];
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) O[nt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int t = 0; t < 5; ++t) {
+        const int j0 = jb + 64 * t;
+        if (j0 >= key_hi) continue;
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          bf16x8 pb;
+#pragma unroll
+          for (int rr = 0; rr < 4; ++rr) {
+            pb[rr] = (bf16)S[t][2 * s][rr];
+            pb[4 + rr] = (bf16)S[t][2 * s + 1][rr];
+          }
+          const int ka = ring(j0 + 32 * s + 4 * g), kb2 = ring(j0 + 32 * s + 16 + 4 * g);
+#pragma unroll
+          for (int nt = 0; nt < 4; ++nt) {
+            const char* vrow = vt + (16 * nt + fr) * VT_PITCH_B;
+            typedef bf16 bf16x4 __attribute__((ext_vector_type(4)));
+            const bf16x4 lo = *reinterpret_cast<const bf16x4*>(vrow + ka * 2);
+            const bf16x4 hi = *reinterpret_cast<const bf16x4*>(vrow + kb2 * 2);
+            const bf16x8 va = (bf16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+            O[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va, pb, O[nt], 0, 0, 0);
+          }
+        }
+      }
+      const int qi = i0 + fr;
+      const bool live = qi < q_valid && l > 0.f;
+      const float inv = live ? 1.f / l : 0.f;
+      bf16* op = out + (size_t)(q_row0 + qi) * d + h * 64;
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        typedef bf16 bf16x4 __attribute__((ext_vector_type(4)));
+        *reinterpret_cast<bf16x4*>(op + 16 * nt + 4 * g) =
+            (bf16x4){(bf16)(O[nt][0] * inv), (bf16)(O[nt][1] * inv), (bf16)(O[nt][2] * inv), (bf16)(O[nt][3] * inv)};
+      }
+    }
+    // ---- the prefetched rows replace the first 2C rows of this pair's windows (no longer needed)
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+      if (pf_row[q] >= 0) stage_pair(pf_row[q], pf_ch[q], pk0[q], pv0[q], pk1[q], pv1[q]);
+    __syncthreads();
+  }
+}
+
+// returns -1 when the shape is not eligible for the ring kernel
+int chunk_attention_masked_bf16(const bf16* q, const bf16* kv, int kv_rows, const bf16* P, int p_rows,
+                                const float* pos_u, const float* pos_v, const int32_t* desc, int n_chunks, int H,
+                                int C, int W, bf16* out, hipStream_t st, int diag) {
+  if (C <= 0 || C > 64 || (C % 16) || (W & 1) || W + C > RING || p_rows > RING || n_chunks <= 0) return -1;
+  const dim3 grid((n_chunks + NCH - 1) / NCH, H);
+  hipLaunchKernelGGL(chunk_attention_ring_kernel, grid, dim3(512), 0, st, q, kv, kv_rows, P, p_rows, pos_u, pos_v,
+                     desc, n_chunks, H, C, W, out, diag);
+  CFM_CHECK_LAUNCH();
+  return 0;
+}
+
 }  // namespace cfm

@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+typedef __bf16 bf16;
+
 namespace cfm {
 
 enum { EPI_STORE = 0, EPI_STORE_F32 = 1, EPI_RESID = 2, EPI_QKV = 3, EPI_GLU = 4 };
@@ -43,6 +45,11 @@ int layernorm2_f32(float* x, int M, int d, const float* w1, const float* b1, con
 template <typename T>
 int chunk_attention(const T* q, const T* kv, int kv_rows, const T* P, int p_rows, const float* pos_u,
                     const float* pos_v, const int32_t* desc, int nblk, int H, T* out, hipStream_t st);
+
+// masked-batch ring kernel (bf16); -1 = shape not eligible
+int chunk_attention_masked_bf16(const bf16* q, const bf16* kv, int kv_rows, const bf16* P, int p_rows,
+                                const float* pos_u, const float* pos_v, const int32_t* desc, int n_chunks, int H,
+                                int C, int W, bf16* out, hipStream_t st, int diag = 0);
 
 // conv module: depthwise k=15 + bias + LayerNorm + SiLU (conv_module.hip)
 template <typename T>

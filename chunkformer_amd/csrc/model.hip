@@ -96,6 +96,8 @@ struct cfm_model {
   std::vector<cfm::LayerW> layers;
   cfm::FrontW fe;
   int max_layers = -1;
+  bool use_ring_attention = true;
+  int attn_diag = 0;                // "attn_diag": 1 = ring kernel without compute (staging only)   // "ring_attention" option (A/B against the generic kernel)
   // profiler: bitmask of PC_* classes to bracket with events on the launch stream
   uint32_t prof_mask = 0;
   mutable std::vector<hipEvent_t> ev_pool;
@@ -275,8 +277,21 @@ struct ModelT : public cfm_model {
       { EpiArgs e; e.bias = Lw.b_qkv; e.out = w.q; e.out2 = w.kv; e.row_off = kvoff; e.d = d;
         PROF(PC_QKV, gemm<T>(EPI_QKV, ACT_NONE, w.h, d, (const T*)Lw.qkv, d, rows, 3 * d, d, e, st)); }
       if (aci && aco) PROF(PC_CACHE, att_cache_out<T>(w.kv, cache_start, L, 2 * d, aco + (size_t)l * L * 2 * d, st));
-      PROF(PC_ATTN, chunk_attention<T>(w.q, w.kv, kv_rows, w.P + (size_t)l * prow_pad * d, p_rows, Lw.pu, Lw.pv, attd, natt, H,
-                              w.ao, st));
+      {
+        int r = -1;
+        hipEvent_t pb_;
+        prof_begin(PC_ATTN, st, &pb_);
+        if constexpr (sizeof(T) == 2) {
+          if (masked && use_ring_attention)
+            r = chunk_attention_masked_bf16(w.q, w.kv, kv_rows, w.P + (size_t)l * prow_pad * d, p_rows, Lw.pu, Lw.pv,
+                                            attd, natt, H, C, hh[PH_L] + C + hh[PH_R], w.ao, st, attn_diag);
+        }
+        if (r == -1)
+          r = chunk_attention<T>(w.q, w.kv, kv_rows, w.P + (size_t)l * prow_pad * d, p_rows, Lw.pu, Lw.pv, attd, natt,
+                                 H, w.ao, st);
+        KCHK(r);
+        prof_end(PC_ATTN, st, pb_);
+      }
       { EpiArgs e; e.bias = Lw.b_o; e.x = w.x; e.ldx = d;
         PROF(PC_OPROJ, gemm<T>(EPI_RESID, ACT_NONE, w.ao, d, (const T*)Lw.wo, d, rows, d, d, e, st)); }
       // convolution module
@@ -517,6 +532,8 @@ cfm_status cfm_model_set_option(cfm_model* m, const char* key, int64_t value) {
   if (!m || !key) return set_error(CFM_ERR_VALUE, "null argument");
   if (!std::strcmp(key, "max_layers")) { m->max_layers = (int)value; return CFM_OK; }
   if (!std::strcmp(key, "profile")) { m->prof_mask = (uint32_t)value; return CFM_OK; }
+  if (!std::strcmp(key, "ring_attention")) { m->use_ring_attention = value != 0; return CFM_OK; }
+  if (!std::strcmp(key, "attn_diag")) { m->attn_diag = (int)value; return CFM_OK; }
   if (!std::strcmp(key, "profile_reset")) {
     m->prof_collect();
     for (int i = 0; i < PC_N; ++i) { m->prof_ms[i] = 0; m->prof_n[i] = 0; }

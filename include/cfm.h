@@ -74,7 +74,9 @@ void cfm_model_destroy(cfm_model* m);
  *   "max_layers"    run only the first N blocks (-1 = all)
  *   "profile"       bitmask of kernel classes to bracket with HIP events on the launch
  *                   stream (bit i = class i of cfm_profile_read); 0 = off
- *   "profile_reset" clear the accumulated profile */
+ *   "profile_reset" clear the accumulated profile
+ *   "ring_attention" 1 (default) = bf16 masked batch uses the sliding-ring attention kernel,
+ *                   0 = the generic per-block kernel (A/B testing) */
 cfm_status cfm_model_set_option(cfm_model* m, const char* key, int64_t value);
 /* Per kernel class: name, accumulated milliseconds and launch count of the
  * event-bracketed launches since the last reset.  Host-synchronising (waits for

@@ -159,3 +159,21 @@ def test_large_12L(cfm, large, dtype):
     else:
         assert _rel_l2(o, g["out"]) <= BF16_RELL2
         assert (ids == g["ids"]).mean() >= 0.99
+
+
+@pytest.mark.parametrize("case", ["a", "c"])
+def test_ring_attention_matches_generic(cfm, small_models, small_g, case):
+    """bf16: the sliding-ring attention kernel against the generic per-block kernel."""
+    from chunkformer_amd.weights import synthetic_features
+    g = small_g
+    enc = small_models["bf16"]
+    lens = g[f"{case}_lens"].tolist()
+    C, L, R = (int(v) for v in g[f"{case}_clr"])
+    xs = synthetic_features(lens, int(g[f"{case}_seed"]))
+    outs = []
+    for ring in (1, 0):
+        enc.set_option("ring_attention", ring)
+        outs.append(enc.forward_parallel_chunk(xs, torch.tensor(lens, dtype=torch.int32), C, L, R)[0].cpu().numpy())
+    enc.set_option("ring_attention", 1)
+    assert _rel_l2(outs[0], outs[1]) <= 1e-2
+    assert _rel_l2(outs[0], g[f"{case}_out"]) <= BF16_RELL2
