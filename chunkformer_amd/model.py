@@ -1,0 +1,312 @@
+"""Host-side mirror of the reference `ChunkFormerModel` callers of the encoder hot path
+(chunkformer/chunkformer_model.py), on top of `ChunkFormerEncoder` (libcfm.so):
+
+  encode           chunkformer_model.py:256-274   padded batch -> (xs, xs_lens)
+  endless_decode   chunkformer_model.py:321-459   segment loop with att/cnn caches carried
+  batch_decode     chunkformer_model.py:462-552   duration-budget grouping -> masked batch -> CTC
+  from_pretrained  chunkformer_model.py:107-200   LOCAL directory only (no hub access)
+
+Audio loading + fbank (`_load_audio_and_extract_features`, 276-319) is outside the hot
+path and its dependencies (pydub, torchaudio) are absent: wherever the reference takes an
+`audio_path`, this mirror takes 80-dim fbank features -- a `[T, 80]` tensor, or a path to
+a `.npy` (loaded with allow_pickle=False) / `.pt` (torch.load weights_only=True) file.
+
+Text post-processing (remove_duplicates_and_blank, class2str, get_output,
+get_output_with_timestamps: chunkformer/utils/model_utils.py:23-221) is restated here so
+`char_dict` models return strings like the reference.
+"""
+from __future__ import annotations
+
+import json
+import math
+import os
+from typing import Dict, List, Optional, Sequence, Union
+
+import numpy as np
+import torch
+
+from .config import EncoderConfig
+from .encoder import ChunkFormerEncoder
+
+Features = Union[torch.Tensor, np.ndarray, str]
+
+
+# ----------------------------------------------------------------------------- text helpers
+def remove_duplicates_and_blank(hyp: Sequence[int], blank_id: int = 0) -> List[int]:
+    """model_utils.py:23-32: collapse repeats, then drop blanks."""
+    out: List[int] = []
+    prev = None
+    for t in hyp:
+        t = int(t)
+        if t != prev and t != blank_id:
+            out.append(t)
+        prev = t
+    return out
+
+
+def class2str(target: Sequence[int], char_dict: Dict[int, str]) -> str:
+    """model_utils.py:135-139."""
+    return "".join(char_dict[int(w)] for w in target).replace("▁", " ")
+
+
+def get_output(hyps, char_dict: Dict[int, str]) -> List[str]:
+    """model_utils.py:164-171 (asr_model branch)."""
+    return [class2str(remove_duplicates_and_blank([int(t) for t in h]), char_dict).strip() for h in hyps]
+
+
+def milliseconds_to_hhmmssms(ms: int) -> str:
+    """model_utils.py:142-161."""
+    h, rem = divmod(int(ms), 3600 * 1000)
+    m, rem = divmod(rem, 60 * 1000)
+    s, rem = divmod(rem, 1000)
+    return f"{h:02}:{m:02}:{s:02}:{rem:03}"
+
+
+def get_output_with_timestamps(hyps, char_dict: Dict[int, str], max_silence_duration: float) -> List[List[dict]]:
+    """model_utils.py:174-221: split a frame-level id stream (80 ms frames) into sentences at
+    silences of `max_silence_duration`.  `hyps` is a list of [T] or [T, 1] id tensors."""
+    decodes = []
+    max_silence = max_silence_duration // 0.08
+    for tokens in hyps:
+        tok = torch.as_tensor(tokens).cpu().reshape(len(tokens), -1)
+        start = end = prev_end = -1
+        silence = 0
+        per_time: List[int] = []
+        items: List[dict] = []
+        t = -1
+        for t in range(tok.shape[0]):
+            row = tok[t]
+            blank = row == 0
+            if bool(blank.all()):
+                silence += 1
+            else:
+                if start == -1 and end == -1:
+                    start = max(math.ceil((t + prev_end) / 2), t - 2) if prev_end != -1 else max(t - 2, 0)
+                silence = 0
+                per_time.extend(row[~blank].tolist())
+            if silence == max_silence and start != -1:
+                end = prev_end = t
+                items.append({"decode": get_output([per_time], char_dict)[0],
+                              "start": milliseconds_to_hhmmssms(start * 80),
+                              "end": milliseconds_to_hhmmssms(end * 80)})
+                per_time, start, end, silence = [], -1, -1, 0
+        if start != -1 and end == -1 and per_time:
+            items.append({"decode": get_output([per_time], char_dict)[0],
+                          "start": milliseconds_to_hhmmssms(start * 80),
+                          "end": milliseconds_to_hhmmssms(t * 80)})
+        decodes.append(items)
+    return decodes
+
+
+# ----------------------------------------------------------------------------- segment math
+def endless_segments(xs_len: int, C: int, L: int, R: int, total_batch_duration: float, num_blocks: int,
+                     kernel_size: int = 15, subsampling: int = 8):
+    """The segment schedule of endless_decode (chunkformer_model.py:355-435) as plain
+    integers: returns (truncated_context_size, [(start, stop, keep_trunc, last), ...]) where
+    frames [start, stop) feed one forward_parallel_chunk call and `keep_trunc` says whether
+    only the first `truncated_context_size` output frames are kept."""
+    lorder = kernel_size // 2
+    max_len = int(total_batch_duration // 0.01) // 2
+    mult = max_len // C // subsampling
+    trunc = C * mult
+    if trunc <= 0:
+        raise ValueError("total_batch_duration too small for one chunk")
+    r = max(R, lorder)
+    rel_right = (r + max(C, r) * (num_blocks - 1)) * subsampling
+    step = trunc * subsampling
+    segs = []
+    for idx in range((xs_len + step - 1) // step if xs_len > 0 else 0):
+        start = step * idx
+        end = min(step * (idx + 1) + 7, xs_len)
+        stop = min(end + rel_right, xs_len)
+        last = step * idx + rel_right >= xs_len
+        segs.append((start, stop, not last, last))
+        if last:
+            break
+    return trunc, segs
+
+
+def budget_groups(lens: Sequence[int], total_batch_duration: float) -> List[List[int]]:
+    """batch_decode's grouping (chunkformer_model.py:481-529): utterances are appended
+    until the frame budget int(tbd // 0.01) // 2 is used up (the utterance that crosses
+    it is included), then the group is flushed; the tail is flushed at the end."""
+    budget = int(total_batch_duration // 0.01) // 2
+    groups, cur, left = [], [], budget
+    for i, t in enumerate(lens):
+        cur.append(i)
+        left -= int(t)
+        if left <= 0 or i == len(lens) - 1:
+            groups.append(cur)
+            cur, left = [], budget
+    return groups
+
+
+def _load_features(x: Features) -> torch.Tensor:
+    if isinstance(x, torch.Tensor):
+        t = x
+    elif isinstance(x, np.ndarray):
+        t = torch.from_numpy(x)
+    elif isinstance(x, str):
+        if x.endswith(".npy"):
+            t = torch.from_numpy(np.load(x, allow_pickle=False))
+        elif x.endswith(".pt"):
+            t = torch.load(x, map_location="cpu", weights_only=True)
+        else:
+            raise ValueError(f"{x}: audio decoding/fbank is not part of this build; pass 80-dim fbank "
+                             "features ([T, 80] tensor, .npy or .pt)")
+    else:
+        raise TypeError(f"unsupported feature input {type(x)}")
+    if t.dim() == 3 and t.shape[0] == 1:
+        t = t[0]
+    if t.dim() != 2:
+        raise ValueError(f"features must be [T, F], got {tuple(t.shape)}")
+    return t.float()
+
+
+# ----------------------------------------------------------------------------- model
+class ChunkFormerModel:
+    """encoder + CTC head; the inference API of chunkformer_model.py on libcfm."""
+
+    def __init__(self, cfg: EncoderConfig, state_dict: Dict[str, torch.Tensor], dtype: str = "bf16", device=None,
+                 char_dict: Optional[Dict[int, str]] = None):
+        self.config = cfg
+        self.encoder = ChunkFormerEncoder(cfg, state_dict, device=device, dtype=dtype)
+        self.device = self.encoder.device
+        self.char_dict = char_dict
+
+    # ---------------------------------------------------------------- loading
+    @classmethod
+    def from_pretrained(cls, path: str, dtype: str = "bf16", device=None) -> "ChunkFormerModel":
+        """Local checkpoint directory in the reference layout (chunkformer_model.py:107-200):
+        config.yaml (yaml.safe_load), global_cmvn (JSON stats, utils/cmvn.py:23-45),
+        pytorch_model.{bin,pt,ckpt} (torch.load weights_only=True) or model.safetensors,
+        vocab.txt ("token id" per line, file_utils.py:62-69)."""
+        import yaml
+        if not os.path.isdir(path):
+            raise FileNotFoundError(f"{path}: only local checkpoint directories are supported (no hub access)")
+        with open(os.path.join(path, "config.yaml")) as f:
+            conf = yaml.safe_load(f)
+        sd: Dict[str, torch.Tensor] = {}
+        st = os.path.join(path, "model.safetensors")
+        if os.path.exists(st):
+            from safetensors.torch import load_file
+            sd = dict(load_file(st))
+        else:
+            for nm in ("pytorch_model.bin", "pytorch_model.pt", "pytorch_model.ckpt"):
+                p = os.path.join(path, nm)
+                if os.path.exists(p):
+                    sd = torch.load(p, map_location="cpu", weights_only=True)
+                    break
+            else:
+                raise FileNotFoundError(f"no checkpoint in {path}")
+        cmvn_path = os.path.join(path, "global_cmvn")
+        has_cmvn = os.path.exists(cmvn_path)
+        if has_cmvn:
+            mean, istd = load_json_cmvn(cmvn_path)
+            sd["encoder.global_cmvn.mean"] = torch.tensor(mean, dtype=torch.float32)
+            sd["encoder.global_cmvn.istd"] = torch.tensor(istd, dtype=torch.float32)
+        vocab = int(conf.get("output_dim", sd["ctc.ctc_lo.weight"].shape[0] if "ctc.ctc_lo.weight" in sd else 0))
+        cfg = EncoderConfig.from_encoder_conf(conf.get("encoder_conf", {}), input_dim=int(conf.get("input_dim", 80)),
+                                              output_dim=vocab, cmvn=has_cmvn)
+        char_dict = None
+        vp = os.path.join(path, "vocab.txt")
+        if os.path.exists(vp):
+            char_dict = {}
+            with open(vp, encoding="utf8") as f:
+                for line in f:
+                    arr = line.strip().split()
+                    if len(arr) != 2:
+                        raise AssertionError(f"bad vocab line {line!r}")
+                    char_dict[int(arr[1])] = arr[0]
+        return cls(cfg, sd, dtype=dtype, device=device, char_dict=char_dict)
+
+    # ---------------------------------------------------------------- API
+    def encode(self, xs: torch.Tensor, xs_lens: torch.Tensor, chunk_size: Optional[int] = None,
+               left_context_size: Optional[int] = None, right_context_size: Optional[int] = None, **kwargs):
+        """chunkformer_model.py:256-274."""
+        out, masks = self.encoder.forward_encoder(xs, xs_lens, chunk_size or 0, left_context_size or 0,
+                                                  right_context_size or 0)
+        return out, masks.squeeze(1).sum(-1)
+
+    @torch.no_grad()
+    def endless_decode(self, audio_path: Features, chunk_size: Optional[int] = 64,
+                       left_context_size: Optional[int] = 128, right_context_size: Optional[int] = 128,
+                       total_batch_duration: int = 1800, return_timestamps: bool = True,
+                       max_silence_duration: float = 0.5, return_encoder_out: bool = False):
+        """chunkformer_model.py:321-459.  Segments of `total_batch_duration` seconds (halved,
+        like the reference) go through forward_parallel_chunk with the attention/conv caches
+        and `offset` carried; the CTC argmax runs per segment on the kept rows (row-wise, so
+        identical to the reference's argmax over the concatenation).
+        Returns text (with char_dict) or ids [1, T', 1] like the reference; with
+        `return_encoder_out` also the concatenated encoder output [1, T', d] (fp32)."""
+        C = chunk_size if chunk_size is not None else 64
+        L = left_context_size if left_context_size is not None else 128
+        R = right_context_size if right_context_size is not None else 128
+        cfg, enc, dev = self.config, self.encoder, self.device
+        xs = _load_features(audio_path)
+        trunc, segs = endless_segments(xs.shape[0], C, L, R, total_batch_duration, cfg.num_blocks, cfg.kernel_size)
+        offset = torch.zeros(1, dtype=torch.int, device=dev)
+        att_cache = torch.zeros(cfg.num_blocks, L, cfg.n_heads, 2 * cfg.head_dim, device=dev)
+        cnn_cache = torch.zeros(cfg.num_blocks, cfg.d_model, cfg.conv_lorder, device=dev)
+        xs_dev = xs.to(dev)
+        ids, outs = [], []
+        for start, stop, keep_trunc, _ in segs:
+            x = xs_dev[start:stop]
+            x_len = torch.tensor([x.shape[0]], dtype=torch.int)
+            eo, el, _, att_cache, cnn_cache, offset = enc.forward_parallel_chunk(
+                [x], x_len, C, L, R, att_cache, cnn_cache, trunc, offset)
+            n = int(el[0])
+            eo = eo.reshape(-1, eo.shape[-1])[:n]
+            if keep_trunc:
+                eo = eo[:trunc]
+            offset = offset - n + eo.shape[0]
+            if cfg.vocab > 0:
+                ids.append(enc.ctc_log_softmax(eo, want_logp=False)[1])
+            if return_encoder_out:
+                outs.append(eo)
+        tokens = torch.cat(ids).long().reshape(1, -1, 1) if ids else None
+        if self.char_dict is not None and tokens is not None:
+            res = get_output_with_timestamps(tokens, self.char_dict, max_silence_duration)[0]
+            if not return_timestamps:
+                res = " ".join(item["decode"] for item in res).strip()
+        else:
+            res = tokens
+        if return_encoder_out:
+            return res, torch.cat(outs).unsqueeze(0)
+        return res
+
+    @torch.no_grad()
+    def batch_decode(self, audio_paths: List[Features], chunk_size: Optional[int] = 64,
+                     left_context_size: Optional[int] = 128, right_context_size: Optional[int] = 128,
+                     total_batch_duration: int = 1800):
+        """chunkformer_model.py:462-552 (asr_model branch): budget grouping, one masked-batch
+        encoder call per group, CTC argmax, per-utterance split to its subsampled length."""
+        C = chunk_size if chunk_size is not None else 64
+        L = left_context_size if left_context_size is not None else 128
+        R = right_context_size if right_context_size is not None else 128
+        feats = [_load_features(a) for a in audio_paths]
+        decodes = []
+        for grp in budget_groups([f.shape[0] for f in feats], total_batch_duration):
+            xs = [feats[i] for i in grp]
+            lens = torch.tensor([x.shape[0] for x in xs], dtype=torch.int)
+            offset = torch.zeros(len(xs), dtype=torch.int)
+            eo, el, n_chunks, _, _, _ = self.encoder.forward_parallel_chunk(xs, lens, C, L, R, offset=offset)
+            _, hyp = self.encoder.ctc_log_softmax(eo, want_logp=False)
+            hyps = [h.flatten()[: int(n)].long() for h, n in zip(hyp.split(n_chunks, dim=0), el.tolist())]
+            if self.char_dict is not None:
+                hyps = get_output(hyps, self.char_dict)
+            decodes.extend(hyps)
+        return decodes
+
+
+def load_json_cmvn(path: str):
+    """utils/cmvn.py:23-45: JSON {mean_stat, var_stat, frame_num} -> (mean, istd)."""
+    with open(path) as f:
+        st = json.load(f)
+    cnt = st["frame_num"]
+    mean = [m / cnt for m in st["mean_stat"]]
+    istd = []
+    for m, v in zip(mean, st["var_stat"]):
+        var = max(v / cnt - m * m, 1.0e-20)
+        istd.append(1.0 / math.sqrt(var))
+    return mean, istd

@@ -1,0 +1,85 @@
+"""Host logic of the ChunkFormerModel mirror (chunkformer_amd/model.py) -- no GPU:
+endless_decode segment schedule, batch_decode budget grouping, CTC text helpers."""
+import numpy as np
+import pytest
+
+from chunkformer_amd.model import (budget_groups, endless_segments, get_output, get_output_with_timestamps,
+                                   milliseconds_to_hhmmssms, remove_duplicates_and_blank, load_json_cmvn)
+
+
+def _reference_schedule(xs_len, C, L, R, tbd, nb, k=15, sub=8):
+    """Literal restatement of chunkformer_model.py:355-435's loop control."""
+    lorder = k // 2
+    mult = (int(tbd // 0.01) // 2) // C // sub
+    trunc = C * mult
+    rel = (max(R, lorder) + max(C, max(R, lorder)) * (nb - 1)) * sub
+    out = []
+    for idx, _ in enumerate(range(0, xs_len, trunc * sub)):
+        start = max(trunc * sub * idx, 0)
+        end = min(trunc * sub * (idx + 1) + 7, xs_len)
+        seg = (start, min(end + rel, xs_len))
+        last = C * mult * sub * idx + rel >= xs_len
+        out.append((seg, not last))
+        if last:
+            break
+    return trunc, out
+
+
+@pytest.mark.parametrize("xs_len,C,L,R,tbd,nb", [(6000, 16, 32, 32, 20, 2), (5_760_000, 64, 128, 128, 1800, 12),
+                                                 (5_760_000, 64, 128, 128, 14400, 12), (100, 64, 128, 128, 1800, 12),
+                                                 (101_895, 64, 128, 128, 1800, 12), (1, 8, 4, 4, 10, 1)])
+def test_endless_schedule_matches_reference_loop(xs_len, C, L, R, tbd, nb):
+    trunc, segs = endless_segments(xs_len, C, L, R, tbd, nb)
+    rt, ref = _reference_schedule(xs_len, C, L, R, tbd, nb)
+    assert trunc == rt
+    assert [((a, b), k) for a, b, k, _ in segs] == ref
+    assert not any(s[3] for s in segs[:-1])
+
+
+def test_endless_schedule_golden_segment_count(golden_dir):
+    g = np.load(f"{golden_dir}/small.npz")
+    C, L, R, tbd = (int(v) for v in g["endless_clrt"])
+    _, segs = endless_segments(6000, C, L, R, tbd, 2)
+    assert len(segs) == int(g["endless_nseg"])
+
+
+def test_endless_schedule_16h_counts():
+    # 65 segments at tbd=1800, 9 at tbd=14400
+    assert len(endless_segments(5_760_000, 64, 128, 128, 1800, 12)[1]) == 65
+    assert len(endless_segments(5_760_000, 64, 128, 128, 14400, 12)[1]) == 9
+    with pytest.raises(ValueError):
+        endless_segments(1000, 64, 128, 128, 0.5, 12)
+
+
+def test_budget_groups():
+    # budget = int(tbd // 0.01) // 2 frames; the utterance that crosses it closes the group
+    assert budget_groups([100, 100, 100], 3) == [[0, 1], [2]]          # budget 149
+    assert budget_groups([148, 1, 5], 3) == [[0, 1], [2]]          # int(3 // 0.01) // 2 = 149
+    assert budget_groups([149, 1, 5], 3) == [[0], [1, 2]]
+    assert budget_groups([10], 1800) == [[0]]
+    assert budget_groups([], 1800) == []
+    assert budget_groups([90000, 1, 2], 1800) == [[0], [1, 2]]
+
+
+def test_text_helpers():
+    assert remove_duplicates_and_blank([0, 1, 1, 0, 1, 2, 2, 0]) == [1, 1, 2]
+    assert remove_duplicates_and_blank([]) == []
+    cd = {0: "<blank>", 1: "▁xin", 2: "▁chào"}
+    assert get_output([[1, 1, 0, 2]], cd) == ["xin chào"]
+    assert milliseconds_to_hhmmssms(3_723_004) == "01:02:03:004"
+    toks = [0, 0, 1, 0, 0, 0, 0, 0, 0, 0, 0, 2, 2, 0]
+    import torch
+    res = get_output_with_timestamps([torch.tensor(toks).view(-1, 1)], cd, 0.5)[0]
+    # max_silence = 0.5 // 0.08 = 6 frames -> first sentence ends at t=8, second runs to the end
+    assert [r["decode"] for r in res] == ["xin", "chào"]
+    assert res[0]["start"] == "00:00:00:000" and res[0]["end"] == milliseconds_to_hhmmssms(8 * 80)
+    assert res[1]["start"] == milliseconds_to_hhmmssms(max(-(-(11 + 8) // 2), 9) * 80)
+
+
+def test_json_cmvn(tmp_path):
+    import json
+    p = tmp_path / "global_cmvn"
+    p.write_text(json.dumps({"mean_stat": [2.0, 4.0], "var_stat": [8.0, 20.0], "frame_num": 2}))
+    mean, istd = load_json_cmvn(str(p))
+    assert mean == [1.0, 2.0]
+    assert istd == pytest.approx([1 / np.sqrt(3.0), 1 / np.sqrt(6.0)])
