@@ -20,6 +20,9 @@ LIB = os.path.join(OUT, "libcfm.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("CFM_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wno-unused-result"]
+# frontend.hip: ReLU on MFMA outputs as a single v_max_f32 (no IEEE-mode canonicalisation);
+# the front-end never sees NaN inputs it would have to propagate
+FILE_FLAGS = {"frontend.hip": ["-fno-honor-nans", "-mno-amdgpu-ieee"]}
 
 
 def _sources():
@@ -37,7 +40,7 @@ def _compile(src: str, force: bool) -> str:
     newest_dep = max(os.path.getmtime(p) for p in [src] + _headers())
     if not force and os.path.exists(obj) and os.path.getmtime(obj) >= newest_dep:
         return obj
-    cmd = [HIPCC, *FLAGS, "-c", src, "-o", obj]
+    cmd = [HIPCC, *FLAGS, *FILE_FLAGS.get(os.path.basename(src), []), "-c", src, "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed on {src}:\n{r.stdout}\n{r.stderr}")

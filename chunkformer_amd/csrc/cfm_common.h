@@ -48,6 +48,28 @@ template <typename T> CFM_DEV typename Frag<T>::type ld8(const T* p) {
 template <typename T> CFM_DEV void st8(T* p, const typename Frag<T>::type& v) {
   *reinterpret_cast<typename Frag<T>::type*>(p) = v;
 }
+// 8 consecutive elements <-> f32[8]
+CFM_DEV void load8(const float* p, float* x) {
+  const f32x4 a = *reinterpret_cast<const f32x4*>(p), b = *reinterpret_cast<const f32x4*>(p + 4);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) { x[q] = a[q]; x[q + 4] = b[q]; }
+}
+CFM_DEV void load8(const bf16* p, float* x) {
+  const bf16x8 a = *reinterpret_cast<const bf16x8*>(p);
+#pragma unroll
+  for (int q = 0; q < 8; ++q) x[q] = (float)a[q];
+}
+CFM_DEV void store8(float* p, const float* x) {
+  *reinterpret_cast<f32x4*>(p) = (f32x4){x[0], x[1], x[2], x[3]};
+  *reinterpret_cast<f32x4*>(p + 4) = (f32x4){x[4], x[5], x[6], x[7]};
+}
+CFM_DEV void store8(bf16* p, const float* x) {
+  bf16x8 v;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) v[q] = (bf16)x[q];
+  *reinterpret_cast<bf16x8*>(p) = v;
+}
+
 template <typename T> CFM_DEV typename Frag<T>::type zero8() {
   typename Frag<T>::type z;
 #pragma unroll

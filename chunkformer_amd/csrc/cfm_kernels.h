@@ -60,7 +60,9 @@ int conv_dw_ln_silu(const T* glu, const int32_t* desc, int nblk, int d, const fl
 template <typename T>
 int frontend_conv0_dw(const float* feats, const int32_t* meta, int meta_stride, int nwin, int W,
                       const float* cmvn_mean, const float* cmvn_istd, const float* w0, const float* b0,
-                      const float* w1, const float* b1, int d, T* out, hipStream_t st);
+                      const float* w1, const float* b1, const float* wpack, int d, T* out, hipStream_t st);
+// per-channel [w0 taps 0..8 | w1 taps 0..8 | b0 | b1 | pad 2] (FE_WPACK floats) for the bf16 MFMA front-end
+constexpr int FE_WPACK = 24;
 template <typename T>
 int frontend_dw2(const T* in, int nwin, int T2, int d, const float* w, const float* b, T* out, hipStream_t st);
 

@@ -14,6 +14,7 @@
 // buffer at meta[PM_SRC_ROW], rows >= meta[PM_NVALID] are zero padding, and
 // CMVN is applied after padding exactly like the reference (padding rows
 // become -mean*istd).
+#include <cstdlib>
 #include "cfm_common.h"
 #include "cfm_kernels.h"
 
@@ -92,38 +93,174 @@ __global__ __launch_bounds__(256) void fe_conv0_dw_kernel(const float* __restric
   }
 }
 
-// dw2: [win][T2][19][d] -> [win][T3][9][d], depthwise 3x3 stride 2 + bias (no activation)
+// bf16 mode: conv0 + ReLU + dw1 fused on MFMA with no LDS round trip.  For a dw1 output
+// position (t2, f2) and channel c:
+//   out1 = b1[c] + sum_{s=(u,v)} w1[c][s] * relu(b0[c] + sum_e w0[c][e] * X[4t2+2u+e/3][4f2+2v+e%3])
+// Each wave owns 32 dw1 positions (MFMA rows) and sweeps all channels in tiles of 32 (MFMA
+// columns).  For each of the 9 dw1 taps s one v_mfma_f32_32x32x16_bf16 (K = the 9 conv0
+// taps, zero-padded to 16; bias-seeded accumulator) yields conv0 at the tap's positions,
+// and the VALU folds relu * w1[c][s] into the dw1 accumulator.  conv0 is recomputed per dw1
+// tap (2.25x its FLOPs, free on MFMA), which removes the conv0 tile in LDS, the barriers
+// between the two convolutions and the partial-row stores of a channel-split grid.
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+constexpr int FE_POS_BLOCK = 128;                     // dw1 positions per block (4 waves x 32)
+constexpr int FE_XROWS = 4 * ((FE_POS_BLOCK - 1) / FE_F2 + 2) + 3;   // staged input rows (>= 4*span + 7)
+
+__global__ __launch_bounds__(256, 3) void fe_conv0_dw_mfma_kernel(const float* __restrict__ feats,
+                                                               const int32_t* __restrict__ meta, int meta_stride,
+                                                               int W, int T2, const float* __restrict__ cm,
+                                                               const float* __restrict__ ci,
+                                                               const float* __restrict__ wpack, int d,
+                                                               bf16* __restrict__ out) {
+  __shared__ float xin[FE_XROWS * FE_F0];
+  const int tid = threadIdx.x;
+  const int win = blockIdx.y;
+  const int P = T2 * FE_F2;
+  const int p0 = blockIdx.x * FE_POS_BLOCK;
+  const int r0 = 4 * (p0 / FE_F2);   // first staged input row
+  const int src = meta[(size_t)win * meta_stride + PM_SRC_ROW];
+  const int nvalid = min(meta[(size_t)win * meta_stride + PM_NVALID], W);
+  for (int idx = tid; idx < FE_XROWS * FE_F0; idx += 256) {
+    const int r = idx / FE_F0, f = idx - r * FE_F0, gr = r0 + r;
+    float v = gr < nvalid ? feats[(size_t)(src + gr) * FE_F0 + f] : 0.f;
+    if (cm) v = (v - cm[f]) * ci[f];   // CMVN after padding, like cmvn.py:32-43 on the padded window
+    xin[idx] = v;
+  }
+  __syncthreads();
+  const int lane = tid & 63, wv = tid >> 6, hh = lane >> 5, n = lane & 31;
+  const int pw = p0 + wv * 32;   // this wave's first position
+  if (pw >= P) return;
+  // A fragments: row m = n -> position pw + n; k = 8*hh + j = conv0 tap e (e < 9)
+  bf16x8 xa[9];
+  {
+    const int pos = min(pw + n, P - 1);   // rows past P are computed and discarded
+    const int t2 = pos / FE_F2, f2 = pos - t2 * FE_F2;
+    const float* xb = xin + (4 * t2 - r0) * FE_F0 + 4 * f2;
+#pragma unroll
+    for (int s = 0; s < 9; ++s) {
+      const float* xs = xb + 2 * (s / 3) * FE_F0 + 2 * (s % 3);
+      if (hh == 0) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) xa[s][j] = (bf16)xs[(j / 3) * FE_F0 + j % 3];
+      } else {
+        xa[s][0] = (bf16)xs[2 * FE_F0 + 2];
+#pragma unroll
+        for (int j = 1; j < 8; ++j) xa[s][j] = (bf16)0.f;
+      }
+    }
+  }
+  // per-channel-tile weights, software-pipelined one tile ahead
+  bf16x8 wb;
+  float wk[9], bc0, bc1;
+  auto load_w = [&](int c) {
+    const f32x4* wp = reinterpret_cast<const f32x4*>(wpack + (size_t)c * FE_WPACK);
+    const f32x4 q0 = wp[0], q1 = wp[1], q2 = wp[2], q3 = wp[3], q4 = wp[4], q5 = wp[5];
+    // lanes of the upper half need only conv0 tap 8 (k = 8); the rest of K is zero
+    const float t[9] = {q0[0], q0[1], q0[2], q0[3], q1[0], q1[1], q1[2], q1[3], q2[0]};
+#pragma unroll
+    for (int j = 0; j < 8; ++j) wb[j] = (bf16)(hh ? (j ? 0.f : t[8]) : t[j]);
+    const float u[9] = {q2[1], q2[2], q2[3], q3[0], q3[1], q3[2], q3[3], q4[0], q4[1]};
+#pragma unroll
+    for (int s = 0; s < 9; ++s) wk[s] = u[s];
+    bc0 = q4[2];
+    bc1 = q4[3];
+    (void)q5;
+  };
+  load_w(n);
+  for (int ct = 0; ct < d; ct += 32) {
+    const int c = ct + n;
+    const bf16x8 wbc = wb;
+    float wkc[9];
+#pragma unroll
+    for (int s = 0; s < 9; ++s) wkc[s] = wk[s];
+    f32x16 seed, o;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      seed[r] = bc0;
+      o[r] = bc1;
+    }
+    if (ct + 32 < d) load_w(c + 32);
+    // taps are software-pipelined one deep: MFMA s+1 is issued before tap s's
+    // relu/FMA work; the asm after each tap's VALU (it consumes the dw1 accumulators and
+    // re-defines the B operand the MFMA two taps ahead reads) keeps at most two
+    // accumulator sets live
+    bf16x8 wcur = wbc;
+    typedef float f32x2 __attribute__((ext_vector_type(2)));
+    f32x16 acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xa[0], wcur, seed, 0, 0, 0);
+#pragma unroll
+    for (int s = 0; s < 9; ++s) {
+      f32x16 nxt;
+      if (s + 1 < 9) nxt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xa[s + 1], wcur, seed, 0, 0, 0);
+      const f32x2 w2 = (f32x2){wkc[s], wkc[s]};
+#pragma unroll
+      for (int r = 0; r < 16; r += 2) {
+        // one v_max_f32 each: this file is built with IEEE mode off (build.py), so no
+        // canonicalising max is added in front
+        const f32x2 a2 = (f32x2){fmaxf(acc[r], 0.f), fmaxf(acc[r + 1], 0.f)};
+        const f32x2 o2 = __builtin_elementwise_fma(w2, a2, (f32x2){o[r], o[r + 1]});
+        o[r] = o2[0];
+        o[r + 1] = o2[1];
+      }
+      asm volatile("" : "+v"(wcur), "+v"(o));
+      if (s + 1 < 9) acc = nxt;
+    }
+    bf16* ow = out + (size_t)win * P * d;   // 32-bit offsets inside the window
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int pos = pw + 8 * (r >> 2) + 4 * hh + (r & 3);
+      if (pos < P) ow[pos * d + c] = (bf16)o[r];
+    }
+  }
+}
+
+// dw2: [win][T2][19][d] -> [win][T3][9][d], depthwise 3x3 stride 2 + bias (no activation), taps
+// tap-major w[9][d];
+// one thread per (output position, 8 channels): 16-B (bf16) / 2x16-B (f32) loads
 template <typename T>
 __global__ __launch_bounds__(256) void fe_dw2_kernel(const T* __restrict__ in, int nwin, int T2, int T3, int d,
                                                      const float* __restrict__ w, const float* __restrict__ b,
                                                      T* __restrict__ out) {
+  const int d8 = d >> 3;
   const size_t idx = (size_t)blockIdx.x * 256 + threadIdx.x;
-  const size_t total = (size_t)nwin * T3 * FE_F3 * d;
+  const size_t total = (size_t)nwin * T3 * FE_F3 * d8;
   if (idx >= total) return;
-  const int c = idx % d;
-  size_t r = idx / d;
+  const int c = (int)(idx % d8) * 8;
+  size_t r = idx / d8;
   const int f3 = r % FE_F3; r /= FE_F3;
   const int t3 = r % T3;
   const size_t wn = r / T3;
   const T* ib = in + ((wn * T2 + 2 * t3) * FE_F2 + 2 * f3) * d + c;
-  float a = b[c];
+  float a[8];
+  load8(b + c, a);
 #pragma unroll
   for (int u = 0; u < 3; ++u)
 #pragma unroll
-    for (int v = 0; v < 3; ++v) a = fmaf(w[c * 9 + u * 3 + v], to_f32(ib[((size_t)u * FE_F2 + v) * d]), a);
-  out[idx] = from_f32<T>(a);
+    for (int v = 0; v < 3; ++v) {
+      float x[8], wt[8];
+      load8(ib + ((size_t)u * FE_F2 + v) * d, x);
+      load8(w + (size_t)(u * 3 + v) * d + c, wt);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) a[q] = fmaf(wt[q], x[q], a[q]);
+    }
+  store8(out + idx * 8, a);
 }
 
 template <typename T>
 int frontend_conv0_dw(const float* feats, const int32_t* meta, int meta_stride, int nwin, int W,
                       const float* cmvn_mean, const float* cmvn_istd, const float* w0, const float* b0,
-                      const float* w1, const float* b1, int d, T* out, hipStream_t st) {
+                      const float* w1, const float* b1, const float* wpack, int d, T* out, hipStream_t st) {
   if (nwin <= 0) return 0;
   const int T1 = (W - 3) / 2 + 1, T2 = (T1 - 3) / 2 + 1;
   if (T2 <= 0 || d % FE_CG) return (int)hipErrorInvalidValue;
   const dim3 grid((T2 + FE_T2_TILE - 1) / FE_T2_TILE, nwin);
-  hipLaunchKernelGGL((fe_conv0_dw_kernel<T>), grid, dim3(256), 0, st, feats, meta, meta_stride, W, T2, cmvn_mean,
-                     cmvn_istd, w0, b0, w1, b1, d, out);
+  if constexpr (std::is_same<T, bf16>::value) {
+    if (d % 32) return (int)hipErrorInvalidValue;
+    hipLaunchKernelGGL(fe_conv0_dw_mfma_kernel, dim3((T2 * FE_F2 + FE_POS_BLOCK - 1) / FE_POS_BLOCK, nwin), dim3(256),
+                       0, st, feats, meta, meta_stride, W, T2, cmvn_mean, cmvn_istd, wpack, d, out);
+  } else {
+    hipLaunchKernelGGL((fe_conv0_dw_kernel<T>), grid, dim3(256), 0, st, feats, meta, meta_stride, W, T2, cmvn_mean,
+                       cmvn_istd, w0, b0, w1, b1, d, out);
+  }
   CFM_CHECK_LAUNCH();
   return 0;
 }
@@ -131,7 +268,8 @@ int frontend_conv0_dw(const float* feats, const int32_t* meta, int meta_stride, 
 template <typename T>
 int frontend_dw2(const T* in, int nwin, int T2, int d, const float* w, const float* b, T* out, hipStream_t st) {
   const int T3 = (T2 - 3) / 2 + 1;
-  const size_t total = (size_t)nwin * T3 * FE_F3 * d;
+  if (d % 8) return (int)hipErrorInvalidValue;
+  const size_t total = (size_t)nwin * T3 * FE_F3 * (d / 8);
   if (total == 0) return 0;
   hipLaunchKernelGGL((fe_dw2_kernel<T>), dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, in, nwin, T2, T3, d,
                      w, b, out);
@@ -140,9 +278,9 @@ int frontend_dw2(const T* in, int nwin, int T2, int d, const float* w, const flo
 }
 
 template int frontend_conv0_dw<float>(const float*, const int32_t*, int, int, int, const float*, const float*,
-                                      const float*, const float*, const float*, const float*, int, float*, hipStream_t);
+                                      const float*, const float*, const float*, const float*, const float*, int, float*, hipStream_t);
 template int frontend_conv0_dw<bf16>(const float*, const int32_t*, int, int, int, const float*, const float*,
-                                     const float*, const float*, const float*, const float*, int, bf16*, hipStream_t);
+                                     const float*, const float*, const float*, const float*, const float*, int, bf16*, hipStream_t);
 template int frontend_dw2<float>(const float*, int, int, int, const float*, const float*, float*, hipStream_t);
 template int frontend_dw2<bf16>(const bf16*, int, int, int, const float*, const float*, bf16*, hipStream_t);
 

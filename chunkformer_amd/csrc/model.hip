@@ -70,7 +70,7 @@ struct LayerW {
 };
 
 struct FrontW {
-  float *cm = nullptr, *ci = nullptr, *w0, *b0, *w1, *b1, *w2, *b2, *b_pw1, *b_pw2, *b_out;
+  float *cm = nullptr, *ci = nullptr, *w0, *b0, *w1, *b1, *w2, *b2, *b_pw1, *b_pw2, *b_out, *wpack;
   void *pw1, *pw2, *wout;
   float *an_w, *an_b;
   void* ctc_w = nullptr;
@@ -233,7 +233,7 @@ struct ModelT : public cfm_model {
     for (int g0 = 0; g0 < nwin; g0 += G) {
       const int ng = std::min(G, nwin - g0);
       PROF(PC_FE_CONV, frontend_conv0_dw<T>(feats, meta + (size_t)g0 * PLAN_REC, PLAN_REC, ng, Wn, fe.cm, fe.ci, fe.w0, fe.b0,
-                                fe.w1, fe.b1, d, w.feA, st));
+                                fe.w1, fe.b1, fe.wpack, d, w.feA, st));
       EpiArgs e1; e1.bias = fe.b_pw1; e1.out = w.feB; e1.ldo = d;
       PROF(PC_FE_GEMM, gemm<T>(EPI_STORE, ACT_RELU, w.feA, d, (const T*)fe.pw1, d, ng * T2 * 19, d, d, e1, st));
       PROF(PC_FE_DW2, frontend_dw2<T>(w.feB, ng, T2, d, fe.w2, fe.b2, w.feA, st));
@@ -404,9 +404,29 @@ static cfm_status build_model(const cfm_config& cfg, const HostW& hw, int device
     put_f32(hw.get(E + "embed.conv.0.bias", d), d, &F.b0);
     put_f32(hw.get(E + "embed.conv.2.weight", (int64_t)d * 9), (size_t)d * 9, &F.w1);
     put_f32(hw.get(E + "embed.conv.2.bias", d), d, &F.b1);
+    {   // conv0 + dw1 weights packed per channel for the MFMA front-end
+      const float *a = hw.get(E + "embed.conv.0.weight", (int64_t)d * 9), *ab = hw.get(E + "embed.conv.0.bias", d);
+      const float *b = hw.get(E + "embed.conv.2.weight", (int64_t)d * 9), *bb = hw.get(E + "embed.conv.2.bias", d);
+      std::vector<float> w((size_t)d * FE_WPACK, 0.f);
+      for (int c = 0; c < d; ++c) {
+        for (int e = 0; e < 9; ++e) {
+          w[(size_t)c * FE_WPACK + e] = a[c * 9 + e];
+          w[(size_t)c * FE_WPACK + 9 + e] = b[c * 9 + e];
+        }
+        w[(size_t)c * FE_WPACK + 18] = ab[c];
+        w[(size_t)c * FE_WPACK + 19] = bb[c];
+      }
+      put_f32(w.data(), w.size(), &F.wpack);
+    }
     put_T(vec(E + "embed.conv.3.weight", (int64_t)d * d), &F.pw1);
     put_f32(hw.get(E + "embed.conv.3.bias", d), d, &F.b_pw1);
-    put_f32(hw.get(E + "embed.conv.5.weight", (int64_t)d * 9), (size_t)d * 9, &F.w2);
+    {   // dw2 taps tap-major [9][d] (16-B channel vectors per tap for fe_dw2_kernel)
+      const float* s = hw.get(E + "embed.conv.5.weight", (int64_t)d * 9);
+      std::vector<float> w((size_t)d * 9);
+      for (int c = 0; c < d; ++c)
+        for (int e = 0; e < 9; ++e) w[(size_t)e * d + c] = s[(size_t)c * 9 + e];
+      put_f32(w.data(), w.size(), &F.w2);
+    }
     put_f32(hw.get(E + "embed.conv.5.bias", d), d, &F.b2);
     put_T(vec(E + "embed.conv.6.weight", (int64_t)d * d), &F.pw2);
     put_f32(hw.get(E + "embed.conv.6.bias", d), d, &F.b_pw2);
