@@ -214,35 +214,56 @@ __global__ __launch_bounds__(256, 3) void fe_conv0_dw_mfma_kernel(const float* _
 }
 
 // dw2: [win][T2][19][d] -> [win][T3][9][d], depthwise 3x3 stride 2 + bias (no activation), taps
-// tap-major w[9][d];
-// one thread per (output position, 8 channels): 16-B (bf16) / 2x16-B (f32) loads
+// tap-major w[9][d].  One thread per (window, f3, 8 channels) walks down the window's rows:
+// input row 2*t3+2 is kept in registers for the next output row, so every input byte is
+// read from HBM once (16-B loads, 64 lanes = one 1-KB channel row).
 template <typename T>
 __global__ __launch_bounds__(256) void fe_dw2_kernel(const T* __restrict__ in, int nwin, int T2, int T3, int d,
                                                      const float* __restrict__ w, const float* __restrict__ b,
                                                      T* __restrict__ out) {
   const int d8 = d >> 3;
   const size_t idx = (size_t)blockIdx.x * 256 + threadIdx.x;
-  const size_t total = (size_t)nwin * T3 * FE_F3 * d8;
+  const size_t total = (size_t)nwin * FE_F3 * d8;
   if (idx >= total) return;
   const int c = (int)(idx % d8) * 8;
-  size_t r = idx / d8;
-  const int f3 = r % FE_F3; r /= FE_F3;
-  const int t3 = r % T3;
-  const size_t wn = r / T3;
-  const T* ib = in + ((wn * T2 + 2 * t3) * FE_F2 + 2 * f3) * d + c;
-  float a[8];
-  load8(b + c, a);
+  const size_t r = idx / d8;
+  const int f3 = r % FE_F3;
+  const size_t wn = r / FE_F3;
+  float wt[9][8], bias[8];
 #pragma unroll
-  for (int u = 0; u < 3; ++u)
+  for (int e = 0; e < 9; ++e) load8(w + (size_t)e * d + c, wt[e]);
+  load8(b + c, bias);
+  const T* ib = in + (wn * T2 * FE_F2 + 2 * f3) * d + c;
+  T* ob = out + (wn * T3 * FE_F3 + f3) * d + c;
+  float top[3][8];   // input row 2*t3 (carried from the previous output row)
+#pragma unroll
+  for (int v = 0; v < 3; ++v) load8(ib + (size_t)v * d, top[v]);
+  for (int t3 = 0; t3 < T3; ++t3) {
+    float mid[3][8], bot[3][8];
+    const T* rb = ib + (size_t)(2 * t3 + 1) * FE_F2 * d;
 #pragma unroll
     for (int v = 0; v < 3; ++v) {
-      float x[8], wt[8];
-      load8(ib + ((size_t)u * FE_F2 + v) * d, x);
-      load8(w + (size_t)(u * 3 + v) * d + c, wt);
-#pragma unroll
-      for (int q = 0; q < 8; ++q) a[q] = fmaf(wt[q], x[q], a[q]);
+      load8(rb + (size_t)v * d, mid[v]);
+      load8(rb + (size_t)(FE_F2 + v) * d, bot[v]);
     }
-  store8(out + idx * 8, a);
+    float a[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      float s = bias[q];
+#pragma unroll
+      for (int v = 0; v < 3; ++v) {
+        s = fmaf(wt[v][q], top[v][q], s);
+        s = fmaf(wt[3 + v][q], mid[v][q], s);
+        s = fmaf(wt[6 + v][q], bot[v][q], s);
+      }
+      a[q] = s;
+    }
+    store8(ob + (size_t)t3 * FE_F3 * d, a);
+#pragma unroll
+    for (int v = 0; v < 3; ++v)
+#pragma unroll
+      for (int q = 0; q < 8; ++q) top[v][q] = bot[v][q];
+  }
 }
 
 template <typename T>
@@ -269,8 +290,8 @@ template <typename T>
 int frontend_dw2(const T* in, int nwin, int T2, int d, const float* w, const float* b, T* out, hipStream_t st) {
   const int T3 = (T2 - 3) / 2 + 1;
   if (d % 8) return (int)hipErrorInvalidValue;
-  const size_t total = (size_t)nwin * T3 * FE_F3 * (d / 8);
-  if (total == 0) return 0;
+  const size_t total = (size_t)nwin * FE_F3 * (d / 8);
+  if (total == 0 || T3 <= 0) return 0;
   hipLaunchKernelGGL((fe_dw2_kernel<T>), dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, in, nwin, T2, T3, d,
                      w, b, out);
   CFM_CHECK_LAUNCH();
