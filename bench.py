@@ -93,6 +93,21 @@ def cpu_baseline(lens_all, budget_s: float = 12.0):
                       f"workload's first utterances (capped at 60k frames each), {frames} frames in {t_tot:.1f} s"}
 
 
+def committed_traffic(cls: str = "ffn_w1_gemm"):
+    """HBM bytes per launch of the roofline kernel from the newest committed PMC summary
+    (profiles/<round>_traffic.json, made by tools/profile_round.sh with rocprofv3
+    FETCH_SIZE/WRITE_SIZE passes on this same workload); None if absent."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_traffic.json")))
+    if not files:
+        return None, None
+    try:
+        ent = json.load(open(files[-1]))["kernels"].get(cls)
+        return (float(ent[0]["hbm_bytes_per_launch"]), os.path.relpath(files[-1], ROOT)) if ent else (None, None)
+    except (OSError, ValueError, KeyError, IndexError):
+        return None, None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -156,6 +171,9 @@ def main():
     avg_s = (ms1 / max(n1, 1)) / 1e3
     achieved = fl_launch / avg_s / 1e12 if n1 else None
     peak = PEAK_TFLOPS[args.dtype]
+    traffic, traffic_src = committed_traffic() if args.dtype == "bf16" else (None, None)
+    # compulsory bytes of one w_1 launch: A [rows, d] + out [rows, ff] bf16 + W [ff, d] bf16 + bias
+    alg_bytes = 2.0 * (rows * LARGE.d_model + rows * LARGE.ffn_dim + LARGE.ffn_dim * LARGE.d_model) + 4 * LARGE.ffn_dim
     step_flops = n_chunks * flops_per_chunk(LARGE) + LARGE.num_blocks * 2 * (L + 2 * C + R - 1) * LARGE.d_model ** 2
 
     # ---- CTC head + the one collective (timed separately; not part of `value`)
@@ -207,7 +225,10 @@ def main():
             "roofline": {"bound": "mfma", "kernel": "ffn_w1_gemm (gemm_kernel<bf16,EPI_STORE,SiLU>)"
                          if args.dtype == "bf16" else "ffn_w1_gemm (gemm_kernel<float,EPI_STORE,SiLU>)",
                          "achieved": round(achieved, 1) if achieved else None, "peak": peak, "unit": "TFLOP/s",
-                         "frac": round(achieved / peak, 4) if achieved else None, "traffic": None,
+                         "frac": round(achieved / peak, 4) if achieved else None, "traffic": traffic,
+                         "traffic_unit": "HBM bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)",
+                         "traffic_source": traffic_src,
+                         "algorithmic_bytes_per_launch": alg_bytes,
                          "flops_per_launch": fl_launch, "avg_launch_ms": round(avg_s * 1e3, 4), "launches": n1},
             "step_tflops_algorithmic": round(step_flops / (dt_max / args.steps) / 1e12, 1),
             "ctc_ms": round(ctc_ms, 3),

@@ -12,6 +12,7 @@
 // One wave per output row, lane l owns channels [l*VPL, l*VPL+VPL); the LN
 // statistics are wave reductions.  Depthwise weights are stored tap-major
 // [15][d] so every tap is one coalesced vector load.
+#include <type_traits>
 #include "cfm_common.h"
 #include "cfm_kernels.h"
 
@@ -93,10 +94,94 @@ __global__ __launch_bounds__(256) void conv_dw_ln_silu_kernel(const T* __restric
   }
 }
 
+// bf16: one block per descriptor.  The window's GLU rows are staged once into LDS with
+// 16-B loads (rows outside the unmasked columns [j_lo, j_hi) are zero there, which is the
+// reference's where(mask_pad, x, 0)), so each HBM row is read by one block instead of by
+// every output-row wave on whichever XCD it lands.  Each wave then produces 8 consecutive
+// output rows: per tap one weight vector load and 8 LDS row reads, LayerNorm statistics
+// as wave reductions, SiLU, one vector store per row.
+template <int VPL>
+__global__ __launch_bounds__(512) void conv_dw_ln_silu_lds_kernel(const bf16* __restrict__ glu,
+                                                                  const int32_t* __restrict__ desc,
+                                                                  const float* __restrict__ wdw,
+                                                                  const float* __restrict__ bdw,
+                                                                  const float* __restrict__ lnw,
+                                                                  const float* __restrict__ lnb, float eps,
+                                                                  bf16* __restrict__ out) {
+  constexpr int d = VPL * 64;
+  constexpr int MAXJ = 64 + 14;
+  constexpr int RW = 8;   // output rows per wave
+  typedef bf16 bvec __attribute__((ext_vector_type(VPL)));
+  __shared__ __attribute__((aligned(16))) bf16 win[MAXJ * d];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int32_t* D = desc + (size_t)blockIdx.x * CD_INTS;
+  const int out_row0 = D[CD_OUT_ROW0], nout = D[CD_NOUT], src0 = D[CD_SRC_ROW0];
+  const int nj = nout + 14;
+  const int jlo = max(D[CD_J_LO], 0), jhi = min(D[CD_J_HI], nj);
+  constexpr int V8 = d / 8;   // 16-B vectors per row
+  for (int idx = tid; idx < nj * V8; idx += 512) {
+    const int j = idx / V8, v = idx % V8;
+    u32x4 val = (u32x4){0u, 0u, 0u, 0u};
+    if (j >= jlo && j < jhi) val = *reinterpret_cast<const u32x4*>(glu + (size_t)(src0 + j) * d + v * 8);
+    *reinterpret_cast<u32x4*>(win + j * d + v * 8) = val;
+  }
+  __syncthreads();
+  const int i0 = w * RW;
+  if (i0 >= nout) return;
+  const int c0 = lane * VPL;
+  float acc[RW][VPL];
+#pragma unroll
+  for (int e = 0; e < VPL; ++e) {
+    const float bv = bdw[c0 + e];
+#pragma unroll
+    for (int r = 0; r < RW; ++r) acc[r][e] = bv;
+  }
+  for (int t = 0; t < 15; ++t) {
+    float wv[VPL];
+    VecIO<float, VPL>::load(wdw + t * d + c0, wv);
+#pragma unroll
+    for (int r = 0; r < RW; ++r) {
+      const bvec x = *reinterpret_cast<const bvec*>(win + min(i0 + r + t, nj - 1) * d + c0);
+#pragma unroll
+      for (int e = 0; e < VPL; ++e) acc[r][e] = fmaf((float)x[e], wv[e], acc[r][e]);
+    }
+  }
+  float lw[VPL], lb[VPL];
+#pragma unroll
+  for (int e = 0; e < VPL; ++e) {
+    lw[e] = lnw[c0 + e];
+    lb[e] = lnb[c0 + e];
+  }
+#pragma unroll
+  for (int r = 0; r < RW; ++r) {
+    if (i0 + r >= nout) break;
+    float sum = 0.f;
+#pragma unroll
+    for (int e = 0; e < VPL; ++e) sum += acc[r][e];
+    const float mean = wave_sum(sum) / d;
+    float q = 0.f;
+#pragma unroll
+    for (int e = 0; e < VPL; ++e) { const float t = acc[r][e] - mean; q += t * t; }
+    const float rstd = rsqrtf(wave_sum(q) / d + eps);
+    bvec o;
+#pragma unroll
+    for (int e = 0; e < VPL; ++e) o[e] = (bf16)silu_f((acc[r][e] - mean) * rstd * lw[e] + lb[e]);
+    *reinterpret_cast<bvec*>(out + (size_t)(out_row0 + i0 + r) * d + c0) = o;
+  }
+}
+
 template <typename T>
 int conv_dw_ln_silu(const T* glu, const int32_t* desc, int nblk, int d, const float* wdw_t, const float* bdw,
                     const float* lnw, const float* lnb, float eps, T* out, hipStream_t st) {
   if (nblk <= 0) return 0;
+  if constexpr (std::is_same<T, bf16>::value) {
+    if (d == 128) hipLaunchKernelGGL((conv_dw_ln_silu_lds_kernel<2>), dim3(nblk), dim3(512), 0, st, glu, desc, wdw_t, bdw, lnw, lnb, eps, out);
+    else if (d == 256) hipLaunchKernelGGL((conv_dw_ln_silu_lds_kernel<4>), dim3(nblk), dim3(512), 0, st, glu, desc, wdw_t, bdw, lnw, lnb, eps, out);
+    else if (d == 512) hipLaunchKernelGGL((conv_dw_ln_silu_lds_kernel<8>), dim3(nblk), dim3(512), 0, st, glu, desc, wdw_t, bdw, lnw, lnb, eps, out);
+    else return (int)hipErrorInvalidValue;
+    CFM_CHECK_LAUNCH();
+    return 0;
+  }
   const dim3 grid(nblk, 4);   // 4 x 4 waves stride over the (<= 64) rows of a block
   if (d == 128) hipLaunchKernelGGL((conv_dw_ln_silu_kernel<T, 2>), grid, dim3(256), 0, st, glu, desc, wdw_t, bdw, lnw, lnb, eps, out);
   else if (d == 256) hipLaunchKernelGGL((conv_dw_ln_silu_kernel<T, 4>), grid, dim3(256), 0, st, glu, desc, wdw_t, bdw, lnw, lnb, eps, out);
