@@ -30,16 +30,21 @@ int gemm(int epi, int act, const T* A, int lda, const T* W, int ldw, int M, int 
 void gemm_force_small_tiles(int v);
 
 // LayerNorm over d (eps) of f32 rows -> T rows; optional 0/1 row mask on the output.
+// fused residual add of the previous sub-block: x += alpha * ymask[row] * y (y null = none)
+template <typename T> struct ResidAdd {
+  const T* y = nullptr;
+  float alpha = 1.f;
+  const uint8_t* ymask = nullptr;
+};
 template <typename T>
-int layernorm(const float* x, int M, int d, const float* w, const float* b, float eps, T* out,
+int layernorm(float* x, const ResidAdd<T>& ra, int M, int d, const float* w, const float* b, float eps, T* out,
               const uint8_t* rowmask, hipStream_t st);
-// y = LN1(x) written back to x (f32); then out = LN2(y) as T (LN2 may be null: out = y as T).
 template <typename T>
-int layernorm2(float* x, int M, int d, const float* w1, const float* b1, const float* w2, const float* b2,
-               float eps, T* out, hipStream_t st);
-// same, with the second output in f32 (final after_norm)
-int layernorm2_f32(float* x, int M, int d, const float* w1, const float* b1, const float* w2, const float* b2,
-                   float eps, float* out, hipStream_t st);
+int layernorm2(float* x, const ResidAdd<T>& ra, int M, int d, const float* w1, const float* b1, const float* w2,
+               const float* b2, float eps, T* out, hipStream_t st);
+template <typename T>
+int layernorm2_f32(float* x, const ResidAdd<T>& ra, int M, int d, const float* w1, const float* b1, const float* w2,
+                   const float* b2, float eps, float* out, hipStream_t st);
 
 // chunk attention (attention.hip)
 template <typename T>

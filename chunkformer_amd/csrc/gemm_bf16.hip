@@ -42,43 +42,125 @@ CFM_DEV bf16x8 lds_read_b128(unsigned addr) {
   return v;
 }
 
-// Epilogue of one 16x16 accumulator (n-tile i, m-tile j) with swapped operands: lane (fr, g)
-// holds C[m = mt0 + fr][n = nt0 + 4g .. 4g+3].  qkv_base / qkv_ld locate the 16-col tile inside q / k / v.
+// fast activations for the bf16 epilogue: v_exp_f32 + v_rcp_f32 (the results are rounded to bf16)
+CFM_DEV float fast_sigmoid(float x) { return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-1.4426950408889634f * x)); }
+CFM_DEV float fast_silu(float x) { return x * fast_sigmoid(x); }
+
+// Tile epilogue of one wave (128 x 64 of C).  With swapped operands acc[i][j] (n-block i of 16
+// columns, m-block j of 16 rows) holds, in lane (fr, g), C[m = 16j + fr][n = 16i + 4g .. 4g+3];
+// the bias is already in the accumulator (it seeds the tile).  bf16 outputs: n-blocks are
+// paired (2p, 2p+1) and packed, then one v_permlane16_swap per dword leaves every lane with
+// 8 contiguous columns, so each row segment of 32 columns is ONE 16-B store per lane
+// (16 stores per tile instead of 32 8-B ones; the store tail is issue-bound).
+//   after the swap lane g holds columns 16*(2p) + 16*(g & 1) + 8*(g >> 1) .. +7
+typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
+CFM_DEV unsigned pack_bf16x2(float a, float b) {
+  typedef bf16 b2 __attribute__((ext_vector_type(2)));
+  return __builtin_bit_cast(unsigned, (b2){(bf16)a, (bf16)b});
+}
+template <int ACT>
+CFM_DEV f32x4 act4(f32x4 v) {
+  if constexpr (ACT == ACT_RELU) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
+  }
+  if constexpr (ACT == ACT_SILU) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = fast_silu(v[r]);
+  }
+  return v;
+}
+// store two packed 16-column blocks (x = block 0, y = block 1) of row `row` after the swap
+CFM_DEV void store_pair16(bf16* base, size_t ld, int row, int g, u32x2_t x, u32x2_t y) {
+  const auto r0 = __builtin_amdgcn_permlane16_swap(x[0], y[0], false, false);
+  const auto r1 = __builtin_amdgcn_permlane16_swap(x[1], y[1], false, false);
+  const int col = 16 * (g & 1) + 8 * (g >> 1);
+  *reinterpret_cast<u32x4*>(base + (size_t)row * ld + col) = (u32x4){r0[0], r1[0], r0[1], r1[1]};
+}
+
 template <int EPI, int ACT>
-CFM_DEV void epi16(const f32x4& c, const f32x4& cgate, const f32x4& bias, const f32x4& bgate, bf16* qkv_base,
-                   size_t qkv_ld, int m, int n, int M, const EpiArgs& ep) {
-  if (m >= M) return;
-  f32x4 v = c + bias;
-  if constexpr (EPI == EPI_STORE) {
-    if constexpr (ACT == ACT_RELU) {
+CFM_DEV void tile_epilogue(f32x4 (&acc)[4][8], int tm, int tn, int wm, int wn, int fr, int g, int M,
+                           const EpiArgs& ep) {
+  const int m0 = tm * 256 + wm * 128 + fr;   // row of j = 0
+  const int nw = tn * 256 + wn * 64;          // first column of this wave
+  if constexpr (EPI == EPI_STORE_F32 || EPI == EPI_RESID) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
-    }
-    if constexpr (ACT == ACT_SILU) {
+    for (int i = 0; i < 4; ++i) {
+      const int n = nw + i * 16 + 4 * g;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = silu_f(v[r]);
+      for (int j = 0; j < 8; ++j) {
+        const int m = m0 + 16 * j;
+        if (m >= M) continue;
+        if constexpr (EPI == EPI_STORE_F32) {
+          *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(ep.out) + (size_t)(m + ep.row_off) * ep.ldo + n) =
+              ep.alpha * acc[i][j];
+        } else {
+          const float mk = ep.rowmask ? (float)ep.rowmask[m] : 1.f;
+          f32x4* xp = reinterpret_cast<f32x4*>(ep.x + (size_t)m * ep.ldx + n);
+          *xp = *xp + (ep.alpha * mk) * acc[i][j];
+        }
+      }
     }
-    *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(ep.out) + (size_t)(m + ep.row_off) * ep.ldo + n) =
-        (bf16x4){(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
-  } else if constexpr (EPI == EPI_STORE_F32) {
-    *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(ep.out) + (size_t)(m + ep.row_off) * ep.ldo + n) = ep.alpha * v;
-  } else if constexpr (EPI == EPI_RESID) {
-    const float mk = ep.rowmask ? (float)ep.rowmask[m] : 1.f;
-    f32x4* xp = reinterpret_cast<f32x4*>(ep.x + (size_t)m * ep.ldx + n);
-    *xp = *xp + (ep.alpha * mk) * v;
-  } else if constexpr (EPI == EPI_QKV) {
-    *reinterpret_cast<bf16x4*>(qkv_base + (size_t)m * qkv_ld) = (bf16x4){(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
   } else if constexpr (EPI == EPI_GLU) {
-    const f32x4 gt = cgate + bgate;
-    const int ch = ((n >> 5) << 4) + (n & 15);
-    bf16x4 o;
+    // n-blocks (0,1) = (a, gate) of output channels c0 .. c0+15, (2,3) of c0+16 .. c0+31
+    bf16* base = reinterpret_cast<bf16*>(ep.out) + (size_t)ep.row_off * ep.ldo + nw / 2;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) o[r] = (bf16)(v[r] * sigmoid_f(gt[r]));
-    *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(ep.out) + (size_t)(m + ep.row_off) * ep.ldo + ch) = o;
+    for (int j = 0; j < 8; ++j) {
+      const int m = m0 + 16 * j;
+      u32x2_t o[2];
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        const f32x4 a = acc[2 * p][j], gt = acc[2 * p + 1][j];
+        o[p] = (u32x2_t){pack_bf16x2(a[0] * fast_sigmoid(gt[0]), a[1] * fast_sigmoid(gt[1])),
+                         pack_bf16x2(a[2] * fast_sigmoid(gt[2]), a[3] * fast_sigmoid(gt[3]))};
+      }
+      if (m < M) store_pair16(base, ep.ldo, m, g, o[0], o[1]);
+    }
+  } else {   // EPI_STORE / EPI_QKV: bf16 out, pairs (0,1) and (2,3)
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const int n = nw + 32 * p;   // a 32-column span never crosses a 64-column head group
+      bf16* base;
+      size_t ld;
+      if constexpr (EPI == EPI_QKV) {
+        const int d = ep.d;
+        if (n < d) {
+          base = reinterpret_cast<bf16*>(ep.out) + n;
+          ld = d;
+        } else {
+          const int c2 = n - d, which = c2 >= d ? 1 : 0, cc = c2 - which * d;
+          base = reinterpret_cast<bf16*>(ep.out2) + (size_t)ep.row_off * 2 * d + (cc >> 6) * 128 + which * 64 + (cc & 63);
+          ld = 2 * (size_t)d;
+        }
+      } else {
+        base = reinterpret_cast<bf16*>(ep.out) + (size_t)ep.row_off * ep.ldo + n;
+        ld = ep.ldo;
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int m = m0 + 16 * j;
+        const f32x4 v0 = act4<ACT>(acc[2 * p][j]), v1 = act4<ACT>(acc[2 * p + 1][j]);
+        const u32x2_t x = (u32x2_t){pack_bf16x2(v0[0], v0[1]), pack_bf16x2(v0[2], v0[3])};
+        const u32x2_t y = (u32x2_t){pack_bf16x2(v1[0], v1[1]), pack_bf16x2(v1[2], v1[3])};
+        if (m < M) store_pair16(base, ld, m, g, x, y);
+      }
+    }
   }
 }
 
-// DIAG: 0 = normal; 1 = skip MFMAs (DMA + epilogue only); 2 = skip DMA inside the loop (MFMA on stale LDS)
+// seed the accumulators of tile (tm, tn) with the bias (every m-block of an n-block gets the same 4 values)
+CFM_DEV void seed_bias(f32x4 (&acc)[4][8], const float* bias, int tn, int wn, int g) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const f32x4 b = bias ? *reinterpret_cast<const f32x4*>(bias + tn * 256 + wn * 64 + i * 16 + 4 * g)
+                         : (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = b;
+  }
+}
+
+// DIAG: 0 = normal; 1 = skip MFMAs (DMA + epilogue only); 2 = skip DMA inside the loop (MFMA on stale LDS);
+// 3 = skip the epilogue (no bias/activation/stores)
 template <int EPI, int ACT, int DIAG = 0>
 __global__ __launch_bounds__(512, 1) void gemm_bf16_256_kernel(const bf16* __restrict__ A, int lda,
                                                                const bf16* __restrict__ W, int ldw, int M, int N,
@@ -138,11 +220,7 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_256_kernel(const bf16* __res
     }
   };
 
-  f32x4 acc[4][8];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  f32x4 acc[4][8];   // seeded with the bias at every tile's first K-step
 
   const int key = (fr >> 1) & 7;   // XOR key of fragment rows (row & 15 == fr)
   const int wrow = (wn * 64 + fr) * 128, arow = (wm * 128 + fr) * 128;
@@ -178,41 +256,12 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_256_kernel(const bf16* __res
 #pragma unroll
       for (int ss = 0; ss < 2; ++ss) {
         // ================= LOAD segment: (epilogue of the previous tile), fragments of (s, ss), DMA issue
-        if (ss == 0 && epi_t >= 0) {
-          const int tm = epi_t / nbn, tn = epi_t - tm * nbn;
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const int n = tn * 256 + wn * 64 + i * 16 + 4 * g;
-            if constexpr (EPI == EPI_GLU) {
-              if (i & 1) continue;
-            }
-            const f32x4 bias = ep.bias ? *reinterpret_cast<const f32x4*>(ep.bias + n) : (f32x4){0.f, 0.f, 0.f, 0.f};
-            f32x4 bgate = (f32x4){0.f, 0.f, 0.f, 0.f};
-            if constexpr (EPI == EPI_GLU) bgate = *reinterpret_cast<const f32x4*>(ep.bias + n + 16);
-            bf16* qb = nullptr;
-            size_t qld = 0;
-            if constexpr (EPI == EPI_QKV) {
-              const int d = ep.d;
-              if (n < d) {
-                qb = reinterpret_cast<bf16*>(ep.out) + n;
-                qld = d;
-              } else {
-                const int c2 = n - d, which = c2 >= d ? 1 : 0, cc = c2 - which * d;
-                qb = reinterpret_cast<bf16*>(ep.out2) + (size_t)ep.row_off * 2 * d + (cc >> 6) * 128 + which * 64 + (cc & 63);
-                qld = 2 * (size_t)d;
-              }
-            }
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-              epi16<EPI, ACT>(acc[i][j], acc[(EPI == EPI_GLU) ? i + 1 : i][j], bias, bgate, qb, qld,
-                              tm * 256 + wm * 128 + j * 16 + fr, n, M, ep);
-            }
+        if (ss == 0 && kt == 0) {
+          if (epi_t >= 0) {
+            if constexpr (DIAG != 3) tile_epilogue<EPI, ACT>(acc, epi_t / nbn, epi_t % nbn, wm, wn, fr, g, M, ep);
+            epi_t = -1;
           }
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int j = 0; j < 8; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-          epi_t = -1;
+          seed_bias(acc, ep.bias, t % nbn, wn, g);
         }
         const int pos = ((ss * 4 + g) ^ key) << 4;
         const unsigned wa = lds_base + (unsigned)(ws - smem) + wrow + pos;
@@ -259,41 +308,12 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_256_kernel(const bf16* __res
     }
   }
   // last tile's epilogue (no MFMA partner left), then rebalance the barrier count
-  if (epi_t >= 0) {
-    const int tm = epi_t / nbn, tn = epi_t - tm * nbn;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int n = tn * 256 + wn * 64 + i * 16 + 4 * g;
-      if constexpr (EPI == EPI_GLU) {
-        if (i & 1) continue;
-      }
-      const f32x4 bias = ep.bias ? *reinterpret_cast<const f32x4*>(ep.bias + n) : (f32x4){0.f, 0.f, 0.f, 0.f};
-      f32x4 bgate = (f32x4){0.f, 0.f, 0.f, 0.f};
-      if constexpr (EPI == EPI_GLU) bgate = *reinterpret_cast<const f32x4*>(ep.bias + n + 16);
-      bf16* qb = nullptr;
-      size_t qld = 0;
-      if constexpr (EPI == EPI_QKV) {
-        const int d = ep.d;
-        if (n < d) {
-          qb = reinterpret_cast<bf16*>(ep.out) + n;
-          qld = d;
-        } else {
-          const int c2 = n - d, which = c2 >= d ? 1 : 0, cc = c2 - which * d;
-          qb = reinterpret_cast<bf16*>(ep.out2) + (size_t)ep.row_off * 2 * d + (cc >> 6) * 128 + which * 64 + (cc & 63);
-          qld = 2 * (size_t)d;
-        }
-      }
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        epi16<EPI, ACT>(acc[i][j], acc[(EPI == EPI_GLU) ? i + 1 : i][j], bias, bgate, qb, qld,
-                        tm * 256 + wm * 128 + j * 16 + fr, n, M, ep);
-    }
-  }
+  if (epi_t >= 0 && DIAG != 3) tile_epilogue<EPI, ACT>(acc, epi_t / nbn, epi_t % nbn, wm, wn, fr, g, M, ep);
   if (grp == 0) asm volatile("s_barrier" ::: "memory");
 }
 
 template <int EPI, int ACT>
-static int launch256(const bf16* A, int lda, const bf16* W, int ldw, int M, int N, int K, const EpiArgs& ep,
+static int launch256(const bf16* A, int lda, const bf16* W, int ldw, int M, int N, int K, const EpiArgs& ep_in,
                      hipStream_t st) {
   const int tiles = ((M + 255) / 256) * (N / 256);
   static int n_cu = 0;
@@ -306,10 +326,14 @@ static int launch256(const bf16* A, int lda, const bf16* W, int ldw, int M, int 
   const int grid = tiles <= n_cu ? tiles : n_cu;   // persistent: one 512-thread block per CU
   static int diag = -1;
   if (diag < 0) { const char* e = getenv("CFM_GEMM_DIAG"); diag = e ? atoi(e) : 0; }
+  const EpiArgs& ep = ep_in;
   if (diag == 1)
     hipLaunchKernelGGL((gemm_bf16_256_kernel<EPI, ACT, 1>), dim3(grid), dim3(512), 0, st, A, lda, W, ldw, M, N, K, ep);
   else if (diag == 2)
     hipLaunchKernelGGL((gemm_bf16_256_kernel<EPI, ACT, 2>), dim3(grid), dim3(512), 0, st, A, lda, W, ldw, M, N, K, ep);
+  else if (diag == 3)
+    hipLaunchKernelGGL((gemm_bf16_256_kernel<EPI, ACT, 3>), dim3(grid), dim3(512), 0, st, A, lda, W, ldw, M, N, K, ep);
+
   else
     hipLaunchKernelGGL((gemm_bf16_256_kernel<EPI, ACT, 0>), dim3(grid), dim3(512), 0, st, A, lda, W, ldw, M, N, K, ep);
   CFM_CHECK_LAUNCH();

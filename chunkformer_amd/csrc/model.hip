@@ -170,7 +170,7 @@ struct ModelT : public cfm_model {
 
   struct WS {
     float* x;
-    T *h, *hid, *q, *kv, *ao, *glu, *cv, *P, *pos, *feA, *feB;
+    T *h, *hid, *q, *kv, *ao, *glu, *cv, *y, *P, *pos, *feA, *feB;
   };
 
   WS carve(void* base, const int32_t* h, size_t* total) const {
@@ -190,6 +190,7 @@ struct ModelT : public cfm_model {
     w.ao = c.take<T>(rows * d);
     w.glu = c.take<T>((size_t)h[PH_GLUROWS] * d);
     w.cv = c.take<T>(rows * d);
+    w.y = c.take<T>(rows * d);
     w.P = c.take<T>((size_t)nb * prow_pad * d);
     w.pos = c.take<T>(prow_pad * d);
     w.feA = c.take<T>(G * T2 * 19 * d);
@@ -260,19 +261,23 @@ struct ModelT : public cfm_model {
     const int natt = hh[PH_NATT], nconv = hh[PH_NCONV];
     const int cache_start = std::min(trunc, rows);   // new cache = stream[:trunc + L][-L:] (attention.py:467)
     if (nl == 0) {
-      PROF(PC_LN, layernorm2_f32(w.x, rows, d, fe.an_w, fe.an_b, nullptr, nullptr, eps, out, st));
+      PROF(PC_LN, layernorm2_f32<T>(w.x, ResidAdd<T>(), rows, d, fe.an_w, fe.an_b, nullptr, nullptr, eps, out, st));
       return CFM_OK;
     }
-    PROF(PC_LN, layernorm<T>(w.x, rows, d, layers[0].ln_ffm_w, layers[0].ln_ffm_b, eps, w.h, nullptr, st));
+    PROF(PC_LN, layernorm<T>(w.x, ResidAdd<T>(), rows, d, layers[0].ln_ffm_w, layers[0].ln_ffm_b, eps, w.h, nullptr, st));
+    // Each residual branch's last GEMM writes y = branch + bias (bf16/T); the residual add
+    // x += alpha * y (0.5 for the FFNs, encoder_layer.py:196/246; the conv branch masked by
+    // the padded path's row mask) is fused into the LayerNorm that reads x next.
+    auto resid = [&](float alpha, const uint8_t* ym) { ResidAdd<T> r; r.y = w.y; r.alpha = alpha; r.ymask = ym; return r; };
     for (int l = 0; l < nl; ++l) {
       const LayerW& Lw = layers[l];
       // macaron FFN (x 0.5)
       { EpiArgs e; e.bias = Lw.b_ff1m; e.out = w.hid; e.ldo = ff;
         PROF(PC_FFN1, gemm<T>(EPI_STORE, ACT_SILU, w.h, d, (const T*)Lw.ff1m, d, rows, ff, d, e, st)); }
-      { EpiArgs e; e.bias = Lw.b_ff2m; e.x = w.x; e.ldx = d; e.alpha = 0.5f;
-        PROF(PC_FFN2, gemm<T>(EPI_RESID, ACT_NONE, w.hid, ff, (const T*)Lw.ff2m, ff, rows, d, ff, e, st)); }
+      { EpiArgs e; e.bias = Lw.b_ff2m; e.out = w.y; e.ldo = d;
+        PROF(PC_FFN2, gemm<T>(EPI_STORE, ACT_NONE, w.hid, ff, (const T*)Lw.ff2m, ff, rows, d, ff, e, st)); }
       // MHSA
-      PROF(PC_LN, layernorm<T>(w.x, rows, d, Lw.ln_mha_w, Lw.ln_mha_b, eps, w.h, nullptr, st));
+      PROF(PC_LN, layernorm<T>(w.x, resid(0.5f, nullptr), rows, d, Lw.ln_mha_w, Lw.ln_mha_b, eps, w.h, nullptr, st));
       if (aci) PROF(PC_CACHE, att_cache_in<T>(aci + (size_t)l * L * 2 * d, L, 2 * d, w.kv, st));
       { EpiArgs e; e.bias = Lw.b_qkv; e.out = w.q; e.out2 = w.kv; e.row_off = kvoff; e.d = d;
         PROF(PC_QKV, gemm<T>(EPI_QKV, ACT_NONE, w.h, d, (const T*)Lw.qkv, d, rows, 3 * d, d, e, st)); }
@@ -292,29 +297,31 @@ struct ModelT : public cfm_model {
         KCHK(r);
         prof_end(PC_ATTN, st, pb_);
       }
-      { EpiArgs e; e.bias = Lw.b_o; e.x = w.x; e.ldx = d;
-        PROF(PC_OPROJ, gemm<T>(EPI_RESID, ACT_NONE, w.ao, d, (const T*)Lw.wo, d, rows, d, d, e, st)); }
+      { EpiArgs e; e.bias = Lw.b_o; e.out = w.y; e.ldo = d;
+        PROF(PC_OPROJ, gemm<T>(EPI_STORE, ACT_NONE, w.ao, d, (const T*)Lw.wo, d, rows, d, d, e, st)); }
       // convolution module
-      PROF(PC_LN, layernorm<T>(w.x, rows, d, Lw.ln_conv_w, Lw.ln_conv_b, eps, w.h, masked ? nullptr : rmask, st));
+      PROF(PC_LN, layernorm<T>(w.x, resid(1.f, nullptr), rows, d, Lw.ln_conv_w, Lw.ln_conv_b, eps, w.h,
+                               masked ? nullptr : rmask, st));
       if (cci) PROF(PC_CACHE, cnn_cache_in<T>(cci + (size_t)l * d * 7, d, 7, w.glu, st));
       { EpiArgs e; e.bias = Lw.b_pw1; e.out = w.glu; e.ldo = d; e.row_off = gluoff;
         PROF(PC_PW1, gemm<T>(EPI_GLU, ACT_NONE, w.h, d, (const T*)Lw.pw1, d, rows, 2 * d, d, e, st)); }
       if (cci && cco) PROF(PC_CACHE, cnn_cache_out<T>(w.glu, cache_start, d, 7, cco + (size_t)l * d * 7, st));
       PROF(PC_CONV, conv_dw_ln_silu<T>(w.glu, convd, nconv, d, Lw.dw_t, Lw.b_dw, Lw.cn_w, Lw.cn_b, eps, w.cv, st));
-      { EpiArgs e; e.bias = Lw.b_pw2; e.x = w.x; e.ldx = d; e.rowmask = rmask;
-        PROF(PC_PW2, gemm<T>(EPI_RESID, ACT_NONE, w.cv, d, (const T*)Lw.pw2, d, rows, d, d, e, st)); }
+      { EpiArgs e; e.bias = Lw.b_pw2; e.out = w.y; e.ldo = d;
+        PROF(PC_PW2, gemm<T>(EPI_STORE, ACT_NONE, w.cv, d, (const T*)Lw.pw2, d, rows, d, d, e, st)); }
       // FFN (x 0.5)
-      PROF(PC_LN, layernorm<T>(w.x, rows, d, Lw.ln_ff_w, Lw.ln_ff_b, eps, w.h, nullptr, st));
+      PROF(PC_LN, layernorm<T>(w.x, resid(1.f, rmask), rows, d, Lw.ln_ff_w, Lw.ln_ff_b, eps, w.h, nullptr, st));
       { EpiArgs e; e.bias = Lw.b_ff1; e.out = w.hid; e.ldo = ff;
         PROF(PC_FFN1, gemm<T>(EPI_STORE, ACT_SILU, w.h, d, (const T*)Lw.ff1, d, rows, ff, d, e, st)); }
-      { EpiArgs e; e.bias = Lw.b_ff2; e.x = w.x; e.ldx = d; e.alpha = 0.5f;
-        PROF(PC_FFN2, gemm<T>(EPI_RESID, ACT_NONE, w.hid, ff, (const T*)Lw.ff2, ff, rows, d, ff, e, st)); }
+      { EpiArgs e; e.bias = Lw.b_ff2; e.out = w.y; e.ldo = d;
+        PROF(PC_FFN2, gemm<T>(EPI_STORE, ACT_NONE, w.hid, ff, (const T*)Lw.ff2, ff, rows, d, ff, e, st)); }
       // norm_final (+ next layer's macaron LN, or after_norm)
       if (l + 1 < nl)
-        PROF(PC_LN, layernorm2<T>(w.x, rows, d, Lw.ln_fin_w, Lw.ln_fin_b, layers[l + 1].ln_ffm_w, layers[l + 1].ln_ffm_b, eps,
-                           w.h, st));
+        PROF(PC_LN, layernorm2<T>(w.x, resid(0.5f, nullptr), rows, d, Lw.ln_fin_w, Lw.ln_fin_b, layers[l + 1].ln_ffm_w,
+                                  layers[l + 1].ln_ffm_b, eps, w.h, st));
       else
-        PROF(PC_LN, layernorm2_f32(w.x, rows, d, Lw.ln_fin_w, Lw.ln_fin_b, fe.an_w, fe.an_b, eps, out, st));
+        PROF(PC_LN, layernorm2_f32<T>(w.x, resid(0.5f, nullptr), rows, d, Lw.ln_fin_w, Lw.ln_fin_b, fe.an_w, fe.an_b, eps,
+                                      out, st));
     }
     return CFM_OK;
   }

@@ -68,8 +68,34 @@ CFM_DEV void store_row(bf16* p, const float (&v)[VPL]) {
   }
 }
 
+template <int VPL>
+CFM_DEV void load_row(const bf16* p, float (&v)[VPL]) {
+  if constexpr (VPL == 2) {
+    const bf16x2 t = *reinterpret_cast<const bf16x2*>(p);
+    v[0] = (float)t[0]; v[1] = (float)t[1];
+  } else {
+#pragma unroll
+    for (int e = 0; e < VPL; e += 4) {
+      const bf16x4 t = *reinterpret_cast<const bf16x4*>(p + e);
+      v[e] = (float)t[0]; v[e + 1] = (float)t[1]; v[e + 2] = (float)t[2]; v[e + 3] = (float)t[3];
+    }
+  }
+}
+
+// x += alpha * ymask[row] * y (the sub-block's residual add, encoder_layer.py:196-246), written back
+template <typename TY, int VPL>
+CFM_DEV void resid_add(float (&v)[VPL], float* xp, const ResidAdd<TY>& ra, int row, int lane) {
+  if (!ra.y) return;
+  float yv[VPL];
+  load_row<VPL>(ra.y + (size_t)row * (VPL * 64) + lane * VPL, yv);
+  const float a = ra.alpha * (ra.ymask ? (float)ra.ymask[row] : 1.f);
+#pragma unroll
+  for (int e = 0; e < VPL; ++e) v[e] = fmaf(a, yv[e], v[e]);
+  store_row<VPL>(xp, v);
+}
+
 template <typename T, int VPL>
-__global__ __launch_bounds__(256) void ln_kernel(const float* __restrict__ x, int M, const float* __restrict__ w,
+__global__ __launch_bounds__(256) void ln_kernel(float* __restrict__ x, ResidAdd<T> ra, int M, const float* __restrict__ w,
                                                  const float* __restrict__ b, float eps, T* __restrict__ out,
                                                  const uint8_t* __restrict__ rowmask) {
   const int lane = threadIdx.x & 63;
@@ -77,7 +103,9 @@ __global__ __launch_bounds__(256) void ln_kernel(const float* __restrict__ x, in
   if (row >= M) return;
   constexpr int d = VPL * 64;
   float v[VPL];
-  load_row<VPL>(x + (size_t)row * d + lane * VPL, v);
+  float* xp = x + (size_t)row * d + lane * VPL;
+  load_row<VPL>(xp, v);
+  resid_add<T, VPL>(v, xp, ra, row, lane);
   ln_row<VPL>(v, d, w, b, eps, lane);
   if (rowmask && !rowmask[row]) {
 #pragma unroll
@@ -86,10 +114,11 @@ __global__ __launch_bounds__(256) void ln_kernel(const float* __restrict__ x, in
   store_row<VPL>(out + (size_t)row * d + lane * VPL, v);
 }
 
-template <typename TO, int VPL>
-__global__ __launch_bounds__(256) void ln2_kernel(float* __restrict__ x, int M, const float* __restrict__ w1,
-                                                  const float* __restrict__ b1, const float* __restrict__ w2,
-                                                  const float* __restrict__ b2, float eps, TO* __restrict__ out) {
+template <typename TY, typename TO, int VPL>
+__global__ __launch_bounds__(256) void ln2_kernel(float* __restrict__ x, ResidAdd<TY> ra, int M,
+                                                  const float* __restrict__ w1, const float* __restrict__ b1,
+                                                  const float* __restrict__ w2, const float* __restrict__ b2, float eps,
+                                                  TO* __restrict__ out) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= M) return;
@@ -97,6 +126,13 @@ __global__ __launch_bounds__(256) void ln2_kernel(float* __restrict__ x, int M, 
   float v[VPL];
   float* xp = x + (size_t)row * d + lane * VPL;
   load_row<VPL>(xp, v);
+  if (ra.y) {
+    float yv[VPL];
+    load_row<VPL>(ra.y + (size_t)row * d + lane * VPL, yv);
+    const float a = ra.alpha * (ra.ymask ? (float)ra.ymask[row] : 1.f);
+#pragma unroll
+    for (int e = 0; e < VPL; ++e) v[e] = fmaf(a, yv[e], v[e]);
+  }
   ln_row<VPL>(v, d, w1, b1, eps, lane);
   store_row<VPL>(xp, v);
   if (w2) ln_row<VPL>(v, d, w2, b2, eps, lane);
@@ -104,42 +140,51 @@ __global__ __launch_bounds__(256) void ln2_kernel(float* __restrict__ x, int M, 
 }
 
 template <typename T>
-int layernorm(const float* x, int M, int d, const float* w, const float* b, float eps, T* out,
+int layernorm(float* x, const ResidAdd<T>& ra, int M, int d, const float* w, const float* b, float eps, T* out,
               const uint8_t* rowmask, hipStream_t st) {
   if (M <= 0) return 0;
-  if (d == 128) hipLaunchKernelGGL((ln_kernel<T, 2>), dim3((M + 3) / 4), dim3(256), 0, st, x, M, w, b, eps, out, rowmask);
-  else if (d == 256) hipLaunchKernelGGL((ln_kernel<T, 4>), dim3((M + 3) / 4), dim3(256), 0, st, x, M, w, b, eps, out, rowmask);
-  else if (d == 512) hipLaunchKernelGGL((ln_kernel<T, 8>), dim3((M + 3) / 4), dim3(256), 0, st, x, M, w, b, eps, out, rowmask);
+  if (d == 128) hipLaunchKernelGGL((ln_kernel<T, 2>), dim3((M + 3) / 4), dim3(256), 0, st, x, ra, M, w, b, eps, out, rowmask);
+  else if (d == 256) hipLaunchKernelGGL((ln_kernel<T, 4>), dim3((M + 3) / 4), dim3(256), 0, st, x, ra, M, w, b, eps, out, rowmask);
+  else if (d == 512) hipLaunchKernelGGL((ln_kernel<T, 8>), dim3((M + 3) / 4), dim3(256), 0, st, x, ra, M, w, b, eps, out, rowmask);
   else return (int)hipErrorInvalidValue;
   CFM_CHECK_LAUNCH();
   return 0;
 }
 
-template <typename T>
-static int ln2_launch(float* x, int M, int d, const float* w1, const float* b1, const float* w2, const float* b2,
-                      float eps, T* out, hipStream_t st) {
+template <typename TY, typename TO>
+static int ln2_launch(float* x, const ResidAdd<TY>& ra, int M, int d, const float* w1, const float* b1, const float* w2,
+                      const float* b2, float eps, TO* out, hipStream_t st) {
   if (M <= 0) return 0;
-  if (d == 128) hipLaunchKernelGGL((ln2_kernel<T, 2>), dim3((M + 3) / 4), dim3(256), 0, st, x, M, w1, b1, w2, b2, eps, out);
-  else if (d == 256) hipLaunchKernelGGL((ln2_kernel<T, 4>), dim3((M + 3) / 4), dim3(256), 0, st, x, M, w1, b1, w2, b2, eps, out);
-  else if (d == 512) hipLaunchKernelGGL((ln2_kernel<T, 8>), dim3((M + 3) / 4), dim3(256), 0, st, x, M, w1, b1, w2, b2, eps, out);
+  if (d == 128) hipLaunchKernelGGL((ln2_kernel<TY, TO, 2>), dim3((M + 3) / 4), dim3(256), 0, st, x, ra, M, w1, b1, w2, b2, eps, out);
+  else if (d == 256) hipLaunchKernelGGL((ln2_kernel<TY, TO, 4>), dim3((M + 3) / 4), dim3(256), 0, st, x, ra, M, w1, b1, w2, b2, eps, out);
+  else if (d == 512) hipLaunchKernelGGL((ln2_kernel<TY, TO, 8>), dim3((M + 3) / 4), dim3(256), 0, st, x, ra, M, w1, b1, w2, b2, eps, out);
   else return (int)hipErrorInvalidValue;
   CFM_CHECK_LAUNCH();
   return 0;
 }
 
 template <typename T>
-int layernorm2(float* x, int M, int d, const float* w1, const float* b1, const float* w2, const float* b2, float eps,
-               T* out, hipStream_t st) {
-  return ln2_launch<T>(x, M, d, w1, b1, w2, b2, eps, out, st);
+int layernorm2(float* x, const ResidAdd<T>& ra, int M, int d, const float* w1, const float* b1, const float* w2,
+               const float* b2, float eps, T* out, hipStream_t st) {
+  return ln2_launch<T, T>(x, ra, M, d, w1, b1, w2, b2, eps, out, st);
 }
-int layernorm2_f32(float* x, int M, int d, const float* w1, const float* b1, const float* w2, const float* b2,
-                   float eps, float* out, hipStream_t st) {
-  return ln2_launch<float>(x, M, d, w1, b1, w2, b2, eps, out, st);
+template <typename T>
+int layernorm2_f32(float* x, const ResidAdd<T>& ra, int M, int d, const float* w1, const float* b1, const float* w2,
+                   const float* b2, float eps, float* out, hipStream_t st) {
+  return ln2_launch<T, float>(x, ra, M, d, w1, b1, w2, b2, eps, out, st);
 }
 
-template int layernorm<float>(const float*, int, int, const float*, const float*, float, float*, const uint8_t*, hipStream_t);
-template int layernorm<bf16>(const float*, int, int, const float*, const float*, float, bf16*, const uint8_t*, hipStream_t);
-template int layernorm2<float>(float*, int, int, const float*, const float*, const float*, const float*, float, float*, hipStream_t);
-template int layernorm2<bf16>(float*, int, int, const float*, const float*, const float*, const float*, float, bf16*, hipStream_t);
+template int layernorm<float>(float*, const ResidAdd<float>&, int, int, const float*, const float*, float, float*,
+                              const uint8_t*, hipStream_t);
+template int layernorm<bf16>(float*, const ResidAdd<bf16>&, int, int, const float*, const float*, float, bf16*,
+                             const uint8_t*, hipStream_t);
+template int layernorm2<float>(float*, const ResidAdd<float>&, int, int, const float*, const float*, const float*,
+                               const float*, float, float*, hipStream_t);
+template int layernorm2<bf16>(float*, const ResidAdd<bf16>&, int, int, const float*, const float*, const float*,
+                              const float*, float, bf16*, hipStream_t);
+template int layernorm2_f32<float>(float*, const ResidAdd<float>&, int, int, const float*, const float*, const float*,
+                                   const float*, float, float*, hipStream_t);
+template int layernorm2_f32<bf16>(float*, const ResidAdd<bf16>&, int, int, const float*, const float*, const float*,
+                                  const float*, float, float*, hipStream_t);
 
 }  // namespace cfm
