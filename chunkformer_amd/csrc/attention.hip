@@ -361,6 +361,20 @@ __global__ __launch_bounds__(512, 1) void chunk_attention_ring_kernel(
         // (3 P subtiles each, keeps the per-wave scratch at 16 x 48 bf16)
 #pragma unroll
         for (int hh = 0; hh < 2; ++hh) {
+          if (diag == 2) {   // timing experiment: no band / skew
+#pragma unroll
+            for (int st2 = 0; st2 < 2; ++st2)
+#pragma unroll
+              for (int rr = 0; rr < 4; ++rr) {
+                const int st = 2 * hh + st2;
+                const int j = j0 + 32 * hh + 16 * st2 + 4 * g + rr;
+                float sv = S[t][st][rr] * scale;
+                if (j < key_lo || j >= key_hi) sv = -INFINITY;
+                S[t][st][rr] = sv;
+                mx = fmaxf(mx, sv);
+              }
+            continue;
+          }
           const int kb = p_base - i0 - 15 + j0 + 32 * hh;
 #pragma unroll
           for (int pt = 0; pt < 3; ++pt) {
@@ -415,7 +429,7 @@ __global__ __launch_bounds__(512, 1) void chunk_attention_ring_kernel(
 #pragma unroll
       for (int t = 0; t < 5; ++t) {
         const int j0 = jb + 64 * t;
-        if (j0 >= key_hi) continue;
+        if (j0 >= key_hi || diag == 3) continue;
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
           bf16x8 pb;
