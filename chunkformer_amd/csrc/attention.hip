@@ -217,11 +217,16 @@ constexpr int KR_BYTES = RING * 128;            // K ring [384][64] bf16, 16-B c
 constexpr int P_BYTES_ = RING * 128;            // P rows [384][64] bf16, swizzled
 constexpr int VT_PITCH_B = (RING + 8) * 2;      // V^T [64 dims][384 (+8)] bf16
 constexpr int VT_BYTES_ = 64 * VT_PITCH_B;
-constexpr int SCR_PITCH = 50;                   // bf16 per query row of the skew scratch (48-wide band)
+constexpr int SCR_PITCH = 49;                   // bf16 per query row of the skew scratch (48-wide band, 4k+1: rel_shift reshape)
 constexpr int SCR_BYTES = 16 * SCR_PITCH * 2;   // per wave
 constexpr int RING_LDS = KR_BYTES + P_BYTES_ + VT_BYTES_ + 8 * SCR_BYTES + 512;
 }  // namespace
 
+typedef unsigned u32x2_a __attribute__((ext_vector_type(2)));
+CFM_DEV unsigned pack_bf16x2_a(float a, float b) {
+  typedef bf16 b2 __attribute__((ext_vector_type(2)));
+  return __builtin_bit_cast(unsigned, (b2){(bf16)a, (bf16)b});
+}
 CFM_DEV int sw128(int row, int ch) { return row * 128 + ((ch ^ ((row >> 1) & 7)) << 4); }
 
 __global__ __launch_bounds__(512, 1) void chunk_attention_ring_kernel(
@@ -237,6 +242,7 @@ __global__ __launch_bounds__(512, 1) void chunk_attention_ring_kernel(
   // waves 0-3 work on chunk c, waves 4-7 on chunk c+1 (both windows live in the ring: W + C <= RING)
   const int half = w >> 2, wq = w & 3;
   bf16* scr = reinterpret_cast<bf16*>(vt + VT_BYTES_ + w * SCR_BYTES);
+  const unsigned scr_base = (unsigned)(size_t)(__attribute__((address_space(3))) char*)scr;
   float* uv = reinterpret_cast<float*>(vt + VT_BYTES_ + 8 * SCR_BYTES);   // [2][64]: pos_bias_u / v of head h
   const int h = blockIdx.y;
   const int d = H * 64;
@@ -384,19 +390,30 @@ __global__ __launch_bounds__(512, 1) void chunk_attention_ring_kernel(
             for (int s = 0; s < 2; ++s)
               a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<const bf16x8*>(pl + sw128(prow, 4 * s + g)),
                                                           qv[s], a, 0, 0, 0);
-            typedef bf16 bf16x4 __attribute__((ext_vector_type(4)));
-            *reinterpret_cast<bf16x4*>(scr + fr * SCR_PITCH + 16 * pt + 4 * g) =
-                (bf16x4){(bf16)a[0], (bf16)a[1], (bf16)a[2], (bf16)a[3]};
+            // rel_shift by the reshape trick: row fr is written at pitch 49 (+1) and read back at
+            // pitch 48, so query fr's band for key jj starts 16 - fr elements later: the reads
+            // are aligned 8-B vectors (4 keys), the writes 2-B aligned (LDS takes unaligned b64)
+            const unsigned waddr = scr_base + 2u * (unsigned)(fr * SCR_PITCH + 1 + 16 * pt + 4 * g);
+            const unsigned lo = pack_bf16x2_a(a[0], a[1]), hi = pack_bf16x2_a(a[2], a[3]);
+            asm volatile("ds_write_b64 %0, %1" ::"v"(waddr), "v"((u32x2_a){lo, hi}) : "memory");
           }
-          // skewed read: score(query fr, key j0+32hh+16st+4g+rr) += band[fr][16st + 4g + rr + 15 - fr]
+          // score(query fr, key j0+32hh+16st2+4g+rr) += band[fr][16st2 + 4g + rr + 15 - fr]
+          typedef bf16 bf16x4 __attribute__((ext_vector_type(4)));
+          bf16x4 bdv4[2];
+#pragma unroll
+          for (int st2 = 0; st2 < 2; ++st2)
+            asm volatile("ds_read_b64 %0, %1"
+                         : "=v"(bdv4[st2])
+                         : "v"(scr_base + 2u * (unsigned)(fr * (SCR_PITCH - 1) + 16 + 16 * st2 + 4 * g))
+                         : "memory");
+          asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(bdv4[0]), "+v"(bdv4[1])::"memory");
 #pragma unroll
           for (int st2 = 0; st2 < 2; ++st2) {
             const int st = 2 * hh + st2;
 #pragma unroll
             for (int rr = 0; rr < 4; ++rr) {
               const int jj = 16 * st2 + 4 * g + rr;
-              const float bdv = (float)scr[fr * SCR_PITCH + jj + 15 - fr];
-              float sv = (S[t][st][rr] + bdv) * scale;
+              float sv = (S[t][st][rr] + (float)bdv4[st2][rr]) * scale;
               const int j = j0 + 32 * hh + jj;
               if (j < key_lo || j >= key_hi) sv = -INFINITY;
               S[t][st][rr] = sv;

@@ -113,6 +113,10 @@ __global__ __launch_bounds__(256, 3) void fe_conv0_dw_mfma_kernel(const float* _
                                                                const float* __restrict__ wpack, int d,
                                                                bf16* __restrict__ out) {
   __shared__ float xin[FE_XROWS * FE_F0];
+  // per-wave output staging [32 positions][64 channels] bf16, 144-B rows: the MFMA layout gives
+  // each lane one channel; two channel tiles are gathered here and leave as full 128-B rows
+  constexpr int OPITCH = 144;
+  __shared__ __attribute__((aligned(16))) char ostage[4][32 * OPITCH];
   const int tid = threadIdx.x;
   const int win = blockIdx.y;
   const int P = T2 * FE_F2;
@@ -204,11 +208,20 @@ __global__ __launch_bounds__(256, 3) void fe_conv0_dw_mfma_kernel(const float* _
       asm volatile("" : "+v"(wcur), "+v"(o));
       if (s + 1 < 9) acc = nxt;
     }
-    bf16* ow = out + (size_t)win * P * d;   // 32-bit offsets inside the window
+    char* os = ostage[wv];
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const int pos = pw + 8 * (r >> 2) + 4 * hh + (r & 3);
-      if (pos < P) ow[pos * d + c] = (bf16)o[r];
+      const int m = 8 * (r >> 2) + 4 * hh + (r & 3);
+      *reinterpret_cast<bf16*>(os + m * OPITCH + ((ct & 32) + n) * 2) = (bf16)o[r];
+    }
+    if (ct & 32) {   // 64 channels staged: lane -> 16-B chunk (lane & 7) of positions (lane >> 3) + 8k
+      bf16* ow = out + (size_t)win * P * d + (ct - 32) + (lane & 7) * 8;   // 32-bit offsets inside the window
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int m = (lane >> 3) + 8 * k;
+        const u32x4 v = *reinterpret_cast<const u32x4*>(os + m * OPITCH + (lane & 7) * 16);
+        if (pw + m < P) *reinterpret_cast<u32x4*>(ow + (pw + m) * d) = v;
+      }
     }
   }
 }
@@ -275,7 +288,7 @@ int frontend_conv0_dw(const float* feats, const int32_t* meta, int meta_stride, 
   if (T2 <= 0 || d % FE_CG) return (int)hipErrorInvalidValue;
   const dim3 grid((T2 + FE_T2_TILE - 1) / FE_T2_TILE, nwin);
   if constexpr (std::is_same<T, bf16>::value) {
-    if (d % 32) return (int)hipErrorInvalidValue;
+    if (d % 64) return (int)hipErrorInvalidValue;
     hipLaunchKernelGGL(fe_conv0_dw_mfma_kernel, dim3((T2 * FE_F2 + FE_POS_BLOCK - 1) / FE_POS_BLOCK, nwin), dim3(256),
                        0, st, feats, meta, meta_stride, W, T2, cmvn_mean, cmvn_istd, wpack, d, out);
   } else {
