@@ -232,7 +232,7 @@ CFM_DEV int sw128(int row, int ch) { return row * 128 + ((ch ^ ((row >> 1) & 7))
 __global__ __launch_bounds__(512, 1) void chunk_attention_ring_kernel(
     const bf16* __restrict__ Q, const bf16* __restrict__ KV, int kv_rows, const bf16* __restrict__ P, int p_rows,
     const float* __restrict__ pos_u, const float* __restrict__ pos_v, const int32_t* __restrict__ desc, int n_chunks,
-    int H, int C, int W, bf16* __restrict__ out, int diag) {
+    int H, int C, int W, bf16* __restrict__ out, int diag, int nch) {
   __shared__ __attribute__((aligned(16))) char smem[RING_LDS];
   char* kr = smem;
   char* pl = smem + KR_BYTES;
@@ -240,13 +240,13 @@ __global__ __launch_bounds__(512, 1) void chunk_attention_ring_kernel(
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int fr = lane & 15, g = lane >> 4;
   // waves 0-3 work on chunk c, waves 4-7 on chunk c+1 (both windows live in the ring: W + C <= RING)
-  const int half = w >> 2, wq = w & 3;
+  const int half = __builtin_amdgcn_readfirstlane(w) >> 2, wq = w & 3;
   bf16* scr = reinterpret_cast<bf16*>(vt + VT_BYTES_ + w * SCR_BYTES);
   const unsigned scr_base = (unsigned)(size_t)(__attribute__((address_space(3))) char*)scr;
   float* uv = reinterpret_cast<float*>(vt + VT_BYTES_ + 8 * SCR_BYTES);   // [2][64]: pos_bias_u / v of head h
   const int h = blockIdx.y;
   const int d = H * 64;
-  const int c0 = blockIdx.x * NCH, c1 = min(c0 + NCH, n_chunks);
+  const int c0 = blockIdx.x * nch, c1 = min(c0 + nch, n_chunks);
   if (c0 >= c1) return;
 
   // ---- zero the K / V^T rings (rows past a window's end are read as masked keys: p = 0 must not meet NaN)
@@ -293,18 +293,38 @@ __global__ __launch_bounds__(512, 1) void chunk_attention_ring_kernel(
 
   const float scale = 0.125f;
   const int i0 = wq * 16;
+  // masked-batch descriptors (planner.cpp, C <= 64: one query block per chunk): chunk c's queries
+  // are rows c*C.., its window starts at flat KV row c*C, P_BASE = C-1, every query row valid;
+  // only the key range [lo, hi) varies.  Q fragments and the key range of the wave's NEXT chunk
+  // are loaded one pair ahead, so no iteration waits on a dependent global load.
+  const int p_base = C - 1, q_valid = C;
+  auto load_q = [&](int c, bf16x8 (&qr)[2]) {
+    const bf16* qp = Q + ((size_t)c * C + i0 + fr) * d + h * 64;
+    qr[0] = *reinterpret_cast<const bf16x8*>(qp + 8 * g);
+    qr[1] = *reinterpret_cast<const bf16x8*>(qp + 32 + 8 * g);
+  };
+  bf16x8 qraw[2], qnext[2];
+  int klo_n = 0, khi_n = 0;
+  {
+    const int c = c0 + half;
+    if (c < c1 && i0 < C) load_q(c, qnext);
+    const int cc = min(c, c1 - 1);
+    klo_n = desc[(size_t)cc * AD_INTS + AD_KEY_LO];
+    khi_n = desc[(size_t)cc * AD_INTS + AD_KEY_HI];
+  }
   for (int cp = c0; cp < c1; cp += 2) {
     const int kvp = kvb + (cp - c0) * C;
     const int c = cp + half;
     const bool active = c < c1 && i0 < C && diag != 1;
-    // ---- query fragment loads first (their wait must not cover the prefetch below)
-    bf16x8 qraw[2];
-    const int32_t* D = desc + (size_t)min(c, c1 - 1) * AD_INTS;
-    const int q_row0 = D[AD_Q_ROW0];
-    if (active) {
-      const bf16* qp = Q + (size_t)(q_row0 + i0 + fr) * d + h * 64;
-      qraw[0] = *reinterpret_cast<const bf16x8*>(qp + 8 * g);
-      qraw[1] = *reinterpret_cast<const bf16x8*>(qp + 32 + 8 * g);
+    qraw[0] = qnext[0];
+    qraw[1] = qnext[1];
+    const int key_lo = klo_n, key_hi = khi_n;
+    {
+      const int cn = c + 2;
+      if (cn < c1 && i0 < C) load_q(cn, qnext);
+      const int cc = min(cn, c1 - 1);
+      klo_n = desc[(size_t)cc * AD_INTS + AD_KEY_LO];
+      khi_n = desc[(size_t)cc * AD_INTS + AD_KEY_HI];
     }
     // ---- prefetch the next pair's 2C new window rows [kvp + W + C, kvp + W + 3C) into registers
     const int n_new = max(0, min(2 * C, (min(cp + 4, c1) - (cp + 2)) * C));
@@ -322,9 +342,8 @@ __global__ __launch_bounds__(512, 1) void chunk_attention_ring_kernel(
       }
     }
     if (active) {
-      const int kv0 = D[AD_KV_ROW0];
-      const int key_lo = D[AD_KEY_LO], key_hi = D[AD_KEY_HI], p_base = D[AD_P_BASE], q_valid = D[AD_Q_VALID];
-      const int rb = kv0 % RING;   // ring row of window key 0
+      const int q_row0 = c * C;
+      const int rb = (c * C) % RING;   // ring row of window key 0
       auto ring = [&](int j) { const int r = rb + j; return r >= RING ? r - RING : r; };
       // ---- query fragments (B operands): lane (fr, g) = query i0+fr, dims 32s + 8g .. +7
       bf16x8 qu[2], qv[2];
@@ -492,9 +511,19 @@ int chunk_attention_masked_bf16(const bf16* q, const bf16* kv, int kv_rows, cons
                                 const float* pos_u, const float* pos_v, const int32_t* desc, int n_chunks, int H,
                                 int C, int W, bf16* out, hipStream_t st, int diag) {
   if (C <= 0 || C > 64 || (C % 16) || (W & 1) || W + C > RING || p_rows > RING || n_chunks <= 0) return -1;
-  const dim3 grid((n_chunks + NCH - 1) / NCH, H);
+  // one block per CU (LDS-bound), each sweeping a long run of chunks of one head: one prologue
+  // (P rows + first window) per block instead of one per 8 chunks
+  static int n_cu = 0;
+  if (!n_cu) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0) n_cu = 256;
+  }
+  int nch = (int)(((long long)n_chunks * H + n_cu - 1) / n_cu);
+  nch = max(NCH, (nch + 1) & ~1);
+  const dim3 grid((n_chunks + nch - 1) / nch, H);
   hipLaunchKernelGGL(chunk_attention_ring_kernel, grid, dim3(512), 0, st, q, kv, kv_rows, P, p_rows, pos_u, pos_v,
-                     desc, n_chunks, H, C, W, out, diag);
+                     desc, n_chunks, H, C, W, out, diag, nch);
   CFM_CHECK_LAUNCH();
   return 0;
 }

@@ -37,7 +37,8 @@ def _close(got, exp, tol):
 
 
 SHAPES = [(1000, 512, 512), (700, 2048, 512), (513, 512, 2048), (256, 256, 4608), (300, 48, 128),
-          (70001, 512, 512), (33000, 2048, 512)]   # the last two run the persistent multi-tile path
+          (70001, 512, 512), (33000, 2048, 512),   # these two run the persistent multi-tile path
+          (1000, 256, 128), (4097, 768, 384)]      # shortest ring K (4 steps); K % 128 != 0 (K-64 kernel)
 MODES = [("bf16", 0), ("bf16", 1), ("fp32", 0)]
 
 
@@ -57,6 +58,16 @@ def test_gemm_store(L, M, N, K, mode, act):
     r = torch.relu(r) if act == 1 else (torch.nn.functional.silu(r) if act == 2 else r)
     _close(out[3:], r, 1e-2 if dt == "bf16" else 1e-5)
     assert torch.isnan(out[:3].float()).all()
+
+
+@pytest.mark.parametrize("M,N,K", [(70001, 512, 512), (1000, 256, 4608)])
+def test_gemm_no_bias(L, M, N, K):
+    g = torch.Generator(device="cuda").manual_seed(7)
+    A = (torch.randn(M, K, device="cuda", generator=g) * 0.5).to(torch.bfloat16)
+    W = (torch.randn(N, K, device="cuda", generator=g) / K ** 0.5).to(torch.bfloat16)
+    out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    _run(L, L.DTYPE_BF16, 0, 0, A, W, None, out=out, ldo=N)
+    _close(out, _ref(A, W, None), 1e-2)
 
 
 @pytest.mark.parametrize("mode", MODES)

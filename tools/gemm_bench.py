@@ -14,9 +14,9 @@ from chunkformer_amd import _lib as L  # noqa: E402
 M = 2845 * 64
 SHAPES = [  # (name, N, K, epi, act)
     ("ffn_w1", 2048, 512, 0, 2),
-    ("ffn_w2", 512, 2048, 2, 0),
+    ("ffn_w2", 512, 2048, 0, 0),
     ("qkv", 1536, 512, 3, 0),
-    ("out/pw2", 512, 512, 2, 0),
+    ("out/pw2", 512, 512, 0, 0),
     ("pw1_glu", 1024, 512, 4, 0),
     ("fe_pw1", 512, 512, 0, 1),
 ]
