@@ -15,9 +15,10 @@ host packer (C++ planner) + plan upload + front-end + 12 blocks + after_norm, wi
 the features already resident in HBM.  value = all ranks' fbank frames / max-over-
 ranks step time.
 
-roofline: the dominant kernel is the FFN w_1 GEMM ([64N, 512] x [512, 2048], bf16
-MFMA); its per-launch time is measured live with HIP events on the launch stream
-(libcfm in-stream profiler) over the timed steps.  cpu_baseline: the CPU oracle
+roofline: the dominant kernel is the FFN (bf16 MFMA): the fused w_2 . SiLU(w_1 . x) kernel
+(2 x 2 x 64N x 512 x 2048 FLOP per launch), or the w_1 GEMM on the two-GEMM path; its
+per-launch time is measured live with HIP events on the launch stream (libcfm in-stream
+profiler) over the timed steps.  cpu_baseline: the CPU oracle
 (oracle/encoder_ref.py, torch fp32) on a bounded sample of the same workload.
 """
 from __future__ import annotations
@@ -140,9 +141,9 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    ffn1_bit = 1 << _lib.PROFILE_CLASSES.index("ffn_w1_gemm")
+    roof_bits = (1 << _lib.PROFILE_CLASSES.index("ffn_w1_gemm")) | (1 << _lib.PROFILE_CLASSES.index("ffn_fused"))
     enc.set_option("profile_reset", 1)
-    enc.set_option("profile", ffn1_bit)
+    enc.set_option("profile", roof_bits)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -164,16 +165,29 @@ def main():
     total_frames = float(frames.item())
     value = total_frames * args.steps / dt_max
 
-    # ---- dominant kernel: FFN w_1 GEMM, per-launch time from in-stream HIP events
-    ms1, n1 = prof["ffn_w1_gemm"]
+    # ---- dominant kernel: the FFN (fused kernel, or its w_1 GEMM on the two-GEMM path);
+    # per-launch time from in-stream HIP events on the launch stream (libcfm profiler)
     rows = n_chunks * C
-    fl_launch = 2.0 * rows * LARGE.ffn_dim * LARGE.d_model
+    d_, ff_ = LARGE.d_model, LARGE.ffn_dim
+    fused = prof.get("ffn_fused", (0.0, 0))[1] > 0
+    if fused:
+        roof_cls = "ffn_fused"
+        roof_name = "ffn_fused (ffn_fused_kernel: w_2 . SiLU(w_1 . x + b_1) + b_2, hidden kept on-chip)"
+        fl_launch = 2.0 * 2.0 * rows * ff_ * d_
+        # compulsory bytes: x [rows, d] in + y [rows, d] out (bf16) + the 4 MiB weight slab stream + biases
+        alg_bytes = 2.0 * (2 * rows * d_ + 2 * ff_ * d_) + 4 * (ff_ + d_)
+    else:
+        roof_cls = "ffn_w1_gemm"
+        roof_name = ("ffn_w1_gemm (gemm_kernel<bf16,EPI_STORE,SiLU>)" if args.dtype == "bf16"
+                     else "ffn_w1_gemm (gemm_kernel<float,EPI_STORE,SiLU>)")
+        fl_launch = 2.0 * rows * ff_ * d_
+        # compulsory bytes of one w_1 launch: A [rows, d] + out [rows, ff] bf16 + W [ff, d] bf16 + bias
+        alg_bytes = 2.0 * (rows * d_ + rows * ff_ + ff_ * d_) + 4 * ff_
+    ms1, n1 = prof[roof_cls]
     avg_s = (ms1 / max(n1, 1)) / 1e3
     achieved = fl_launch / avg_s / 1e12 if n1 else None
     peak = PEAK_TFLOPS[args.dtype]
-    traffic, traffic_src = committed_traffic() if args.dtype == "bf16" else (None, None)
-    # compulsory bytes of one w_1 launch: A [rows, d] + out [rows, ff] bf16 + W [ff, d] bf16 + bias
-    alg_bytes = 2.0 * (rows * LARGE.d_model + rows * LARGE.ffn_dim + LARGE.ffn_dim * LARGE.d_model) + 4 * LARGE.ffn_dim
+    traffic, traffic_src = committed_traffic(roof_cls) if args.dtype == "bf16" else (None, None)
     step_flops = n_chunks * flops_per_chunk(LARGE) + LARGE.num_blocks * 2 * (L + 2 * C + R - 1) * LARGE.d_model ** 2
 
     # ---- CTC head + the one collective (timed separately; not part of `value`)
@@ -222,8 +236,7 @@ def main():
                                    f"utterances, seed 0), forward_parallel_chunk C=64 L=128 R=128",
                        "utterances_rank0": len(lens), "chunks_rank0": n_chunks, "frames_total": int(total_frames),
                        "parallelism": f"dp{world} (LPT utterance sharding)"},
-            "roofline": {"bound": "mfma", "kernel": "ffn_w1_gemm (gemm_kernel<bf16,EPI_STORE,SiLU>)"
-                         if args.dtype == "bf16" else "ffn_w1_gemm (gemm_kernel<float,EPI_STORE,SiLU>)",
+            "roofline": {"bound": "mfma", "kernel": roof_name,
                          "achieved": round(achieved, 1) if achieved else None, "peak": peak, "unit": "TFLOP/s",
                          "frac": round(achieved / peak, 4) if achieved else None, "traffic": traffic,
                          "traffic_unit": "HBM bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)",

@@ -71,7 +71,8 @@ cfm_ctc_logprobs = _sig("cfm_ctc_logprobs", I32, P, P, I32, P, P, P, SZ, P)
 # include/cfm_ops.h
 cfm_op_gemm = _sig("cfm_op_gemm", I32, I32, I32, I32, P, I32, P, I32, I32, I32, I32, P, ctypes.c_float, P, I32, I32, P,
                    I32, P, I32, P, I32, P)
-EXPORTED_OPS = ["cfm_op_gemm"]
+cfm_op_ffn = _sig("cfm_op_ffn", I32, P, P, P, P, P, P, I32, I32, I32, P)
+EXPORTED_OPS = ["cfm_op_gemm", "cfm_op_ffn"]
 
 EXPORTED = ["cfm_version", "cfm_last_error", "cfm_model_create", "cfm_model_destroy", "cfm_model_set_option",
             "cfm_plan_masked", "cfm_plan_padded", "cfm_workspace_bytes_masked", "cfm_workspace_bytes_padded",
@@ -91,7 +92,7 @@ def profile_read(h):
 
 PROFILE_CLASSES = ["frontend_conv0_dw", "frontend_pw_gemm", "frontend_dw2", "pos_gemm", "layernorm", "ffn_w1_gemm",
                    "ffn_w2_gemm", "qkv_gemm", "chunk_attention", "out_proj_gemm", "pw1_glu_gemm", "conv_dw_ln_silu",
-                   "pw2_gemm", "cache_copy", "ctc"]
+                   "pw2_gemm", "cache_copy", "ctc", "ffn_fused"]
 
 
 def check(status: int) -> None:

@@ -56,6 +56,11 @@ int chunk_attention_masked_bf16(const bf16* q, const bf16* kv, int kv_rows, cons
                                 const float* pos_u, const float* pos_v, const int32_t* desc, int n_chunks, int H,
                                 int C, int W, bf16* out, hipStream_t st, int diag = 0);
 
+// fused FFN (ffn.hip): y = w2 . SiLU(w1 . x + b1) + b2 over a repacked slab stream; -1 = not eligible
+int ffn_fused(const bf16* x, int M, const bf16* wstream, const float* b1, const float* b2, bf16* y, int d, int ff,
+              hipStream_t st);
+void ffn_pack_stream(const float* w1, const float* w2, int d, int ff, uint16_t* out, uint16_t (*to_bf16)(float));
+
 // conv module: depthwise k=15 + bias + LayerNorm + SiLU (conv_module.hip)
 template <typename T>
 int conv_dw_ln_silu(const T* glu, const int32_t* desc, int nblk, int d, const float* wdw_t /*[15][d]*/,

@@ -64,6 +64,7 @@ struct Carver {
 
 struct LayerW {
   void *ff1m, *ff2m, *ff1, *ff2, *qkv, *pos, *wo, *pw1, *pw2;   // T matrices [N][K]
+  void *ffs_m = nullptr, *ffs = nullptr;   // bf16 fused-FFN slab streams (ffn.hip), macaron / final
   float *b_ff1m, *b_ff2m, *b_ff1, *b_ff2, *b_qkv, *b_o, *b_pw1, *b_pw2;
   float *pu, *pv, *dw_t, *b_dw, *cn_w, *cn_b;
   float *ln_ffm_w, *ln_ffm_b, *ln_mha_w, *ln_mha_b, *ln_conv_w, *ln_conv_b, *ln_ff_w, *ln_ff_b, *ln_fin_w, *ln_fin_b;
@@ -82,12 +83,12 @@ struct FrontW {
 // Kernel classes timed by the optional in-stream profiler (HIP events around launches)
 enum {
   PC_FE_CONV = 0, PC_FE_GEMM, PC_FE_DW2, PC_POS, PC_LN, PC_FFN1, PC_FFN2, PC_QKV, PC_ATTN, PC_OPROJ, PC_PW1,
-  PC_CONV, PC_PW2, PC_CACHE, PC_CTC, PC_N
+  PC_CONV, PC_PW2, PC_CACHE, PC_CTC, PC_FFNF, PC_N
 };
 static const char* const PC_NAMES[PC_N] = {
     "frontend_conv0_dw", "frontend_pw_gemm", "frontend_dw2", "pos_gemm", "layernorm", "ffn_w1_gemm", "ffn_w2_gemm",
     "qkv_gemm", "chunk_attention", "out_proj_gemm", "pw1_glu_gemm", "conv_dw_ln_silu", "pw2_gemm", "cache_copy",
-    "ctc"};
+    "ctc", "ffn_fused"};
 
 struct cfm_model {
   cfm_config cfg;
@@ -97,6 +98,7 @@ struct cfm_model {
   cfm::FrontW fe;
   int max_layers = -1;
   bool use_ring_attention = true;
+  bool use_fused_ffn = true;        // "fused_ffn": bf16 d=512 FFN as one kernel (ffn.hip) instead of two GEMMs
   int attn_diag = 0;                // "attn_diag": 1 = ring kernel without compute (staging only)   // "ring_attention" option (A/B against the generic kernel)
   // profiler: bitmask of PC_* classes to bracket with events on the launch stream
   uint32_t prof_mask = 0;
@@ -269,13 +271,24 @@ struct ModelT : public cfm_model {
     // x += alpha * y (0.5 for the FFNs, encoder_layer.py:196/246; the conv branch masked by
     // the padded path's row mask) is fused into the LayerNorm that reads x next.
     auto resid = [&](float alpha, const uint8_t* ym) { ResidAdd<T> r; r.y = w.y; r.alpha = alpha; r.ymask = ym; return r; };
+    // y = w2 . SiLU(w1 . h + b1) + b2: one fused kernel (bf16, d = 512) or two GEMMs through w.hid
+    auto ffn = [&](const void* w1, const float* b1, const void* w2, const float* b2, const void* stream_w) -> cfm_status {
+      if constexpr (sizeof(T) == 2) {
+        if (use_fused_ffn && stream_w) {
+          PROF(PC_FFNF, ffn_fused((const bf16*)w.h, rows, (const bf16*)stream_w, b1, b2, (bf16*)w.y, d, ff, st));
+          return CFM_OK;
+        }
+      }
+      { EpiArgs e; e.bias = b1; e.out = w.hid; e.ldo = ff;
+        PROF(PC_FFN1, gemm<T>(EPI_STORE, ACT_SILU, w.h, d, (const T*)w1, d, rows, ff, d, e, st)); }
+      { EpiArgs e; e.bias = b2; e.out = w.y; e.ldo = d;
+        PROF(PC_FFN2, gemm<T>(EPI_STORE, ACT_NONE, w.hid, ff, (const T*)w2, ff, rows, d, ff, e, st)); }
+      return CFM_OK;
+    };
     for (int l = 0; l < nl; ++l) {
       const LayerW& Lw = layers[l];
       // macaron FFN (x 0.5)
-      { EpiArgs e; e.bias = Lw.b_ff1m; e.out = w.hid; e.ldo = ff;
-        PROF(PC_FFN1, gemm<T>(EPI_STORE, ACT_SILU, w.h, d, (const T*)Lw.ff1m, d, rows, ff, d, e, st)); }
-      { EpiArgs e; e.bias = Lw.b_ff2m; e.out = w.y; e.ldo = d;
-        PROF(PC_FFN2, gemm<T>(EPI_STORE, ACT_NONE, w.hid, ff, (const T*)Lw.ff2m, ff, rows, d, ff, e, st)); }
+      { const cfm_status fs = ffn(Lw.ff1m, Lw.b_ff1m, Lw.ff2m, Lw.b_ff2m, Lw.ffs_m); if (fs != CFM_OK) return fs; }
       // MHSA
       PROF(PC_LN, layernorm<T>(w.x, resid(0.5f, nullptr), rows, d, Lw.ln_mha_w, Lw.ln_mha_b, eps, w.h, nullptr, st));
       if (aci) PROF(PC_CACHE, att_cache_in<T>(aci + (size_t)l * L * 2 * d, L, 2 * d, w.kv, st));
@@ -311,10 +324,7 @@ struct ModelT : public cfm_model {
         PROF(PC_PW2, gemm<T>(EPI_STORE, ACT_NONE, w.cv, d, (const T*)Lw.pw2, d, rows, d, d, e, st)); }
       // FFN (x 0.5)
       PROF(PC_LN, layernorm<T>(w.x, resid(1.f, rmask), rows, d, Lw.ln_ff_w, Lw.ln_ff_b, eps, w.h, nullptr, st));
-      { EpiArgs e; e.bias = Lw.b_ff1; e.out = w.hid; e.ldo = ff;
-        PROF(PC_FFN1, gemm<T>(EPI_STORE, ACT_SILU, w.h, d, (const T*)Lw.ff1, d, rows, ff, d, e, st)); }
-      { EpiArgs e; e.bias = Lw.b_ff2; e.out = w.y; e.ldo = d;
-        PROF(PC_FFN2, gemm<T>(EPI_STORE, ACT_NONE, w.hid, ff, (const T*)Lw.ff2, ff, rows, d, ff, e, st)); }
+      { const cfm_status fs = ffn(Lw.ff1, Lw.b_ff1, Lw.ff2, Lw.b_ff2, Lw.ffs); if (fs != CFM_OK) return fs; }
       // norm_final (+ next layer's macaron LN, or after_norm)
       if (l + 1 < nl)
         PROF(PC_LN, layernorm2<T>(w.x, resid(0.5f, nullptr), rows, d, Lw.ln_fin_w, Lw.ln_fin_b, layers[l + 1].ln_ffm_w,
@@ -362,6 +372,13 @@ struct HostW {
   bool has(const std::string& k) const { return m.count(k) > 0; }
 };
 
+static uint16_t bf16_bits_rne(float f) {   // round-to-nearest-even f32 -> bf16 bits (host)
+  uint32_t u;
+  std::memcpy(&u, &f, 4);
+  if ((u & 0x7f800000u) == 0x7f800000u) return (uint16_t)((u >> 16) | ((u & 0xffff) ? 0x40 : 0));
+  return (uint16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+}
+
 template <typename T>
 static cfm_status build_model(const cfm_config& cfg, const HostW& hw, int device, cfm_model** out) {
   auto* M = new ModelT<T>();
@@ -397,6 +414,12 @@ static cfm_status build_model(const cfm_config& cfg, const HostW& hw, int device
         std::memcpy(&p[i], &r, 2);
       }
     }
+    fix.push_back({off, slot});
+  };
+  auto put_ffn_stream = [&](const float* w1, const float* w2, void** slot) {
+    const size_t n = (size_t)2 * d * ff;
+    size_t off = reserve(n * 2);
+    ffn_pack_stream(w1, w2, d, ff, reinterpret_cast<uint16_t*>(img.data() + off), &bf16_bits_rne);
     fix.push_back({off, slot});
   };
   auto vec = [&](const std::string& k, int64_t n) { const float* s = hw.get(k, n); return std::vector<float>(s, s + n); };
@@ -464,6 +487,12 @@ static cfm_status build_model(const cfm_config& cfg, const HostW& hw, int device
       put_f32(hw.get(p + "feed_forward.w_1.bias", ff), ff, &Lw.b_ff1);
       put_T(vec(p + "feed_forward.w_2.weight", (int64_t)d * ff), &Lw.ff2);
       put_f32(hw.get(p + "feed_forward.w_2.bias", d), d, &Lw.b_ff2);
+      if (sizeof(T) == 2 && d == 512 && ff % 64 == 0) {   // fused-FFN slab streams (ffn.hip)
+        put_ffn_stream(hw.get(p + "feed_forward_macaron.w_1.weight", (int64_t)ff * d),
+                       hw.get(p + "feed_forward_macaron.w_2.weight", (int64_t)d * ff), &Lw.ffs_m);
+        put_ffn_stream(hw.get(p + "feed_forward.w_1.weight", (int64_t)ff * d),
+                       hw.get(p + "feed_forward.w_2.weight", (int64_t)d * ff), &Lw.ffs);
+      }
       {
         std::vector<float> w, b;
         for (const char* nm : {"linear_q", "linear_k", "linear_v"}) {
@@ -560,6 +589,7 @@ cfm_status cfm_model_set_option(cfm_model* m, const char* key, int64_t value) {
   if (!std::strcmp(key, "max_layers")) { m->max_layers = (int)value; return CFM_OK; }
   if (!std::strcmp(key, "profile")) { m->prof_mask = (uint32_t)value; return CFM_OK; }
   if (!std::strcmp(key, "ring_attention")) { m->use_ring_attention = value != 0; return CFM_OK; }
+  if (!std::strcmp(key, "fused_ffn")) { m->use_fused_ffn = value != 0; return CFM_OK; }
   if (!std::strcmp(key, "attn_diag")) { m->attn_diag = (int)value; return CFM_OK; }
   if (!std::strcmp(key, "profile_reset")) {
     m->prof_collect();
@@ -644,6 +674,23 @@ cfm_status cfm_op_gemm(int32_t dtype, int32_t epi, int32_t act, const void* A, i
     r = gemm<bf16>(epi, act, (const bf16*)A, lda, (const bf16*)W, ldw, M, N, K, e, (hipStream_t)stream);
   gemm_force_small_tiles(0);
   if (r) return set_error(CFM_ERR_RUNTIME, std::string("gemm: ") + hipGetErrorString((hipError_t)r));
+  return CFM_OK;
+}
+
+cfm_status cfm_op_ffn(const float* w1, const float* b1, const float* w2, const float* b2, const void* x, void* y,
+                      int32_t M, int32_t d, int32_t ff, cfm_stream stream) {
+  if (!w1 || !w2 || !b1 || !b2 || !x || !y) return set_error(CFM_ERR_VALUE, "null argument");
+  if (d != 512 || ff <= 0 || ff % 64) return set_error(CFM_ERR_VALUE, "fused FFN needs d == 512 and ff % 64 == 0");
+  std::vector<uint16_t> host((size_t)2 * d * ff);
+  ffn_pack_stream(w1, w2, d, ff, host.data(), &bf16_bits_rne);
+  void* dev = nullptr;
+  HIPC(hipMalloc(&dev, host.size() * 2));
+  hipError_t e = hipMemcpyAsync(dev, host.data(), host.size() * 2, hipMemcpyHostToDevice, (hipStream_t)stream);
+  int r = e == hipSuccess ? ffn_fused((const bf16*)x, M, (const bf16*)dev, b1, b2, (bf16*)y, d, ff, (hipStream_t)stream)
+                          : (int)e;
+  if (r == 0) r = (int)hipStreamSynchronize((hipStream_t)stream);
+  (void)hipFree(dev);
+  if (r) return set_error(CFM_ERR_RUNTIME, std::string("ffn: ") + hipGetErrorString((hipError_t)r));
   return CFM_OK;
 }
 

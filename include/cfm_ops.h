@@ -30,6 +30,13 @@ cfm_status cfm_op_gemm(int32_t dtype, int32_t epi, int32_t act, const void* A, i
                        int32_t row_off, void* out2, int32_t d, float* x, int32_t ldx, const uint8_t* rowmask,
                        int32_t small_tiles, cfm_stream stream);
 
+/* fused position-wise FFN (bf16): y[M,d] = w2 . SiLU(w1 . x + b1) + b2, x / y bf16 device rows,
+ * w1 [ff,d] / w2 [d,ff] f32 HOST arrays in the reference layout (repacked into the slab stream
+ * here: this test entry point allocates and synchronises), b1 / b2 f32 device.  d must be 512.
+ * Replaces PositionwiseFeedForward.forward (positionwise_feed_forward.py:51-60) with SiLU. */
+cfm_status cfm_op_ffn(const float* w1, const float* b1, const float* w2, const float* b2, const void* x, void* y,
+                      int32_t M, int32_t d, int32_t ff, cfm_stream stream);
+
 #ifdef __cplusplus
 }
 #endif

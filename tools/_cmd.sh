@@ -1,3 +1,4 @@
 set -e
-timeout -k 10 300 python -m pytest tests -m gpu -x -q > gpurun_out/gpu_tests3.log 2>&1
-for a in 0 1 2 3; do timeout -k 10 120 python3 tools/layer_bench.py --iters 2 --opt attn_diag=$a > gpurun_out/attn3_d$a.log 2>&1; done
+timeout -k 10 300 python -m pytest tests/test_gpu_ops.py -x -q -k ffn > gpurun_out/ffn_test.log 2>&1
+timeout -k 10 300 python -m pytest tests -m gpu -x -q > gpurun_out/gpu_tests4.log 2>&1
+timeout -k 10 300 python3 bench.py --no-cpu-baseline > gpurun_out/bench4.log 2>&1

@@ -23,6 +23,7 @@ CLASSES = [
     ("conv_dw_ln_silu_kernel", "conv_dw_ln_silu"),
     ("ln_kernel", "layernorm"),
     ("ln2_kernel", "layernorm2"),
+    ("ffn_fused_kernel", "ffn_fused"),
 ]
 
 
