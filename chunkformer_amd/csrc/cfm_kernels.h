@@ -59,6 +59,7 @@ int chunk_attention_masked_bf16(const bf16* q, const bf16* kv, int kv_rows, cons
 // fused FFN (ffn.hip): y = w2 . SiLU(w1 . x + b1) + b2 over a repacked slab stream; -1 = not eligible
 int ffn_fused(const bf16* x, int M, const bf16* wstream, const float* b1, const float* b2, bf16* y, int d, int ff,
               hipStream_t st);
+void ffn_set_variant(int v);
 void ffn_pack_stream(const float* w1, const float* w2, int d, int ff, uint16_t* out, uint16_t (*to_bf16)(float));
 
 // conv module: depthwise k=15 + bias + LayerNorm + SiLU (conv_module.hip)

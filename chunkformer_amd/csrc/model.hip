@@ -98,7 +98,7 @@ struct cfm_model {
   cfm::FrontW fe;
   int max_layers = -1;
   bool use_ring_attention = true;
-  bool use_fused_ffn = true;        // "fused_ffn": bf16 d=512 FFN as one kernel (ffn.hip) instead of two GEMMs
+  bool use_fused_ffn = false;       // "fused_ffn": bf16 d=512 FFN as one kernel (ffn.hip) instead of two GEMMs (A/B: 16% slower)
   int attn_diag = 0;                // "attn_diag": 1 = ring kernel without compute (staging only)   // "ring_attention" option (A/B against the generic kernel)
   // profiler: bitmask of PC_* classes to bracket with events on the launch stream
   uint32_t prof_mask = 0;
@@ -590,6 +590,7 @@ cfm_status cfm_model_set_option(cfm_model* m, const char* key, int64_t value) {
   if (!std::strcmp(key, "profile")) { m->prof_mask = (uint32_t)value; return CFM_OK; }
   if (!std::strcmp(key, "ring_attention")) { m->use_ring_attention = value != 0; return CFM_OK; }
   if (!std::strcmp(key, "fused_ffn")) { m->use_fused_ffn = value != 0; return CFM_OK; }
+  if (!std::strcmp(key, "ffn_variant")) { ffn_set_variant((int)value); return CFM_OK; }
   if (!std::strcmp(key, "attn_diag")) { m->attn_diag = (int)value; return CFM_OK; }
   if (!std::strcmp(key, "profile_reset")) {
     m->prof_collect();
