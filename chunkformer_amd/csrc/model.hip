@@ -352,8 +352,17 @@ struct ModelT : public cfm_model {
       A = a;
     }
     float* dst = logp ? logp : logits;
-    EpiArgs e; e.bias = fe.ctc_b; e.out = dst; e.ldo = V;
-    PROF(PC_CTC, gemm<T>(EPI_STORE_F32, ACT_NONE, A, d, (const T*)fe.ctc_w, d, rows, V, d, e, st));
+    // the vocabulary splits into a 256-multiple part (256 x 256 MFMA tiles) and a remainder (128 x 128
+    // tiles); f32x4 epilogue stores need the row pitch V % 4 == 0
+    const int V1 = (sizeof(T) == 2 && V % 4 == 0) ? V / 256 * 256 : 0;
+    if (V1 > 0) {
+      EpiArgs e; e.bias = fe.ctc_b; e.out = dst; e.ldo = V;
+      PROF(PC_CTC, gemm<T>(EPI_STORE_F32, ACT_NONE, A, d, (const T*)fe.ctc_w, d, rows, V1, d, e, st));
+    }
+    if (V1 < V) {
+      EpiArgs e; e.bias = fe.ctc_b + V1; e.out = dst + V1; e.ldo = V;
+      PROF(PC_CTC, gemm<T>(EPI_STORE_F32, ACT_NONE, A, d, (const T*)fe.ctc_w + (size_t)V1 * d, d, rows, V - V1, d, e, st));
+    }
     PROF(PC_CTC, log_softmax_rows(dst, rows, V, logp ? 1 : 0, ids, st));
     return CFM_OK;
   }
