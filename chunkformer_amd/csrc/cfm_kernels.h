@@ -28,6 +28,7 @@ int gemm(int epi, int act, const T* A, int lda, const T* W, int ldw, int M, int 
          hipStream_t st);
 
 void gemm_force_small_tiles(int v);
+void gemm_set_variant(int v);
 
 // LayerNorm over d (eps) of f32 rows -> T rows; optional 0/1 row mask on the output.
 // fused residual add of the previous sub-block: x += alpha * ymask[row] * y (y null = none)

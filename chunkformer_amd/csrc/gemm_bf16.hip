@@ -248,6 +248,7 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_256_kernel(const bf16* __res
   advance(t2, k2);
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
   if (grp == 1) asm volatile("s_barrier" ::: "memory");   // stagger group 1 by one segment
+  if constexpr (DIAG == 6) { if (grp == 1) __builtin_amdgcn_s_setprio(1); }   // static priority, later half
 
   // pending epilogue (tile finished in the previous MFMA segment), executed in the next LOAD segment
   int epi_t = -1;
@@ -296,11 +297,13 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_256_kernel(const bf16* __res
 #pragma unroll
           for (int j = 0; j < 8; ++j) asm volatile("" ::"v"(af[j]));
         } else {
+          if constexpr (DIAG == 5) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
           for (int i = 0; i < 4; ++i)
 #pragma unroll
             for (int j = 0; j < 8; ++j)
               acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[i], af[j], acc[i][j], 0, 0, 0);
+          if constexpr (DIAG == 5) __builtin_amdgcn_s_setprio(0);
         }
         __builtin_amdgcn_sched_barrier(0);
         asm volatile("s_barrier" ::: "memory");
@@ -783,6 +786,11 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_spread_kernel(const bf16* __
   if (grp == 0) asm volatile("s_barrier" ::: "memory");
 }
 
+// A/B switch for in-process experiments ("gemm_variant" model option): 5 = s_setprio(1) around each
+// MFMA segment, 6 = static priority 1 for the later wave group (MI355X_MICROARCH.md, two waves per SIMD)
+static int g_gemm_variant = 0;
+void gemm_set_variant(int v) { g_gemm_variant = v; }
+
 static int ring_mode() {
   static int v = -1;
   if (v < 0) { const char* e = getenv("CFM_GEMM_RING"); v = e ? atoi(e) : 0; }
@@ -801,8 +809,9 @@ static int launch256(const bf16* A, int lda, const bf16* W, int ldw, int M, int 
     n_cu = (n_cu + 7) / 8 * 8;
   }
   const int grid = tiles <= n_cu ? tiles : n_cu;   // persistent: one 512-thread block per CU
-  static int diag = -1;
-  if (diag < 0) { const char* e = getenv("CFM_GEMM_DIAG"); diag = e ? atoi(e) : 0; }
+  static int diag_env = -1;
+  if (diag_env < 0) { const char* e = getenv("CFM_GEMM_DIAG"); diag_env = e ? atoi(e) : 0; }
+  const int diag = g_gemm_variant ? g_gemm_variant : diag_env;
   const EpiArgs& ep = ep_in;
   if constexpr (EPI == EPI_STORE || EPI == EPI_QKV || EPI == EPI_GLU) {
     if (ring_mode() == 2 && diag == 0 && K % 512 == 0 && (size_t)256 * ldw * 2 < (1u << 31) &&
@@ -832,6 +841,10 @@ static int launch256(const bf16* A, int lda, const bf16* W, int ldw, int M, int 
     hipLaunchKernelGGL((gemm_bf16_256_kernel<EPI, ACT, 1>), dim3(grid), dim3(512), 0, st, A, lda, W, ldw, M, N, K, ep);
   else if (diag == 2)
     hipLaunchKernelGGL((gemm_bf16_256_kernel<EPI, ACT, 2>), dim3(grid), dim3(512), 0, st, A, lda, W, ldw, M, N, K, ep);
+  else if (diag == 5)
+    hipLaunchKernelGGL((gemm_bf16_256_kernel<EPI, ACT, 5>), dim3(grid), dim3(512), 0, st, A, lda, W, ldw, M, N, K, ep);
+  else if (diag == 6)
+    hipLaunchKernelGGL((gemm_bf16_256_kernel<EPI, ACT, 6>), dim3(grid), dim3(512), 0, st, A, lda, W, ldw, M, N, K, ep);
   else
     hipLaunchKernelGGL((gemm_bf16_256_kernel<EPI, ACT, 0>), dim3(grid), dim3(512), 0, st, A, lda, W, ldw, M, N, K, ep);
   CFM_CHECK_LAUNCH();

@@ -600,6 +600,7 @@ cfm_status cfm_model_set_option(cfm_model* m, const char* key, int64_t value) {
   if (!std::strcmp(key, "ring_attention")) { m->use_ring_attention = value != 0; return CFM_OK; }
   if (!std::strcmp(key, "fused_ffn")) { m->use_fused_ffn = value != 0; return CFM_OK; }
   if (!std::strcmp(key, "ffn_variant")) { ffn_set_variant((int)value); return CFM_OK; }
+  if (!std::strcmp(key, "gemm_variant")) { gemm_set_variant((int)value); return CFM_OK; }
   if (!std::strcmp(key, "attn_diag")) { m->attn_diag = (int)value; return CFM_OK; }
   if (!std::strcmp(key, "profile_reset")) {
     m->prof_collect();
