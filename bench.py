@@ -118,7 +118,15 @@ def main():
     ap.add_argument("--minutes", type=float, default=240.0, help="audio minutes per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-breakdown", action="store_true")
+    ap.add_argument("--config", default="masked", choices=["masked", "endless", "full"],
+                    help="masked = configs[1] (default, the headline line); endless = configs[3] (16 h "
+                         "endless_decode, graph-replayed segments); full = configs[4] (full attention, B=256)")
+    ap.add_argument("--hours", type=float, default=16.0, help="endless: audio hours")
+    ap.add_argument("--tbd", type=int, default=1800, help="endless: total_batch_duration (s)")
+    ap.add_argument("--batch", type=int, default=256, help="full: utterances of T=3000 frames")
     args = ap.parse_args()
+    if args.config != "masked":
+        return bench_single(args)
 
     rank, world, local = init_from_env()
     torch.cuda.set_device(local)
@@ -253,6 +261,95 @@ def main():
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def bench_single(args):
+    """configs[3] (endless_decode, 16 h, one GPU) and configs[4] (full attention, B=256 x 30 s):
+    one JSON line each, same keys as the headline line.  These run on one GPU only (configs[3] is
+    sequential by construction; configs[4] is a parity / roofline check): --gpus must be 1."""
+    from chunkformer_amd.model import ChunkFormerModel
+    if args.gpus != 1:
+        raise SystemExit(f"--config {args.config} runs on one GPU")
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    model = ChunkFormerModel(LARGE, synthetic_state_dict(LARGE, 0), dtype=args.dtype, device=dev)
+    enc = model.encoder
+    g = torch.Generator(device=dev).manual_seed(1234)
+    d_, ff_ = LARGE.d_model, LARGE.ffn_dim
+    if args.config == "endless":
+        T = int(args.hours * 3600 * 100)
+        x = torch.randn(T, 80, generator=g, device=dev)
+        frames = T
+
+        def step():
+            return model.endless_decode(x, C, L, R, total_batch_duration=args.tbd, return_timestamps=False)
+        from chunkformer_amd.model import endless_segments
+        trunc, segs = endless_segments(T, C, L, R, args.tbd, LARGE.num_blocks, LARGE.kernel_size)
+        seg_len = max(b - a for a, b, _, _ in segs)
+        prof_x = [x[:seg_len]]
+        prof_call = lambda: enc.forward_parallel_chunk(prof_x, torch.tensor([seg_len], dtype=torch.int32), C, L, R)
+        rows = sum(chunks_of(seg_len, C) for _ in range(1)) * C
+        roof_cls, attn_fl = "ffn_w1_gemm", None
+        workload = (f"endless_decode over one {args.hours:g} h utterance (synthetic N(0,1) fbank), C=64 L=128 "
+                    f"R=128, total_batch_duration={args.tbd}: {len(segs)} segments of <= {seg_len} frames "
+                    f"(trunc {trunc} rows kept each), att/cnn caches carried, middle segments replayed from one "
+                    f"captured HIP graph (front-end + 12 blocks + after_norm + CTC argmax)")
+        extra = {"segments": len(segs), "segment_frames": seg_len, "truncated_context_size": trunc}
+    else:
+        B, T = args.batch, 3000
+        xs = torch.randn(B, T, 80, generator=g, device=dev)
+        lens = torch.full((B,), T, dtype=torch.int32)
+        frames = B * T
+
+        def step():
+            return model.encode(xs, lens, -1, -1, -1)
+        prof_call = step
+        Tp = 1 + (T - 15) // 8
+        rows = B * Tp
+        roof_cls = "chunk_attention"
+        # dense rel-pos attention per layer: scores T'xT', rel-pos band T'x(2T'-1), P.V T'xT' (x d, x2)
+        attn_fl = 2.0 * B * Tp * d_ * (Tp + (2 * Tp - 1) + Tp)
+        workload = (f"forward_encoder full attention (chunk_size=-1), B={B} x T={T} frames (30 s, T'={Tp}), "
+                    f"synthetic N(0,1) fbank, padded batch")
+        extra = {"batch": B, "frames_per_utt": T, "subsampled_frames": Tp}
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    value = frames * args.steps / dt
+    # roofline kernel: per-launch time from in-stream HIP events on an eager call of the same shape
+    enc.set_option("profile_reset", 1)
+    enc.set_option("profile", 1 << _lib.PROFILE_CLASSES.index(roof_cls))
+    prof_call()
+    torch.cuda.synchronize()
+    enc.set_option("profile", 0)
+    ms1, n1 = _lib.profile_read(enc._h)[roof_cls]
+    avg_s = ms1 / max(n1, 1) / 1e3
+    peak = PEAK_TFLOPS[args.dtype]
+    if roof_cls == "ffn_w1_gemm":
+        fl_launch = 2.0 * rows * ff_ * d_
+        kname = "ffn_w1_gemm (gemm_bf16_256_kernel<STORE,SiLU>)"
+    else:
+        fl_launch = attn_fl
+        kname = "chunk_attention (chunk_attention_kernel<bf16>, full-attention descriptors)"
+    achieved = fl_launch / avg_s / 1e12 if n1 else None
+    res = {
+        "metric": METRIC, "value": round(value, 1), "unit": "audio-frames/s", "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
+        "data": "synthetic (N(0,1) 80-dim fbank, seeded random chunkformer-large weights; no checkpoint offline)",
+        "config": {"workload": workload, "config_index": 3 if args.config == "endless" else 4, **extra,
+                   "parallelism": "single GPU"},
+        "roofline": {"bound": "mfma", "kernel": kname, "achieved": round(achieved, 1) if achieved else None,
+                     "peak": peak, "unit": "TFLOP/s", "frac": round(achieved / peak, 4) if achieved else None,
+                     "traffic": None, "flops_per_launch": fl_launch, "avg_launch_ms": round(avg_s * 1e3, 4),
+                     "launches": n1},
+    }
+    print(json.dumps(res), flush=True)
 
 
 if __name__ == "__main__":

@@ -127,9 +127,7 @@ class ChunkFormerEncoder:
             cco = torch.empty_like(cci)
         ws_bytes = _lib.cfm_workspace_bytes_masked(self._h, N, C, L, R)
         ws = self._workspace(ws_bytes)
-        _lib.check(_lib.cfm_encode_masked(self._h, feats.data_ptr(), plan.data_ptr(), plan_dev.data_ptr(),
-                                          _lib.ptr(aci), _lib.ptr(cci), int(truncated_context_size), _lib.ptr(aco),
-                                          _lib.ptr(cco), out.data_ptr(), ws.data_ptr(), ws_bytes, self._stream()))
+        self._encode_masked_raw(feats, plan, plan_dev, aci, cci, int(truncated_context_size), aco, cco, out, ws)
         xs_lens = torch.tensor(out_lens, dtype=torch.int32, device=xs_origin_lens.device)
         offset += xs_lens.to(offset.device)
         if has_cache:
@@ -139,6 +137,25 @@ class ChunkFormerEncoder:
             r_cnn = torch.zeros(self.num_blocks, 0, 0, device=dev)
         self._last_plan = (plan, plan_dev)   # keep the uploaded plan alive until the stream consumed it
         return out.view(N, C, d), xs_lens, n_chunks, r_att, r_cnn, offset
+
+    def _encode_masked_raw(self, feats, plan, plan_dev, aci, cci, trunc, aco, cco, out, ws) -> None:
+        """One cfm_encode_masked launch sequence on the current stream: no allocation and no host
+        synchronisation, so it can be captured into a HIP graph (EndlessGraphRunner)."""
+        C, L, R = (int(plan[i]) for i in (5, 6, 7))
+        ws_bytes = _lib.cfm_workspace_bytes_masked(self._h, int(plan[1]), C, L, R)
+        if ws.numel() < ws_bytes:
+            raise ValueError(f"workspace {ws.numel()} B < {ws_bytes} B")
+        _lib.check(_lib.cfm_encode_masked(self._h, feats.data_ptr(), plan.data_ptr(), plan_dev.data_ptr(),
+                                          _lib.ptr(aci), _lib.ptr(cci), int(trunc), _lib.ptr(aco), _lib.ptr(cco),
+                                          out.data_ptr(), ws.data_ptr(), ws_bytes, self._stream()))
+
+    def _ctc_raw(self, enc: torch.Tensor, rows: int, logp, ids, ws) -> None:
+        """cfm_ctc_logprobs over the first `rows` rows of enc [*, d] (graph-capturable)."""
+        nbytes = _lib.cfm_ctc_workspace_bytes(self._h, rows)
+        if ws.numel() < nbytes:
+            raise ValueError(f"CTC workspace {ws.numel()} B < {nbytes} B")
+        _lib.check(_lib.cfm_ctc_logprobs(self._h, enc.data_ptr(), rows, _lib.ptr(logp), _lib.ptr(ids), ws.data_ptr(),
+                                         nbytes, self._stream()))
 
     @torch.no_grad()
     def masks(self, xs_origin_lens, chunk_size: int, left_context_size: int, right_context_size: int,

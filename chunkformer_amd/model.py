@@ -27,6 +27,7 @@ import torch
 
 from .config import EncoderConfig
 from .encoder import ChunkFormerEncoder
+from .streaming import EndlessGraphRunner
 
 Features = Union[torch.Tensor, np.ndarray, str]
 
@@ -173,6 +174,7 @@ class ChunkFormerModel:
         self.encoder = ChunkFormerEncoder(cfg, state_dict, device=device, dtype=dtype)
         self.device = self.encoder.device
         self.char_dict = char_dict
+        self._endless_runners: Dict[tuple, EndlessGraphRunner] = {}
 
     # ---------------------------------------------------------------- loading
     @classmethod
@@ -232,37 +234,40 @@ class ChunkFormerModel:
     def endless_decode(self, audio_path: Features, chunk_size: Optional[int] = 64,
                        left_context_size: Optional[int] = 128, right_context_size: Optional[int] = 128,
                        total_batch_duration: int = 1800, return_timestamps: bool = True,
-                       max_silence_duration: float = 0.5, return_encoder_out: bool = False):
+                       max_silence_duration: float = 0.5, return_encoder_out: bool = False,
+                       cuda_graph: bool = True):
         """chunkformer_model.py:321-459.  Segments of `total_batch_duration` seconds (halved,
         like the reference) go through forward_parallel_chunk with the attention/conv caches
         and `offset` carried; the CTC argmax runs per segment on the kept rows (row-wise, so
         identical to the reference's argmax over the concatenation).
         Returns text (with char_dict) or ids [1, T', 1] like the reference; with
-        `return_encoder_out` also the concatenated encoder output [1, T', d] (fp32)."""
+        `return_encoder_out` also the concatenated encoder output [1, T', d] (fp32).
+        `cuda_graph`: the full-size middle segments replay one captured HIP graph (front-end,
+        blocks with the caches carried, after_norm, CTC argmax); see streaming.py.  The
+        result is identical to the eager loop (same kernels, same plans)."""
         C = chunk_size if chunk_size is not None else 64
         L = left_context_size if left_context_size is not None else 128
         R = right_context_size if right_context_size is not None else 128
         cfg, enc, dev = self.config, self.encoder, self.device
         xs = _load_features(audio_path)
         trunc, segs = endless_segments(xs.shape[0], C, L, R, total_batch_duration, cfg.num_blocks, cfg.kernel_size)
-        offset = torch.zeros(1, dtype=torch.int, device=dev)
-        att_cache = torch.zeros(cfg.num_blocks, L, cfg.n_heads, 2 * cfg.head_dim, device=dev)
-        cnn_cache = torch.zeros(cfg.num_blocks, cfg.d_model, cfg.conv_lorder, device=dev)
-        xs_dev = xs.to(dev)
+        xs_dev = xs.to(dev, torch.float32)
         ids, outs = [], []
+        seg_len = max(stop - start for start, stop, _, _ in segs) if segs else 0
+        key = (C, L, R, trunc, seg_len, bool(return_encoder_out), bool(cuda_graph))
+        runner = self._endless_runners.get(key)
+        if runner is None:   # graphs are captured once per segment geometry and reused across calls
+            runner = EndlessGraphRunner(enc, C, L, R, trunc, seg_len, return_encoder_out, use_graph=cuda_graph)
+            self._endless_runners = {key: runner}
+        runner.reset()
+        offset = 0
         for start, stop, keep_trunc, _ in segs:
-            x = xs_dev[start:stop]
-            x_len = torch.tensor([x.shape[0]], dtype=torch.int)
-            eo, el, _, att_cache, cnn_cache, offset = enc.forward_parallel_chunk(
-                [x], x_len, C, L, R, att_cache, cnn_cache, trunc, offset)
-            n = int(el[0])
-            eo = eo.reshape(-1, eo.shape[-1])[:n]
-            if keep_trunc:
-                eo = eo[:trunc]
-            offset = offset - n + eo.shape[0]
-            if cfg.vocab > 0:
-                ids.append(enc.ctc_log_softmax(eo, want_logp=False)[1])
-            if return_encoder_out:
+            # forward_parallel_chunk with att/cnn caches carried; offset += len, then -= dropped rows
+            tok, eo, kept = runner.step(xs_dev[start:stop], offset, keep_trunc)
+            offset += kept
+            if tok is not None:
+                ids.append(tok)
+            if eo is not None:
                 outs.append(eo)
         tokens = torch.cat(ids).long().reshape(1, -1, 1) if ids else None
         if self.char_dict is not None and tokens is not None:

@@ -1,0 +1,149 @@
+"""HIP-graph replay of endless_decode's segment steps (BASELINE configs[3]).
+
+The reference's endless_decode (chunkformer_model.py:321-459) calls
+forward_parallel_chunk once per segment of one long utterance, carrying the attention
+/ conv caches (attention.py:466-467, convolution.py:228-230) and `offset` from one
+segment to the next, then runs the CTC head on the kept rows (436-438).
+
+Every segment between the first and the last has the same input length
+(step + 7 + rel_right fbank frames) and, once `offset` >= max(L, 7), the same plan:
+the packer's masks only look at `offset` through max(0, L - offset - 64c) and
+max(0, 7 - offset - 64c) (encoder.py:625-645, planner.cpp).  So one segment step --
+front-end, 12 blocks with caches in/out, after_norm, CTC argmax of the kept rows --
+is captured once into a HIP graph (torch.cuda.CUDAGraph over libcfm's stream-ordered,
+allocation-free C-ABI calls) and replayed for every middle segment.  The caches
+ping-pong between two fixed buffer pairs, so two graphs are captured (A -> B and
+B -> A).  The first segment (offset 0) and the ragged last segment run eagerly through
+the same entry points; each replayed segment's plan is re-derived on the host and
+compared with the captured one, so a plan mismatch falls back to the eager call
+instead of replaying the wrong masks.
+"""
+from __future__ import annotations
+
+from typing import List, Optional
+
+import torch
+
+from . import _lib
+
+
+class EndlessGraphRunner:
+    """Runs the segment schedule of one endless_decode call; middle segments by graph replay."""
+
+    def __init__(self, encoder, C: int, L: int, R: int, trunc: int, seg_len: int, want_out: bool,
+                 use_graph: bool = True):
+        self.enc = encoder
+        cfg = encoder.cfg
+        self.C, self.L, self.R, self.trunc = C, L, R, trunc
+        self.seg_len = seg_len
+        self.want_out = want_out
+        self.use_graph = use_graph
+        dev = encoder.device
+        self.dev = dev
+        nb, H, dk, d = cfg.num_blocks, cfg.n_heads, cfg.head_dim, cfg.d_model
+        # caches: pair 0 and pair 1 (ping-pong across graph replays)
+        self.att = [torch.zeros(nb, L, H, 2 * dk, device=dev) for _ in range(2)]
+        self.cnn = [torch.zeros(nb, d, cfg.conv_lorder, device=dev) for _ in range(2)]
+        self.cur = 0   # index of the pair holding the carried caches
+        self.graphs: List[Optional[torch.cuda.CUDAGraph]] = [None, None]
+        self.g_plan = None
+        self.vocab = cfg.vocab
+
+    def reset(self) -> None:
+        """Start a new utterance: zero caches (chunkformer_model.py:376-379); graphs are kept."""
+        self.cur = 0
+        self.att[0].zero_()
+        self.cnn[0].zero_()
+
+    # ------------------------------------------------------------------ eager step
+    def _eager(self, x: torch.Tensor, offset: int):
+        enc = self.enc
+        n_frames = x.shape[0]
+        plan, n_chunks, out_lens = _lib.plan_masked([n_frames], [offset], self.C, self.L, self.R)
+        N = n_chunks[0]
+        plan_dev = enc._upload(plan)
+        out = torch.empty(N * self.C, enc.cfg.d_model, device=self.dev)
+        ws = enc._workspace(_lib.cfm_workspace_bytes_masked(enc._h, N, self.C, self.L, self.R))
+        src, dst = self.cur, 1 - self.cur
+        enc._encode_masked_raw(x.contiguous(), plan, plan_dev, self.att[src], self.cnn[src], self.trunc,
+                               self.att[dst], self.cnn[dst], out, ws)
+        self.cur = dst
+        self._keep = (plan, plan_dev)
+        return out, out_lens[0]
+
+    # ------------------------------------------------------------------ graph step
+    def _capture(self, offset: int):
+        enc = self.enc
+        plan, n_chunks, out_lens = _lib.plan_masked([self.seg_len], [offset], self.C, self.L, self.R)
+        N = n_chunks[0]
+        self.g_plan = plan
+        self.g_plan_dev = enc._upload(plan)
+        self.g_n = out_lens[0]
+        self.g_rows = min(self.g_n, self.trunc)
+        self.g_feats = torch.zeros(self.seg_len, enc.cfg.input_dim, device=self.dev)
+        self.g_out = torch.empty(N * self.C, enc.cfg.d_model, device=self.dev)
+        self.g_ws = torch.empty(_lib.cfm_workspace_bytes_masked(enc._h, N, self.C, self.L, self.R),
+                                dtype=torch.uint8, device=self.dev)
+        if self.vocab > 0:
+            self.g_ids = torch.empty(self.g_rows, dtype=torch.int32, device=self.dev)
+            self.g_ctc_ws = torch.empty(_lib.cfm_ctc_workspace_bytes(enc._h, self.g_rows), dtype=torch.uint8,
+                                        device=self.dev)
+        torch.cuda.current_stream(self.dev).synchronize()
+
+        def body(src: int):
+            dst = 1 - src
+            enc._encode_masked_raw(self.g_feats, self.g_plan, self.g_plan_dev, self.att[src], self.cnn[src],
+                                   self.trunc, self.att[dst], self.cnn[dst], self.g_out, self.g_ws)
+            if self.vocab > 0:
+                enc._ctc_raw(self.g_out, self.g_rows, None, self.g_ids, self.g_ctc_ws)
+
+        # warm the launch path on a side stream (libcfm's one-time queries happen outside capture),
+        # on scratch caches so the carried state is untouched
+        saved = [(a.clone(), c.clone()) for a, c in zip(self.att, self.cnn)]
+        side = torch.cuda.Stream(self.dev)
+        side.wait_stream(torch.cuda.current_stream(self.dev))
+        with torch.cuda.stream(side):
+            body(0)
+        torch.cuda.current_stream(self.dev).wait_stream(side)
+        for src in (0, 1):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=side):
+                body(src)
+            self.graphs[src] = g
+        for (a, c), (sa, sc) in zip(zip(self.att, self.cnn), saved):
+            a.copy_(sa)
+            c.copy_(sc)
+
+    def _replayable(self, n_frames: int, offset: int) -> bool:
+        if not self.use_graph or n_frames != self.seg_len:
+            return False
+        if self.g_plan is None:   # capture only where the plan no longer depends on offset
+            return offset >= max(self.L, 7)
+        plan, _, _ = _lib.plan_masked([n_frames], [offset], self.C, self.L, self.R)
+        return bool(torch.equal(plan, self.g_plan))
+
+    def step(self, x: torch.Tensor, offset: int, keep_trunc: bool):
+        """One segment: returns (CTC ids of the kept rows or None, kept encoder rows or None, kept row
+        count).  Rows are kept as chunkformer_model.py:419-431 keeps them: eo[:n], then [:trunc]."""
+        if self._replayable(x.shape[0], offset):
+            if self.graphs[0] is None:
+                self._capture(offset)
+            self.g_feats.copy_(x)
+            self.graphs[self.cur].replay()
+            self.cur = 1 - self.cur
+            eo = self.g_out[: self.g_n]
+            if keep_trunc:
+                eo = eo[: self.trunc]
+            if eo.shape[0] == self.g_rows and self.vocab > 0:
+                ids = self.g_ids.clone()
+            else:
+                ids = self.enc.ctc_log_softmax(eo, want_logp=False)[1] if self.vocab > 0 else None
+            return ids, (eo.clone() if self.want_out else None), eo.shape[0]
+        out, n = self._eager(x, offset)
+        eo = out[:n]
+        if keep_trunc:
+            eo = eo[: self.trunc]
+        ids = None
+        if self.vocab > 0 and eo.shape[0] > 0:
+            ids = self.enc.ctc_log_softmax(eo, want_logp=False)[1]
+        return ids, (eo if self.want_out else None), eo.shape[0]

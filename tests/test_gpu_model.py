@@ -76,3 +76,19 @@ def test_encode_returns_lengths(small):
     out, ol = models["fp32"].encode(xp, torch.tensor(lens), 16, 32, 32)
     np.testing.assert_allclose(out.cpu().numpy(), g["pc_out"], atol=1e-4, rtol=0)
     assert ol.tolist() == g["pc_mask"].squeeze(1).sum(-1).tolist()
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_endless_graph_replay_equals_eager(small, dtype):
+    """configs[3] path: the HIP-graph-replayed middle segments (streaming.py) give exactly the
+    eager segment loop's encoder rows and ids (same kernels, same plans, caches carried)."""
+    from chunkformer_amd.weights import synthetic_features
+    g, models = small
+    C, L, R, tbd = (int(v) for v in g["endless_clrt"])
+    x = synthetic_features([6000], int(g["endless_seed"]))[0]
+    m = models[dtype]
+    ids_e, eo_e = m.endless_decode(x, C, L, R, total_batch_duration=tbd, return_encoder_out=True, cuda_graph=False)
+    ids_g, eo_g = m.endless_decode(x, C, L, R, total_batch_duration=tbd, return_encoder_out=True, cuda_graph=True)
+    assert eo_g.shape == eo_e.shape
+    assert torch.equal(eo_g, eo_e)
+    assert torch.equal(ids_g, ids_e)
