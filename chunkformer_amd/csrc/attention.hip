@@ -291,7 +291,6 @@ __global__ __launch_bounds__(512, 1) void chunk_attention_ring_kernel(
   }
   __syncthreads();
 
-  const float scale = 0.125f;
   const int i0 = wq * 16;
   // masked-batch descriptors (planner.cpp, C <= 64: one query block per chunk): chunk c's queries
   // are rows c*C.., its window starts at flat KV row c*C, P_BASE = C-1, every query row valid;
@@ -355,11 +354,15 @@ __global__ __launch_bounds__(512, 1) void chunk_attention_ring_kernel(
         const f32x4 v1_ = *reinterpret_cast<const f32x4*>(uv + 64 + s * 32 + 8 * g + 4);
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
+          // the 1/sqrt(dk) = 2^-3 scale is folded into both operands: exact in bf16 and in the f32
+          // accumulation, so (qu.k + bd) * 0.125 is reproduced bit for bit
           const float qf = (float)qraw[s][e];
-          qu[s][e] = (bf16)(qf + (e < 4 ? u0[e] : u1[e - 4]));
-          qv[s][e] = (bf16)(qf + (e < 4 ? v0_[e] : v1_[e - 4]));
+          qu[s][e] = (bf16)((qf + (e < 4 ? u0[e] : u1[e - 4])) * 0.125f);
+          qv[s][e] = (bf16)((qf + (e < 4 ? v0_[e] : v1_[e - 4])) * 0.125f);
         }
       }
+      // interior chunks see the whole window (key_lo = 0, key_hi = W): no per-score mask
+      const bool need_mask = __builtin_amdgcn_readfirstlane((key_lo != (key_lo & ~15)) || ((key_hi - (key_lo & ~15)) & 63)) != 0;
       const int jb = key_lo & ~15;
       f32x4 S[5][4];
       float mx = -INFINITY;
@@ -383,7 +386,9 @@ __global__ __launch_bounds__(512, 1) void chunk_attention_ring_kernel(
           S[t][st] = a;
         }
         // band^T[P row kb + 16pt + 4g + rr][query fr] -> scratch[query][band pos], in two 32-key halves
-        // (3 P subtiles each, keeps the per-wave scratch at 16 x 48 bf16)
+        // (3 P subtiles each, keeps the per-wave scratch at 16 x 48 bf16); the second half's first
+        // subtile is the first half's last one (kb + 32), so 5 of the 6 products are computed
+        f32x4 shared_pt;
 #pragma unroll
         for (int hh = 0; hh < 2; ++hh) {
           if (diag == 2) {   // timing experiment: no band / skew
@@ -393,7 +398,7 @@ __global__ __launch_bounds__(512, 1) void chunk_attention_ring_kernel(
               for (int rr = 0; rr < 4; ++rr) {
                 const int st = 2 * hh + st2;
                 const int j = j0 + 32 * hh + 16 * st2 + 4 * g + rr;
-                float sv = S[t][st][rr] * scale;
+                float sv = S[t][st][rr];
                 if (j < key_lo || j >= key_hi) sv = -INFINITY;
                 S[t][st][rr] = sv;
                 mx = fmaxf(mx, sv);
@@ -403,12 +408,17 @@ __global__ __launch_bounds__(512, 1) void chunk_attention_ring_kernel(
           const int kb = p_base - i0 - 15 + j0 + 32 * hh;
 #pragma unroll
           for (int pt = 0; pt < 3; ++pt) {
-            const int prow = min(max(kb + 16 * pt + fr, 0), p_rows - 1);
             f32x4 a = (f32x4){0.f, 0.f, 0.f, 0.f};
+            if (hh == 1 && pt == 0) {
+              a = shared_pt;
+            } else {
+              const int prow = min(max(kb + 16 * pt + fr, 0), p_rows - 1);
 #pragma unroll
-            for (int s = 0; s < 2; ++s)
-              a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<const bf16x8*>(pl + sw128(prow, 4 * s + g)),
-                                                          qv[s], a, 0, 0, 0);
+              for (int s = 0; s < 2; ++s)
+                a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<const bf16x8*>(pl + sw128(prow, 4 * s + g)),
+                                                            qv[s], a, 0, 0, 0);
+            }
+            if (hh == 0 && pt == 2) shared_pt = a;
             // rel_shift by the reshape trick: row fr is written at pitch 49 (+1) and read back at
             // pitch 48, so query fr's band for key jj starts 16 - fr elements later: the reads
             // are aligned 8-B vectors (4 keys), the writes 2-B aligned (LDS takes unaligned b64)
@@ -426,17 +436,30 @@ __global__ __launch_bounds__(512, 1) void chunk_attention_ring_kernel(
                          : "v"(scr_base + 2u * (unsigned)(fr * (SCR_PITCH - 1) + 16 + 16 * st2 + 4 * g))
                          : "memory");
           asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(bdv4[0]), "+v"(bdv4[1])::"memory");
+          if (need_mask) {
 #pragma unroll
-          for (int st2 = 0; st2 < 2; ++st2) {
-            const int st = 2 * hh + st2;
+            for (int st2 = 0; st2 < 2; ++st2) {
+              const int st = 2 * hh + st2;
 #pragma unroll
-            for (int rr = 0; rr < 4; ++rr) {
-              const int jj = 16 * st2 + 4 * g + rr;
-              float sv = (S[t][st][rr] + (float)bdv4[st2][rr]) * scale;
-              const int j = j0 + 32 * hh + jj;
-              if (j < key_lo || j >= key_hi) sv = -INFINITY;
-              S[t][st][rr] = sv;
-              mx = fmaxf(mx, sv);
+              for (int rr = 0; rr < 4; ++rr) {
+                const int jj = 16 * st2 + 4 * g + rr;
+                float sv = S[t][st][rr] + (float)bdv4[st2][rr];
+                const int j = j0 + 32 * hh + jj;
+                if (j < key_lo || j >= key_hi) sv = -INFINITY;
+                S[t][st][rr] = sv;
+                mx = fmaxf(mx, sv);
+              }
+            }
+          } else {
+#pragma unroll
+            for (int st2 = 0; st2 < 2; ++st2) {
+              const int st = 2 * hh + st2;
+#pragma unroll
+              for (int rr = 0; rr < 4; ++rr) {
+                const float sv = S[t][st][rr] + (float)bdv4[st2][rr];
+                S[t][st][rr] = sv;
+                mx = fmaxf(mx, sv);
+              }
             }
           }
         }
@@ -445,6 +468,7 @@ __global__ __launch_bounds__(512, 1) void chunk_attention_ring_kernel(
       mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
       if (mx == -INFINITY) mx = 0.f;   // fully masked query: every p = 0, output 0 (reference: NaN -> 0)
+      const float mxl = mx * 1.4426950408889634f;
       float l = 0.f;
 #pragma unroll
       for (int t = 0; t < 5; ++t)
@@ -452,7 +476,7 @@ __global__ __launch_bounds__(512, 1) void chunk_attention_ring_kernel(
         for (int st = 0; st < 4; ++st)
 #pragma unroll
           for (int rr = 0; rr < 4; ++rr) {
-            const float p = __expf(S[t][st][rr] - mx);
+            const float p = __builtin_amdgcn_exp2f(fmaf(S[t][st][rr], 1.4426950408889634f, -mxl));
             S[t][st][rr] = p;
             l += p;
           }

@@ -21,6 +21,8 @@ struct EpiArgs {
   int ldx = 0;
   const uint8_t* rowmask = nullptr;  // RESID: per-row 0/1 multiplier (null = all 1)
   int d = 0;                     // QKV: model dim
+  int col_group = 0;             // bf16 256-tile walk: column tiles per group (0 = all; tiles ordered group, row, col)
+  int store_mode = 0;            // bf16 epilogue stores: 0 = plain, 1 = sc1 (drop the line from L2), 2 = nt
 };
 
 template <typename T>

@@ -72,14 +72,22 @@ CFM_DEV f32x4 act4(f32x4 v) {
 }
 // store two packed 16-column blocks (x = block 0, y = block 1) of row `row` after the swap
 template <bool NOST = false>
-CFM_DEV void store_pair16(bf16* base, size_t ld, int row, int g, u32x2_t x, u32x2_t y) {
+CFM_DEV void store_pair16(bf16* base, size_t ld, int row, int g, u32x2_t x, u32x2_t y, int sm = 0) {
   const auto r0 = __builtin_amdgcn_permlane16_swap(x[0], y[0], false, false);
   const auto r1 = __builtin_amdgcn_permlane16_swap(x[1], y[1], false, false);
   const int col = 16 * (g & 1) + 8 * (g >> 1);
-  if constexpr (NOST)   // timing experiment: values computed, not stored
+  const u32x4 v = (u32x4){r0[0], r1[0], r0[1], r1[1]};
+  u32x4* p = reinterpret_cast<u32x4*>(base + (size_t)row * ld + col);
+  if constexpr (NOST) {   // timing experiment: values computed, not stored
     asm volatile("" ::"v"(r0[0]), "v"(r1[0]), "v"(r0[1]), "v"(r1[1]));
-  else
-    *reinterpret_cast<u32x4*>(base + (size_t)row * ld + col) = (u32x4){r0[0], r1[0], r0[1], r1[1]};
+  } else {
+    if (sm == 1)
+      asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+    else if (sm == 2)
+      __builtin_nontemporal_store(v, p);
+    else
+      *p = v;
+  }
 }
 
 template <int EPI, int ACT, bool NOST = false>
@@ -118,7 +126,7 @@ CFM_DEV void tile_epilogue(f32x4 (&acc)[4][8], int tm, int tn, int wm, int wn, i
         o[p] = (u32x2_t){pack_bf16x2(a[0] * fast_sigmoid(gt[0]), a[1] * fast_sigmoid(gt[1])),
                          pack_bf16x2(a[2] * fast_sigmoid(gt[2]), a[3] * fast_sigmoid(gt[3]))};
       }
-      if (m < M) store_pair16<NOST>(base, ep.ldo, m, g, o[0], o[1]);
+      if (m < M) store_pair16<NOST>(base, ep.ldo, m, g, o[0], o[1], ep.store_mode);
     }
   } else {   // EPI_STORE / EPI_QKV: bf16 out, pairs (0,1) and (2,3)
 #pragma unroll
@@ -146,7 +154,7 @@ CFM_DEV void tile_epilogue(f32x4 (&acc)[4][8], int tm, int tn, int wm, int wn, i
         const f32x4 v0 = act4<ACT>(acc[2 * p][j]), v1 = act4<ACT>(acc[2 * p + 1][j]);
         const u32x2_t x = (u32x2_t){pack_bf16x2(v0[0], v0[1]), pack_bf16x2(v0[2], v0[3])};
         const u32x2_t y = (u32x2_t){pack_bf16x2(v1[0], v1[1]), pack_bf16x2(v1[2], v1[3])};
-        if (m < M) store_pair16<NOST>(base, ld, m, g, x, y);
+        if (m < M) store_pair16<NOST>(base, ld, m, g, x, y, ep.store_mode);
       }
     }
   }
@@ -180,6 +188,10 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_256_kernel(const bf16* __res
   const int grp = __builtin_amdgcn_readfirstlane(wid >> 2);
 
   const int nbn = N >> 8, nbm = (M + 255) >> 8, T = nbn * nbm;
+  // tile order: column groups of cgw tiles, then rows, then the columns of the group
+  const int cgw = (ep.col_group > 0 && nbn % ep.col_group == 0) ? ep.col_group : nbn;
+  auto tile_m = [&](int t) { return (t % (nbm * cgw)) / cgw; };
+  auto tile_n = [&](int t) { return (t / (nbm * cgw)) * cgw + t % cgw; };
   const int G = gridDim.x;
   int t_first, t_step, t_end;
   if (G >= T) {   // one tile per block: bijective XCD remap
@@ -200,7 +212,7 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_256_kernel(const bf16* __res
   // ---- LDS-DMA: wave w, instruction i covers tile rows (w*4+i)*8 .. +8 (1 KiB, lane-linear);
   // row = (w*4+i)*8 + lane/8, its XOR key (row>>1)&7 = (4i + lane/16) & 7 (pre-swizzled source)
   auto stage_a = [&](int t, int kt, int slot) {
-    const int tm = t / nbn;
+    const int tm = tile_m(t);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int srow = (wid * 4 + i) * 8 + (lane >> 3);
@@ -212,7 +224,7 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_256_kernel(const bf16* __res
     }
   };
   auto stage_w = [&](int t, int kt, int slot) {
-    const int tn = t - (t / nbn) * nbn;
+    const int tn = tile_n(t);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int srow = (wid * 4 + i) * 8 + (lane >> 3);
@@ -263,10 +275,10 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_256_kernel(const bf16* __res
         // ================= LOAD segment: (epilogue of the previous tile), fragments of (s, ss), DMA issue
         if (ss == 0 && kt == 0) {
           if (epi_t >= 0) {
-            if constexpr (DIAG != 3) tile_epilogue<EPI, ACT>(acc, epi_t / nbn, epi_t % nbn, wm, wn, fr, g, M, ep);
+            if constexpr (DIAG != 3) tile_epilogue<EPI, ACT>(acc, tile_m(epi_t), tile_n(epi_t), wm, wn, fr, g, M, ep);
             epi_t = -1;
           }
-          seed_bias(acc, ep.bias, t % nbn, wn, g);
+          seed_bias(acc, ep.bias, tile_n(t), wn, g);
         }
         const int pos = ((ss * 4 + g) ^ key) << 4;
         const unsigned wa = lds_base + (unsigned)(ws - smem) + wrow + pos;
@@ -315,7 +327,7 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_256_kernel(const bf16* __res
     }
   }
   // last tile's epilogue (no MFMA partner left), then rebalance the barrier count
-  if (epi_t >= 0 && DIAG != 3) tile_epilogue<EPI, ACT>(acc, epi_t / nbn, epi_t % nbn, wm, wn, fr, g, M, ep);
+  if (epi_t >= 0 && DIAG != 3) tile_epilogue<EPI, ACT>(acc, tile_m(epi_t), tile_n(epi_t), wm, wn, fr, g, M, ep);
   if (grp == 0) asm volatile("s_barrier" ::: "memory");
 }
 
@@ -812,7 +824,13 @@ static int launch256(const bf16* A, int lda, const bf16* W, int ldw, int M, int 
   static int diag_env = -1;
   if (diag_env < 0) { const char* e = getenv("CFM_GEMM_DIAG"); diag_env = e ? atoi(e) : 0; }
   const int diag = g_gemm_variant ? g_gemm_variant : diag_env;
-  const EpiArgs& ep = ep_in;
+  EpiArgs ep = ep_in;
+  static int store_env = -1;
+  if (store_env < 0) { const char* e = getenv("CFM_STORE_MODE"); store_env = e ? atoi(e) : 0; }
+  if (store_env) ep.store_mode = store_env;
+  static int cg_env = -1;
+  if (cg_env < 0) { const char* e = getenv("CFM_GEMM_COLGROUP"); cg_env = e ? atoi(e) : 0; }
+  if (cg_env) ep.col_group = cg_env;
   if constexpr (EPI == EPI_STORE || EPI == EPI_QKV || EPI == EPI_GLU) {
     if (ring_mode() == 2 && diag == 0 && K % 512 == 0 && (size_t)256 * ldw * 2 < (1u << 31) &&
         (size_t)256 * lda * 2 < (1u << 31)) {

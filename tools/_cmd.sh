@@ -1,7 +1,5 @@
 set -e
 mkdir -p gpurun_out
-timeout -k 10 300 python3 -u -m pytest tests/test_gpu_model.py -x -v --timeout 120 --timeout-method thread > gpurun_out/gpu_tests_model.log 2>&1
-timeout -k 10 300 python3 bench.py --config endless --steps 2 --warmup 1 > gpurun_out/bench_endless.log 2>&1
-timeout -k 10 300 python3 bench.py --config full --steps 3 --warmup 1 > gpurun_out/bench_full.log 2>&1
-tail -1 gpurun_out/bench_endless.log
-tail -1 gpurun_out/bench_full.log
+timeout -k 10 300 python3 -u -m pytest tests/test_gpu_parity.py -x -q --timeout 120 --timeout-method thread > gpurun_out/parity.log 2>&1
+tail -2 gpurun_out/parity.log
+for i in 1 2; do timeout -k 10 120 python3 tools/layer_bench.py --layers 1 --iters 3 | grep chunk_attention; done
