@@ -342,8 +342,16 @@ __global__ __launch_bounds__(512, 1) void chunk_attention_ring_kernel(
     }
     if (active) {
       const int q_row0 = c * C;
-      const int rb = (c * C) % RING;   // ring row of window key 0
-      auto ring = [&](int j) { const int r = rb + j; return r >= RING ? r - RING : r; };
+      // Addresses split into a wave-uniform part and a lane constant: the window start rb, every
+      // tile / subtile start and the band's P row base kb0 are multiples of 16 (C % 16 == 0), so a
+      // 16-row subtile never straddles the ring wrap and the 16-B chunk swizzle of row base+fr is
+      // (fr >> 1) & 7 for every subtile.  Out-of-range band rows (edge chunks only) read finite
+      // LDS bytes whose products land in skew positions no valid (query, key) pair reads.
+      const int rb = __builtin_amdgcn_readfirstlane((c * C) % RING);   // ring row of window key 0
+      auto ring16 = [&](int j) { const int r = rb + j; return r >= RING ? r - RING : r; };   // j % 16 == 0
+      const int key8 = (fr >> 1) & 7;
+      const int frag_lane[2] = {fr * 128 + ((g ^ key8) << 4), fr * 128 + (((4 + g) ^ key8) << 4)};
+      const int vt_lane = fr * VT_PITCH_B + 8 * g;
       // ---- query fragments (B operands): lane (fr, g) = query i0+fr, dims 32s + 8g .. +7
       bf16x8 qu[2], qv[2];
 #pragma unroll
@@ -374,21 +382,44 @@ __global__ __launch_bounds__(512, 1) void chunk_attention_ring_kernel(
           for (int st = 0; st < 4; ++st) S[t][st] = (f32x4){-INFINITY, -INFINITY, -INFINITY, -INFINITY};
           continue;
         }
+        // all fragment reads of the tile first (K: 4 subtiles x 2, P: 5 band subtiles x 2), then the
+        // MFMAs back to back: one LDS latency per tile instead of one per MFMA pair
+        bf16x8 kf[4][2], pf[5][2];
+#pragma unroll
+        for (int st = 0; st < 4; ++st) {
+          const char* kb_ = kr + ring16(j0 + 16 * st) * 128;
+#pragma unroll
+          for (int s = 0; s < 2; ++s) kf[st][s] = *reinterpret_cast<const bf16x8*>(kb_ + frag_lane[s]);
+        }
         // S^T[key 16st + 4g + rr][query fr]
 #pragma unroll
         for (int st = 0; st < 4; ++st) {
-          const int rr_ = ring(j0 + 16 * st + fr);
           f32x4 a = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-          for (int s = 0; s < 2; ++s)
-            a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<const bf16x8*>(kr + sw128(rr_, 4 * s + g)), qu[s],
-                                                        a, 0, 0, 0);
+          for (int s = 0; s < 2; ++s) a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[st][s], qu[s], a, 0, 0, 0);
           S[t][st] = a;
         }
-        // band^T[P row kb + 16pt + 4g + rr][query fr] -> scratch[query][band pos], in two 32-key halves
-        // (3 P subtiles each, keeps the per-wave scratch at 16 x 48 bf16); the second half's first
-        // subtile is the first half's last one (kb + 32), so 5 of the 6 products are computed
-        f32x4 shared_pt;
+        const int kb0 = p_base - i0 - 15 + j0;
+        if (diag != 2) {
+#pragma unroll
+          for (int pt = 0; pt < 5; ++pt) {
+            const char* pb_ = pl + (kb0 + 16 * pt) * 128;
+#pragma unroll
+            for (int s = 0; s < 2; ++s) pf[pt][s] = *reinterpret_cast<const bf16x8*>(pb_ + frag_lane[s]);
+          }
+        }
+        // band^T[P row kb0 + 16pt + 4g + rr][query fr], pt = 0..4 (80 rows for 64 keys + 15 skew); the
+        // two 32-key halves use subtiles 0-2 and 2-4 -> scratch[query][band pos] (16 x 48 bf16 per wave)
+        f32x4 band[5];
+        if (diag != 2) {
+#pragma unroll
+          for (int pt = 0; pt < 5; ++pt) {
+            f32x4 a = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int s = 0; s < 2; ++s) a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pf[pt][s], qv[s], a, 0, 0, 0);
+            band[pt] = a;
+          }
+        }
 #pragma unroll
         for (int hh = 0; hh < 2; ++hh) {
           if (diag == 2) {   // timing experiment: no band / skew
@@ -405,20 +436,9 @@ __global__ __launch_bounds__(512, 1) void chunk_attention_ring_kernel(
               }
             continue;
           }
-          const int kb = p_base - i0 - 15 + j0 + 32 * hh;
 #pragma unroll
           for (int pt = 0; pt < 3; ++pt) {
-            f32x4 a = (f32x4){0.f, 0.f, 0.f, 0.f};
-            if (hh == 1 && pt == 0) {
-              a = shared_pt;
-            } else {
-              const int prow = min(max(kb + 16 * pt + fr, 0), p_rows - 1);
-#pragma unroll
-              for (int s = 0; s < 2; ++s)
-                a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<const bf16x8*>(pl + sw128(prow, 4 * s + g)),
-                                                            qv[s], a, 0, 0, 0);
-            }
-            if (hh == 0 && pt == 2) shared_pt = a;
+            const f32x4 a = band[2 * hh + pt];
             // rel_shift by the reshape trick: row fr is written at pitch 49 (+1) and read back at
             // pitch 48, so query fr's band for key jj starts 16 - fr elements later: the reads
             // are aligned 8-B vectors (4 keys), the writes 2-B aligned (LDS takes unaligned b64)
@@ -498,13 +518,13 @@ __global__ __launch_bounds__(512, 1) void chunk_attention_ring_kernel(
             pb[rr] = (bf16)S[t][2 * s][rr];
             pb[4 + rr] = (bf16)S[t][2 * s + 1][rr];
           }
-          const int ka = ring(j0 + 32 * s + 4 * g), kb2 = ring(j0 + 32 * s + 16 + 4 * g);
+          const char* va_ = vt + vt_lane + ring16(j0 + 32 * s) * 2;
+          const char* vb_ = vt + vt_lane + ring16(j0 + 32 * s + 16) * 2;
 #pragma unroll
           for (int nt = 0; nt < 4; ++nt) {
-            const char* vrow = vt + (16 * nt + fr) * VT_PITCH_B;
             typedef bf16 bf16x4 __attribute__((ext_vector_type(4)));
-            const bf16x4 lo = *reinterpret_cast<const bf16x4*>(vrow + ka * 2);
-            const bf16x4 hi = *reinterpret_cast<const bf16x4*>(vrow + kb2 * 2);
+            const bf16x4 lo = *reinterpret_cast<const bf16x4*>(va_ + 16 * nt * VT_PITCH_B);
+            const bf16x4 hi = *reinterpret_cast<const bf16x4*>(vb_ + 16 * nt * VT_PITCH_B);
             const bf16x8 va = (bf16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
             O[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va, pb, O[nt], 0, 0, 0);
           }
