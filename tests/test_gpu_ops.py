@@ -37,7 +37,8 @@ def _close(got, exp, tol):
 
 
 SHAPES = [(1000, 512, 512), (700, 2048, 512), (513, 512, 2048), (256, 256, 4608), (300, 48, 128),
-          (70001, 512, 512), (33000, 2048, 512),   # these two run the persistent multi-tile path
+          (70001, 512, 512), (33000, 2048, 512),   # these two run the K = 512 weight-in-registers kernel
+          (40000, 1536, 512),
           (1000, 256, 128), (4097, 768, 384)]      # shortest ring K (4 steps); K % 128 != 0 (K-64 kernel)
 MODES = [("bf16", 0), ("bf16", 1), ("fp32", 0)]
 
@@ -91,11 +92,12 @@ def test_gemm_store_f32_and_resid(L, mode):
 
 
 @pytest.mark.parametrize("mode", MODES)
-def test_gemm_qkv_and_glu(L, mode):
+@pytest.mark.parametrize("M", [900, 40000])   # 40000 rows: the K = 512 weight-in-registers kernel
+def test_gemm_qkv_and_glu(L, mode, M):
     dt, small = mode
     tdt = torch.bfloat16 if dt == "bf16" else torch.float32
     code = L.DTYPE_BF16 if dt == "bf16" else L.DTYPE_F32
-    d, M, Lc = 512, 900, 5
+    d, Lc = 512, 5
     g = torch.Generator(device="cuda").manual_seed(9)
     A = (torch.randn(M, d, device="cuda", generator=g) * 0.5).to(tdt)
     W = (torch.randn(3 * d, d, device="cuda", generator=g) / d ** 0.5).to(tdt)

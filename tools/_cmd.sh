@@ -1,5 +1,4 @@
 set -e
-mkdir -p gpurun_out
-timeout -k 10 300 python3 -u -m pytest tests/test_gpu_parity.py -x -q --timeout 120 --timeout-method thread > gpurun_out/parity.log 2>&1
-tail -2 gpurun_out/parity.log
-for i in 1 2; do timeout -k 10 120 python3 tools/layer_bench.py --layers 1 --iters 3 | grep chunk_attention; done
+for d in 0 1 3 4 6 7; do echo "== wst diag $d"; CFM_GEMM_DIAG=$d timeout -k 10 120 python3 tools/gemm_bench.py --iters 20 --only ffn_w1 2>&1 | grep -v amdgpu; done
+echo "== 256 kernel"; CFM_GEMM_WST=0 timeout -k 10 120 python3 tools/gemm_bench.py --iters 20 2>&1 | grep -v amdgpu
+echo "== wst"; timeout -k 10 120 python3 tools/gemm_bench.py --iters 20 2>&1 | grep -v amdgpu
