@@ -25,6 +25,7 @@
 #include "cfm_kernels.h"
 #include "gemm_bf16_epi.h"
 #include <cstdlib>
+#include <type_traits>
 
 namespace cfm {
 
@@ -186,9 +187,356 @@ __global__ __launch_bounds__(256, 1) void gemm_wst_kernel(const bf16* __restrict
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// Software-pipelined variant ("wsp"): same data flow as gemm_wst_kernel, but with ONE wave per SIMD
+// nothing else hides the non-MFMA work, so every K-step is laid out by hand as 32 MFMA gaps:
+//   * the 8 ds_read_b128 of the NEXT step's A fragments sit in gaps 0, 2, .., 14;
+//   * the 2 LDS-DMA pieces of step y + 15 in gaps 6 and 22;
+//   * the PREVIOUS tile's epilogue (bias-seeded accumulators double-buffered: the tile computes
+//     into acc[BUF] while acc[1 - BUF] is drained) is cut into micro-ops (scale, exp2, +1, rcp,
+//     mul, pack, permlane16 swap, one 16-B store, re-seed) spread evenly over the gaps, one
+//     epilogue group (a 32-column x 16-row piece) per K-step;
+//   * __builtin_amdgcn_sched_barrier(0) after every gap keeps hipcc from regrouping them.
+// An MFMA (16x16x32 bf16) occupies 16 cycles of which it holds vector issue for 8, so one or two
+// VALU micro-ops per gap ride for free; the MFMA asm is opaque to the compiler's hazard
+// recognizer, which is fine here: every VALU access to an accumulator buffer is at least 11
+// MFMAs away from the last MFMA that wrote it (or an explicit s_nop pads the gap).
+// in-place LDS reads ("+v": the destination keeps its register, so hipcc does not rename the
+// fragment / accumulator buffers between steps and pay for it in copies and pressure)
+template <int OFF>
+CFM_DEV void lds_read_into(f32x4& v, unsigned addr) {
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "+v"(v) : "v"(addr), "i"(OFF));
+}
+template <int OFF>
+CFM_DEV void lds_read_into(bf16x8& v, unsigned addr) {
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "+v"(v) : "v"(addr), "i"(OFF));
+}
+
+namespace {
+template <int B, int E, class F>
+CFM_DEV void sfor(F&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    sfor<B + 1, E>(f);
+  }
+}
+// micro-ops of epilogue group s (0..7).  STORE/QKV: two halves (one 16-column n-block each) of
+// [activation ops on 4 values, 2 packs], then 2 permlane swaps, 1 store, 2 re-seeds.
+// GLU: group s = (m-block s/2, channel half s%1): 20 sigmoid-gate ops + 2 packs (+ swaps and the
+// store on odd s), 2 re-seeds.
+template <int ACT>
+constexpr int wsp_half() { return (ACT == ACT_SILU ? 20 : ACT == ACT_RELU ? 4 : 0) + 2; }
+template <int EPI, int ACT>
+constexpr int wsp_nops(int s) {
+  return EPI == EPI_GLU ? ((s & 1) ? 27 : 24) : 2 * wsp_half<ACT>() + 5;
+}
+constexpr int wsp_lo(int i, int n) { return (i * n + 31) / 32; }   // first op of gap i
+}  // namespace
+
+template <int EPI, int ACT, int DIAG = 0>
+__global__ __launch_bounds__(256, 1) void gemm_wsp_kernel(const bf16* __restrict__ A, int lda,
+                                                          const bf16* __restrict__ W, int ldw, int M, int N,
+                                                          EpiArgs ep) {
+  // A ring + the block's 256 bias values (the re-seed reads them straight into the accumulators)
+  __shared__ __attribute__((aligned(16))) char smem[WST_NSLOT * WST_SLOT + 1024];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int fr = lane & 15, g = lane >> 4;
+
+  const int nbn = N >> 8, nbm = (M + WST_MT - 1) / WST_MT;
+  const int xcd = blockIdx.x & 7, j = blockIdx.x >> 3, per = gridDim.x >> 3;
+  const int cpx = per / nbn;
+  if (cpx == 0 || j >= cpx * nbn) return;
+  const int ct = j % nbn, sub = j / nbn;
+  const int xr0 = (int)((long long)xcd * nbm / 8), xr1 = (int)((long long)(xcd + 1) * nbm / 8);
+  const int r0 = xr0 + (int)((long long)sub * (xr1 - xr0) / cpx);
+  const int r1 = xr0 + (int)((long long)(sub + 1) * (xr1 - xr0) / cpx);
+  if (r0 >= r1) return;
+
+  // ---- A stream: buffer LDS-DMA, descriptor = the 64-row tile (rows past M read as 0, so the
+  // pieces issued past the block's end need no clamp), lane offset (row, swizzled 16-B chunk)
+  unsigned voffA[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = (2 * wv + i) * 8 + (lane >> 3);
+    voffA[i] = (unsigned)(row * lda + ((lane & 7) ^ ((row >> 1) & 7)) * 8) * 2;
+  }
+  // descriptor of row tile rt (built once per tile, not per piece: the SALU work would sit in the
+  // MFMA gaps).  readfirstlane: min/max of uniform ints select v_med3 (VALU only), and a VGPR
+  // descriptor would wrap every buffer op in a waterfall loop
+  auto tile_rsrc = [&](int rt) {
+    const int rows = __builtin_amdgcn_readfirstlane(max(0, min(WST_MT, M - rt * WST_MT)));
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(A + (size_t)rt * WST_MT * lda), (short)0, rows * lda * 2,
+                                             0x00020000);
+  };
+  auto issue_piece = [&](__amdgpu_buffer_rsrc_t rs, auto Ic, auto KSc, auto SLc) {
+    constexpr int i = decltype(Ic)::value, ks = decltype(KSc)::value, slot = decltype(SLc)::value;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(
+        rs, (__attribute__((address_space(3))) void*)(smem + slot * WST_SLOT + (2 * wv + i) * 1024), 16, voffA[i],
+        ks * WST_KS * 2, 0, 0);   // K slice in soffset: the immediate offset would move the LDS side too
+  };
+  {
+    const __amdgpu_buffer_rsrc_t d0 = tile_rsrc(r0), d1 = tile_rsrc(r0 + 1);
+    sfor<0, WST_DEPTH>([&](auto Pc) {
+      constexpr int P = decltype(Pc)::value;
+      issue_piece(P < WST_NK ? d0 : d1, std::integral_constant<int, 0>{}, std::integral_constant<int, P % WST_NK>{}, Pc);
+      issue_piece(P < WST_NK ? d0 : d1, std::integral_constant<int, 1>{}, std::integral_constant<int, P % WST_NK>{}, Pc);
+    });
+  }
+
+  const int col0 = ct * 256 + wv * 64;
+  bf16x8 wf[4][16];
+#pragma unroll
+  for (int nb = 0; nb < 4; ++nb) {
+    const bf16* wp = W + (size_t)(col0 + 16 * nb + fr) * ldw + 8 * g;
+#pragma unroll
+    for (int kk = 0; kk < 16; ++kk) wf[nb][kk] = *reinterpret_cast<const bf16x8*>(wp + 32 * kk);
+  }
+  if (tid < 64)
+    reinterpret_cast<f32x4*>(smem + WST_NSLOT * WST_SLOT)[tid] =
+        ep.bias ? *reinterpret_cast<const f32x4*>(ep.bias + ct * 256 + 4 * tid) : (f32x4){0.f, 0.f, 0.f, 0.f};
+  // output of the wave's two 32-column spans: wave-uniform base + row stride, lane offset
+  // (row fr, 8 columns after the permlane swap)
+  bf16* obase[2];
+  int old[2];
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    if constexpr (EPI == EPI_QKV) {
+      const int d = ep.d, n = col0 + 32 * p;
+      if (n < d) {
+        obase[p] = reinterpret_cast<bf16*>(ep.out) + n;
+        old[p] = d;
+      } else {
+        const int c2 = n - d, which = c2 >= d ? 1 : 0, cc = c2 - which * d;
+        obase[p] = reinterpret_cast<bf16*>(ep.out2) + (size_t)ep.row_off * 2 * d + (cc >> 6) * 128 + which * 64 + (cc & 63);
+        old[p] = 2 * d;
+      }
+    } else if constexpr (EPI == EPI_GLU) {
+      obase[p] = reinterpret_cast<bf16*>(ep.out) + (size_t)ep.row_off * ep.ldo + col0 / 2;
+      old[p] = ep.ldo;
+    } else {
+      obase[p] = reinterpret_cast<bf16*>(ep.out) + (size_t)ep.row_off * ep.ldo + col0 + 32 * p;
+      old[p] = ep.ldo;
+    }
+  }
+  const int lcol = 16 * (g & 1) + 8 * (g >> 1);
+  unsigned voffS[2];
+#pragma unroll
+  for (int p = 0; p < 2; ++p) voffS[p] = (unsigned)(fr * old[p] + lcol) * 2;
+
+  const unsigned lds_base = (unsigned)(size_t)(__attribute__((address_space(3))) char*)smem;
+  const int key = (fr >> 1) & 7;
+  // read bases [slot half][kh]; the slot's offset inside its half and the m-block go in the immediate
+  unsigned rdb[2][2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    rdb[h][0] = lds_base + h * 8 * WST_SLOT + (unsigned)(fr * 128 + ((g ^ key) << 4));
+    rdb[h][1] = lds_base + h * 8 * WST_SLOT + (unsigned)(fr * 128 + (((4 + g) ^ key) << 4));
+  }
+
+  // lane's bias f32x4 of n-block nb at bias_lds + 64 nb
+  const unsigned bias_lds = lds_base + WST_NSLOT * WST_SLOT + (unsigned)(wv * 64 + 4 * g) * 4;
+  f32x4 acc[2][4][4];
+  bf16x8 afr[2][4][2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+      for (int kh = 0; kh < 2; ++kh) afr[u][mb][kh] = (bf16x8){};
+  float et[4];
+  unsigned epk[4];
+#pragma unroll
+  for (int nb = 0; nb < 4; ++nb)
+#pragma unroll
+    for (int mb = 0; mb < 4; ++mb) acc[1][nb][mb] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    et[i] = 0.f;
+    epk[i] = 0u;
+  }
+
+  // Epilogue micro-op O of group S on accumulator buffer a (rows of tile rtp; rows >= lim are not
+  // stored: they fall outside the store descriptor's range, so no branch splits the MFMA stream).
+  // Every result is pinned where it is produced (empty asm volatile): without that, LLVM sinks the
+  // pure arithmetic next to its use and the gaps run dry.
+  auto pin = [](auto& v) { asm volatile("" : "+v"(v)); };
+  // RESEED = false (the final drain): no re-seed reads -- an async ds_read into an accumulator that
+  // is dead afterwards would land in whatever hipcc reuses that register for
+  // store descriptors of tile rtp's rows below lim (one per 32-column span, built once per tile)
+  struct StoreD { __amdgpu_buffer_rsrc_t d[2]; };
+  auto store_rsrc = [&](int rtp, int lim) {
+    StoreD sd;
+    const int rows = __builtin_amdgcn_readfirstlane(max(0, min(WST_MT, lim - rtp * WST_MT)));
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+      sd.d[p] = __builtin_amdgcn_make_buffer_rsrc((void*)(obase[p] + (size_t)rtp * WST_MT * old[p]), (short)0,
+                                                  rows * old[p] * 2, 0x00020000);
+    return sd;
+  };
+  auto epi_op = [&](auto Sc, auto Oc, f32x4(&a)[4][4], const StoreD& sd, auto RSc) {
+    constexpr int S = decltype(Sc)::value, O = decltype(Oc)::value;
+    constexpr bool RESEED = decltype(RSc)::value;
+    constexpr float NL2E = -1.4426950408889634f;
+    auto store = [&](int p, int jj) {
+      if constexpr (DIAG != 5)
+        __builtin_amdgcn_raw_buffer_store_b128((u32x4){epk[0], epk[1], epk[2], epk[3]}, sd.d[p],
+                                               voffS[p] + (unsigned)(16 * jj * old[p] * 2), 0, 0);
+    };
+    // q = 0: pk0 <-> pk2, q = 1: pk1 <-> pk3 (in place); after both, lane g holds 8 contiguous
+    // columns {pk0, pk1, pk2, pk3} (gemm_bf16_epi.h store_pair16)
+    auto swap = [&](int q) {
+      const auto r = __builtin_amdgcn_permlane16_swap(epk[q], epk[q + 2], false, false);
+      epk[q] = r[0];
+      epk[q + 2] = r[1];
+      pin(epk[q]);
+      pin(epk[q + 2]);
+    };
+    // re-seed with the bias: one ds_read_b128 into the accumulator (waited by the step's
+    // closing lgkmcnt(0); the first MFMA on it is a tile later)
+    auto seed = [&](auto NBc, int jj) {
+      constexpr int nb = decltype(NBc)::value;
+      if constexpr (RESEED) lds_read_into<nb * 64>(a[nb][jj], bias_lds);
+    };
+    // sigmoid-style chain on 4 values: t = x * -log2e; t = 2^t; t += 1; t = 1 / t; t = y * t
+    auto chain = [&](int o, auto xf, auto yf) {
+      const int i = o & 3;
+      if (o < 4) et[i] = xf(i) * NL2E;
+      else if (o < 8) et[i] = __builtin_amdgcn_exp2f(et[i]);
+      else if (o < 12) et[i] = et[i] + 1.f;
+      else if (o < 16) et[i] = __builtin_amdgcn_rcpf(et[i]);
+      else et[i] = yf(i) * et[i];
+      pin(et[i]);
+    };
+    if constexpr (EPI == EPI_GLU) {
+      constexpr int jj = S >> 1, h = S & 1;
+      constexpr int nseed = h ? 25 : 22;
+      auto gate = [&](int i) -> float { return a[2 * h + 1][jj][i]; };
+      auto lin = [&](int i) -> float { return a[2 * h][jj][i]; };
+      if constexpr (O >= nseed) {
+        seed(std::integral_constant<int, 2 * h + (O - nseed)>{}, jj);
+      } else if constexpr (DIAG == 3) {
+      } else if constexpr (O < 20) {
+        chain(O, gate, lin);
+      } else if constexpr (O < 22) {
+        epk[2 * h + O - 20] = pack_bf16x2(et[2 * (O - 20)], et[2 * (O - 20) + 1]);
+        pin(epk[2 * h + O - 20]);
+      } else if constexpr (O < 24) {
+        swap(O - 22);
+      } else {   // O == 24
+        store(0, jj);
+      }
+    } else {
+      constexpr int p = S >> 2, jj = S & 3;
+      constexpr int H = wsp_half<ACT>();
+      if constexpr (O >= 2 * H + 3) {
+        seed(std::integral_constant<int, 2 * p + (O - 2 * H - 3)>{}, jj);
+      } else if constexpr (DIAG == 3) {
+      } else if constexpr (O < 2 * H) {
+        constexpr int q = O / H, o = O % H;
+        auto val = [&](int i) -> float { return a[2 * p + q][jj][i]; };
+        if constexpr (o < H - 2) {
+          if constexpr (ACT == ACT_SILU) {
+            chain(o, val, val);
+          } else {
+            et[o] = fmaxf(val(o), 0.f);
+            pin(et[o]);
+          }
+        } else {
+          constexpr int k = o - (H - 2);   // pack k of this half: values 2k, 2k+1
+          if constexpr (ACT == ACT_NONE) epk[2 * q + k] = pack_bf16x2(val(2 * k), val(2 * k + 1));
+          else epk[2 * q + k] = pack_bf16x2(et[2 * k], et[2 * k + 1]);
+          pin(epk[2 * q + k]);
+        }
+      } else if constexpr (O < 2 * H + 2) {
+        swap(O - 2 * H);
+      } else {   // O == 2H + 2
+        store(p, jj);
+      }
+    }
+  };
+
+  // one 64-row tile into acc[BUF]; the gaps drain acc[1 - BUF] (tile rtp, stores below row lim)
+  auto tile = [&](auto BUFc, int rt, int rtp, int lim) {
+    constexpr int BUF = decltype(BUFc)::value;
+    const __amdgpu_buffer_rsrc_t dA1 = tile_rsrc(rt + 1), dA2 = tile_rsrc(rt + 2);
+    const StoreD sd = store_rsrc(rtp, lim);
+    sfor<0, WST_NK>([&](auto KSc) {
+      constexpr int KS = decltype(KSc)::value;
+      constexpr int slot_n = (8 * BUF + KS + 1) % WST_NSLOT;          // next step's slot (read)
+      constexpr int slot_d = (8 * BUF + KS + WST_DEPTH) % WST_NSLOT;  // step y + 15's slot (DMA)
+      constexpr int n_ops = wsp_nops<EPI, ACT>(KS);
+      // step y+1 landed (2 pieces per step, issued unconditionally -- past the block's end they
+      // land in dead slots -- so exactly 28 loads are younger-or-equal here) and, after the
+      // barrier, every wave's pieces of it; every wave is also past its reads of slot y-1, which
+      // the DMA below refills
+      WST_VMCNT(26);
+      asm volatile("s_barrier" ::: "memory");
+      bf16x8(&cur)[4][2] = afr[KS & 1];
+      bf16x8(&nxt)[4][2] = afr[(KS + 1) & 1];
+      sfor<0, 32>([&](auto Ic) {
+        constexpr int i = decltype(Ic)::value;
+        constexpr int kh = i >> 4, nb = (i >> 2) & 3, mb = i & 3;
+        if constexpr (DIAG != 1) mfma_wa(acc[BUF][nb][mb], wf[nb][2 * KS + kh], cur[mb][kh]);
+        if constexpr (i < 16 && (i & 1) == 0) {
+          constexpr int rmb = (i >> 1) & 3, rkh = i >> 3;
+          lds_read_into<(slot_n & 7) * WST_SLOT + rmb * 2048>(nxt[rmb][rkh], rdb[slot_n >> 3][rkh]);
+        }
+        if constexpr (i == 6 || i == 22)
+          issue_piece(KS == 0 ? dA1 : dA2, std::integral_constant<int, i == 22 ? 1 : 0>{},
+                      std::integral_constant<int, (KS + WST_DEPTH) % WST_NK>{},
+                      std::integral_constant<int, slot_d>{});
+        sfor<wsp_lo(i, n_ops), wsp_lo(i + 1, n_ops)>([&](auto Oc) { epi_op(KSc, Oc, acc[1 - BUF], sd, std::true_type{}); });
+        __builtin_amdgcn_sched_barrier(0);
+      });
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    });
+  };
+  auto drain = [&](f32x4(&a)[4][4], int rt) {
+    const StoreD sd = store_rsrc(rt, M);
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");   // last MFMA writes -> VALU reads
+    sfor<0, 8>([&](auto Sc) {
+      constexpr int S = decltype(Sc)::value;
+      sfor<0, wsp_nops<EPI, ACT>(S)>([&](auto Oc) { epi_op(Sc, Oc, a, sd, std::false_type{}); });
+    });
+  };
+
+  // prologue: weights in AGPRs (s_nop: AGPR writes -> MFMA reads), step 0 landed, its fragments read
+  asm volatile("s_nop 7" ::: "memory");
+  WST_VMCNT(28);
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // + the bias in LDS
+#pragma unroll
+  for (int nb = 0; nb < 4; ++nb)
+#pragma unroll
+    for (int mb = 0; mb < 4; ++mb) {
+      acc[0][nb][mb] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      lds_read_into<0>(acc[0][nb][mb], bias_lds + nb * 64);
+    }
+  sfor<0, 8>([&](auto Rc) {
+    constexpr int r = decltype(Rc)::value;
+    lds_read_into<(r & 3) * 2048>(afr[0][r & 3][r >> 2], rdb[0][r >> 2]);
+  });
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+
+  // tiles in pairs (acc[0], acc[1]); an odd count runs one dummy tile past the block's range whose
+  // results are never stored (lim = 0 in the drain), which keeps one straight loop body
+  const int npair = (r1 - r0 + 1) >> 1;
+  for (int it = 0; it < npair; ++it) {
+    const int rt = r0 + 2 * it;
+    // the first tile's gaps drain a fake previous tile: rows of a REAL tile (never negative, so the
+    // store descriptors' row bases stay inside the output) with lim = 0, i.e. zero-record stores
+    tile(std::integral_constant<int, 0>{}, rt, it > 0 ? rt - 1 : rt, it > 0 ? M : 0);
+    tile(std::integral_constant<int, 1>{}, rt + 1, rt, M);
+  }
+  if (((r1 - r0) & 1) == 0) drain(acc[1], r1 - 1);
+  // the pieces issued past the end land (and the drain's seed reads return) before the
+  // workgroup's LDS is released
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+}
+
 static int wst_enabled() {
   static int v = -1;
-  if (v < 0) { const char* e = getenv("CFM_GEMM_WST"); v = e ? atoi(e) : 0; }
+  if (v < 0) { const char* e = getenv("CFM_GEMM_WST"); v = e ? atoi(e) : 2; }
   return v;
 }
 
@@ -204,18 +552,25 @@ static int launch_wst(const bf16* A, int lda, const bf16* W, int ldw, int M, int
   }
   static int diag = -1;
   if (diag < 0) { const char* e = getenv("CFM_GEMM_DIAG"); diag = e ? atoi(e) : 0; }
+  if (wst_enabled() == 2) {
+    // 32-bit buffer-store offsets: every output row offset must stay below 2^31 bytes
+    const size_t ld = EPI == EPI_QKV ? 2 * (size_t)ep.d : (size_t)ep.ldo;
+    if ((size_t)M * ld * 2 >= (1ull << 31)) return -1;
+    if (diag == 1)
+      hipLaunchKernelGGL((gemm_wsp_kernel<EPI, ACT, 1>), dim3(n_cu), dim3(256), 0, st, A, lda, W, ldw, M, N, ep);
+    else if (diag == 3)
+      hipLaunchKernelGGL((gemm_wsp_kernel<EPI, ACT, 3>), dim3(n_cu), dim3(256), 0, st, A, lda, W, ldw, M, N, ep);
+    else if (diag == 5)
+      hipLaunchKernelGGL((gemm_wsp_kernel<EPI, ACT, 5>), dim3(n_cu), dim3(256), 0, st, A, lda, W, ldw, M, N, ep);
+    else
+      hipLaunchKernelGGL((gemm_wsp_kernel<EPI, ACT, 0>), dim3(n_cu), dim3(256), 0, st, A, lda, W, ldw, M, N, ep);
+    CFM_CHECK_LAUNCH();
+    return 0;
+  }
   if (diag == 1)
     hipLaunchKernelGGL((gemm_wst_kernel<EPI, ACT, 1>), dim3(n_cu), dim3(256), 0, st, A, lda, W, ldw, M, N, ep);
   else if (diag == 3)
     hipLaunchKernelGGL((gemm_wst_kernel<EPI, ACT, 3>), dim3(n_cu), dim3(256), 0, st, A, lda, W, ldw, M, N, ep);
-  else if (diag == 2)
-    hipLaunchKernelGGL((gemm_wst_kernel<EPI, ACT, 2>), dim3(n_cu), dim3(256), 0, st, A, lda, W, ldw, M, N, ep);
-  else if (diag == 7)
-    hipLaunchKernelGGL((gemm_wst_kernel<EPI, ACT, 7>), dim3(n_cu), dim3(256), 0, st, A, lda, W, ldw, M, N, ep);
-  else if (diag == 6)
-    hipLaunchKernelGGL((gemm_wst_kernel<EPI, ACT, 6>), dim3(n_cu), dim3(256), 0, st, A, lda, W, ldw, M, N, ep);
-  else if (diag == 4)
-    hipLaunchKernelGGL((gemm_wst_kernel<EPI, ACT, 4>), dim3(n_cu), dim3(256), 0, st, A, lda, W, ldw, M, N, ep);
   else
     hipLaunchKernelGGL((gemm_wst_kernel<EPI, ACT, 0>), dim3(n_cu), dim3(256), 0, st, A, lda, W, ldw, M, N, ep);
   CFM_CHECK_LAUNCH();

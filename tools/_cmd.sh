@@ -1,4 +1,5 @@
 set -e
-for d in 0 1 3 4 6 7; do echo "== wst diag $d"; CFM_GEMM_DIAG=$d timeout -k 10 120 python3 tools/gemm_bench.py --iters 20 --only ffn_w1 2>&1 | grep -v amdgpu; done
-echo "== 256 kernel"; CFM_GEMM_WST=0 timeout -k 10 120 python3 tools/gemm_bench.py --iters 20 2>&1 | grep -v amdgpu
-echo "== wst"; timeout -k 10 120 python3 tools/gemm_bench.py --iters 20 2>&1 | grep -v amdgpu
+timeout -k 10 600 python3 -u -m pytest tests/ -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 || { tail -30 gpurun_out/gpu_tests.log; exit 1; }
+tail -2 gpurun_out/gpu_tests.log
+timeout -k 10 300 python3 bench.py > gpurun_out/bench.log 2>&1 || { tail -20 gpurun_out/bench.log; exit 1; }
+tail -1 gpurun_out/bench.log
