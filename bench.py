@@ -186,8 +186,8 @@ def main():
         alg_bytes = 2.0 * (2 * rows * d_ + 2 * ff_ * d_) + 4 * (ff_ + d_)
     else:
         roof_cls = "ffn_w1_gemm"
-        roof_name = ("ffn_w1_gemm (gemm_kernel<bf16,EPI_STORE,SiLU>)" if args.dtype == "bf16"
-                     else "ffn_w1_gemm (gemm_kernel<float,EPI_STORE,SiLU>)")
+        roof_name = ("ffn_w1_gemm (gemm_wsp_kernel<EPI_STORE,SiLU>: K=512 weight-stationary bf16 MFMA)"
+                     if args.dtype == "bf16" else "ffn_w1_gemm (gemm_kernel<float,EPI_STORE,SiLU>)")
         fl_launch = 2.0 * rows * ff_ * d_
         # compulsory bytes of one w_1 launch: A [rows, d] + out [rows, ff] bf16 + W [ff, d] bf16 + bias
         alg_bytes = 2.0 * (rows * d_ + rows * ff_ + ff_ * d_) + 4 * ff_
@@ -332,7 +332,7 @@ def bench_single(args):
     peak = PEAK_TFLOPS[args.dtype]
     if roof_cls == "ffn_w1_gemm":
         fl_launch = 2.0 * rows * ff_ * d_
-        kname = "ffn_w1_gemm (gemm_bf16_256_kernel<STORE,SiLU>)"
+        kname = "ffn_w1_gemm (gemm_wsp_kernel<EPI_STORE,SiLU>: K=512 weight-stationary bf16 MFMA)"
     else:
         fl_launch = attn_fl
         kname = "chunk_attention (chunk_attention_kernel<bf16>, full-attention descriptors)"
