@@ -99,6 +99,23 @@ CFM_DEV float group16_sum(float v) {
   return v;
 }
 
+// wave-wide sum with no LDS round trip: DPP quad / half-row / row mirrors leave every lane of a
+// 16-lane row with the row total, row_bcast:15 / row_bcast:31 fold the rows into lane 63, and a
+// readlane returns that one value to every lane (bit-identical, wave-uniform)
+template <int CTRL, int ROWS = 0xF>
+CFM_DEV float dpp_f32(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, ROWS, 0xF, false));
+}
+CFM_DEV float wave_sum_dpp(float v) {
+  v += dpp_f32<0xB1>(v);          // quad_perm [1,0,3,2]
+  v += dpp_f32<0x4E>(v);          // quad_perm [2,3,0,1]
+  v += dpp_f32<0x141>(v);         // row_half_mirror
+  v += dpp_f32<0x140>(v);         // row_mirror
+  v += dpp_f32<0x142, 0xA>(v);    // row_bcast:15 into rows 1, 3
+  v += dpp_f32<0x143, 0xC>(v);    // row_bcast:31 into rows 2, 3
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 63));
+}
+
 CFM_DEV float silu_f(float x) { return x / (1.0f + __expf(-x)); }
 CFM_DEV float sigmoid_f(float x) { return 1.0f / (1.0f + __expf(-x)); }
 

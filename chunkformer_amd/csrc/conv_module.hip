@@ -12,6 +12,7 @@
 // One wave per output row, lane l owns channels [l*VPL, l*VPL+VPL); the LN
 // statistics are wave reductions.  Depthwise weights are stored tap-major
 // [15][d] so every tap is one coalesced vector load.
+#include <cstdlib>
 #include <type_traits>
 #include "cfm_common.h"
 #include "cfm_kernels.h"
@@ -170,11 +171,149 @@ __global__ __launch_bounds__(512) void conv_dw_ln_silu_lds_kernel(const bf16* __
   }
 }
 
+// bf16, VPL even (d = 128 / 256 / 512): the k = 15 depthwise conv as bf16 dot products over TAP
+// PAIRS -- v_dot2_f32_bf16 adds x[j] w[t] + x[j+1] w[t+1] to an f32 accumulator in one
+// instruction (bf16 taps: what conv1d runs on under the reference's bf16 autocast), instead of
+// one bf16 -> f32 conversion plus one FMA per tap.  Lane l owns channels [VPL l, VPL l + VPL);
+// a wave owns 8 output rows i0 + r.  The row pair (i0 + j, i0 + j + 1) is packed once per
+// channel pair (v_perm_b32) and feeds every output r whose tap t = j - r is even; tap 14 pairs
+// with w[15] = 0 on the window's extra zero row.  LayerNorm statistics by DPP / permlane
+// reductions (no LDS round trips), SiLU as v_exp + v_rcp.
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+CFM_DEV float dot2_bf16(unsigned a, unsigned b, float c) {
+  return __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, a), __builtin_bit_cast(bf16x2_t, b), c, false);
+}
+CFM_DEV unsigned pk_bf16(float lo, float hi) {
+  return __builtin_bit_cast(unsigned, (bf16x2_t){(__bf16)lo, (__bf16)hi});
+}
+template <int VPL>
+__global__ __launch_bounds__(512) void conv_dw_ln_silu_dot2_kernel(const bf16* __restrict__ glu,
+                                                                   const int32_t* __restrict__ desc,
+                                                                   const float* __restrict__ wdw,
+                                                                   const float* __restrict__ bdw,
+                                                                   const float* __restrict__ lnw,
+                                                                   const float* __restrict__ lnb, float eps,
+                                                                   bf16* __restrict__ out) {
+  constexpr int d = VPL * 64, NW = VPL / 2;   // NW dwords (channel pairs) per lane per row
+  constexpr int MAXJ = 64 + 15;               // window rows + the zero row of the w[15] = 0 tap
+  constexpr int RW = 8;                       // output rows per wave
+  typedef bf16 bvec __attribute__((ext_vector_type(VPL)));
+  __shared__ __attribute__((aligned(16))) bf16 win[MAXJ * d];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int32_t* D = desc + (size_t)blockIdx.x * CD_INTS;
+  const int out_row0 = D[CD_OUT_ROW0], nout = D[CD_NOUT], src0 = D[CD_SRC_ROW0];
+  const int nj = nout + 14;
+  const int jlo = max(D[CD_J_LO], 0), jhi = min(D[CD_J_HI], nj);
+  constexpr int V8 = d / 8;   // 16-B vectors per row
+  for (int idx = tid; idx < MAXJ * V8; idx += 512) {
+    const int j = idx / V8, v = idx % V8;
+    u32x4 val = (u32x4){0u, 0u, 0u, 0u};
+    if (j >= jlo && j < jhi) val = *reinterpret_cast<const u32x4*>(glu + (size_t)(src0 + j) * d + v * 8);
+    *reinterpret_cast<u32x4*>(win + j * d + v * 8) = val;
+  }
+  __syncthreads();
+  const int i0 = w * RW;
+  if (i0 >= nout) return;
+  const int c0 = lane * VPL;
+  // tap-pair weights: wp[p][e] = (w[2p][c0 + e], w[2p + 1][c0 + e]) as bf16x2, w[15] = 0
+  unsigned wp[8][VPL];
+#pragma unroll
+  for (int p = 0; p < 8; ++p) {
+    float lo[VPL], hi[VPL];
+    VecIO<float, VPL>::load(wdw + (2 * p) * d + c0, lo);
+    if (p < 7) {
+      VecIO<float, VPL>::load(wdw + (2 * p + 1) * d + c0, hi);
+    } else {
+#pragma unroll
+      for (int e = 0; e < VPL; ++e) hi[e] = 0.f;
+    }
+#pragma unroll
+    for (int e = 0; e < VPL; ++e) wp[p][e] = pk_bf16(lo[e], hi[e]);
+  }
+  float acc[RW][VPL];
+#pragma unroll
+  for (int e = 0; e < VPL; ++e) {
+    const float bv = bdw[c0 + e];
+#pragma unroll
+    for (int r = 0; r < RW; ++r) acc[r][e] = bv;
+  }
+  auto ld = [&](unsigned (&x)[NW], int row) {
+    const unsigned* p = reinterpret_cast<const unsigned*>(win + row * d + c0);
+    if constexpr (NW == 4) {
+      const u32x4 t = *reinterpret_cast<const u32x4*>(p);
+      x[0] = t[0]; x[1] = t[1]; x[2] = t[2]; x[3] = t[3];
+    } else if constexpr (NW == 2) {
+      typedef unsigned u32x2_ __attribute__((ext_vector_type(2)));
+      const u32x2_ t = *reinterpret_cast<const u32x2_*>(p);
+      x[0] = t[0]; x[1] = t[1];
+    } else {
+      x[0] = p[0];
+    }
+  };
+  unsigned ra[NW], rb[NW];
+  ld(ra, i0);
+#pragma unroll
+  for (int j = 0; j < RW + 14; ++j) {
+    ld(rb, i0 + j + 1);
+    unsigned pk[VPL];   // channel e: (row i0 + j, row i0 + j + 1)
+#pragma unroll
+    for (int k = 0; k < NW; ++k) {
+      pk[2 * k] = __builtin_amdgcn_perm(rb[k], ra[k], 0x05040100u);
+      pk[2 * k + 1] = __builtin_amdgcn_perm(rb[k], ra[k], 0x07060302u);
+    }
+#pragma unroll
+    for (int r = 0; r < RW; ++r) {
+      const int t = j - r;
+      if (t >= 0 && t <= 14 && (t & 1) == 0) {
+#pragma unroll
+        for (int e = 0; e < VPL; ++e) acc[r][e] = dot2_bf16(pk[e], wp[t >> 1][e], acc[r][e]);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < NW; ++k) ra[k] = rb[k];
+  }
+  float lw[VPL], lb[VPL];
+#pragma unroll
+  for (int e = 0; e < VPL; ++e) {
+    lw[e] = lnw[c0 + e];
+    lb[e] = lnb[c0 + e];
+  }
+#pragma unroll
+  for (int r = 0; r < RW; ++r) {
+    if (i0 + r >= nout) break;
+    float sum = 0.f;
+#pragma unroll
+    for (int e = 0; e < VPL; ++e) sum += acc[r][e];
+    const float mean = wave_sum_dpp(sum) / d;
+    float q = 0.f;
+#pragma unroll
+    for (int e = 0; e < VPL; ++e) { const float t = acc[r][e] - mean; q += t * t; }
+    const float rstd = rsqrtf(wave_sum_dpp(q) / d + eps);
+    bvec o;
+#pragma unroll
+    for (int e = 0; e < VPL; ++e) {
+      const float y = (acc[r][e] - mean) * rstd * lw[e] + lb[e];
+      o[e] = (bf16)(y * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-1.4426950408889634f * y)));
+    }
+    *reinterpret_cast<bvec*>(out + (size_t)(out_row0 + i0 + r) * d + c0) = o;
+  }
+}
+
 template <typename T>
 int conv_dw_ln_silu(const T* glu, const int32_t* desc, int nblk, int d, const float* wdw_t, const float* bdw,
                     const float* lnw, const float* lnb, float eps, T* out, hipStream_t st) {
   if (nblk <= 0) return 0;
+  static int dot2 = -1;   // CFM_CONV_DOT2=0: the per-tap f32 kernel (A/B)
+  if (dot2 < 0) { const char* e = getenv("CFM_CONV_DOT2"); dot2 = e ? atoi(e) : 1; }
   if constexpr (std::is_same<T, bf16>::value) {
+    if (dot2) {
+      if (d == 128) hipLaunchKernelGGL((conv_dw_ln_silu_dot2_kernel<2>), dim3(nblk), dim3(512), 0, st, glu, desc, wdw_t, bdw, lnw, lnb, eps, out);
+      else if (d == 256) hipLaunchKernelGGL((conv_dw_ln_silu_dot2_kernel<4>), dim3(nblk), dim3(512), 0, st, glu, desc, wdw_t, bdw, lnw, lnb, eps, out);
+      else if (d == 512) hipLaunchKernelGGL((conv_dw_ln_silu_dot2_kernel<8>), dim3(nblk), dim3(512), 0, st, glu, desc, wdw_t, bdw, lnw, lnb, eps, out);
+      else return (int)hipErrorInvalidValue;
+      CFM_CHECK_LAUNCH();
+      return 0;
+    }
     if (d == 128) hipLaunchKernelGGL((conv_dw_ln_silu_lds_kernel<2>), dim3(nblk), dim3(512), 0, st, glu, desc, wdw_t, bdw, lnw, lnb, eps, out);
     else if (d == 256) hipLaunchKernelGGL((conv_dw_ln_silu_lds_kernel<4>), dim3(nblk), dim3(512), 0, st, glu, desc, wdw_t, bdw, lnw, lnb, eps, out);
     else if (d == 512) hipLaunchKernelGGL((conv_dw_ln_silu_lds_kernel<8>), dim3(nblk), dim3(512), 0, st, glu, desc, wdw_t, bdw, lnw, lnb, eps, out);

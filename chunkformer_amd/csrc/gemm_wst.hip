@@ -291,7 +291,7 @@ __global__ __launch_bounds__(256, 1) void gemm_wsp_kernel(const bf16* __restrict
         store(0, jj);
       }
     } else {
-      constexpr int p = S >> 2, jj = S & 3;
+      constexpr int p = S & 1, jj = S >> 1;   // the two 64-B halves of a 128-B row piece in consecutive steps
       constexpr int H = wsp_half<ACT>();
       if constexpr (O >= 2 * H + 3) {
         seed(std::integral_constant<int, 2 * p + (O - 2 * H - 3)>{}, jj);

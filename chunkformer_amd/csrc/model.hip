@@ -165,7 +165,8 @@ struct ModelT : public cfm_model {
     const int W = h[PH_W];
     const int T1 = (W - 3) / 2 + 1, T2 = (T1 - 3) / 2 + 1;
     const size_t per = (size_t)T2 * 19 * cfg.d_model * sizeof(T);
-    const size_t cap = (size_t)768 << 20;   // 768 MiB per intermediate buffer
+    static size_t cap = 0;   // 768 MiB per intermediate buffer (CFM_FE_CAP_MB: experiments)
+    if (!cap) { const char* e = getenv("CFM_FE_CAP_MB"); cap = (size_t)(e ? atoi(e) : 768) << 20; }
     int g = (int)std::max<size_t>(1, cap / per);
     return std::min(g, h[PH_NWIN]);
   }

@@ -16,14 +16,14 @@ CFM_DEV void ln_row(float (&v)[VPL], int d, const float* w, const float* b, floa
   float s = 0.f;
 #pragma unroll
   for (int e = 0; e < VPL; ++e) s += v[e];
-  const float mean = wave_sum(s) / d;
+  const float mean = wave_sum_dpp(s) / d;
   float q = 0.f;
 #pragma unroll
   for (int e = 0; e < VPL; ++e) {
     const float t = v[e] - mean;
     q += t * t;
   }
-  const float rstd = rsqrtf(wave_sum(q) / d + eps);
+  const float rstd = rsqrtf(wave_sum_dpp(q) / d + eps);
 #pragma unroll
   for (int e = 0; e < VPL; ++e) {
     const int c = lane * VPL + e;

@@ -24,7 +24,7 @@ CLASSES = [
     ("fe_conv0_dw_mfma_kernel", "frontend_conv0_dw"),
     ("fe_dw2_kernel", "frontend_dw2"),
     ("chunk_attention_ring_kernel", "chunk_attention"),
-    ("conv_dw_ln_silu_kernel", "conv_dw_ln_silu"),
+    ("conv_dw_ln_silu", "conv_dw_ln_silu"),
     ("ln_kernel", "layernorm"),
     ("ln2_kernel", "layernorm2"),
     ("ffn_fused_kernel", "ffn_fused"),
