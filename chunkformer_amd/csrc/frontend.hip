@@ -227,9 +227,12 @@ __global__ __launch_bounds__(256, 3) void fe_conv0_dw_mfma_kernel(const float* _
 }
 
 // dw2: [win][T2][19][d] -> [win][T3][9][d], depthwise 3x3 stride 2 + bias (no activation), taps
-// tap-major w[9][d].  One thread per (window, f3, 8 channels) walks down the window's rows:
-// input row 2*t3+2 is kept in registers for the next output row, so every input byte is
-// read from HBM once (16-B loads, 64 lanes = one 1-KB channel row).
+// tap-major w[9][d].  One thread per (window, f3, 8 channels, row segment) walks down its
+// FE_DW2_SEG-th of the window's output rows: input row 2*t3+2 is kept in registers for the next
+// output row, so every input byte is read from HBM once, plus one shared row per segment start
+// (16-B loads, 64 lanes = one 1-KB channel row).  The segments multiply the waves in flight
+// (one walk per thread is latency-bound at ~11 waves per CU).
+constexpr int FE_DW2_SEG = 4;
 template <typename T>
 __global__ __launch_bounds__(256) void fe_dw2_kernel(const T* __restrict__ in, int nwin, int T2, int T3, int d,
                                                      const float* __restrict__ w, const float* __restrict__ b,
@@ -238,6 +241,7 @@ __global__ __launch_bounds__(256) void fe_dw2_kernel(const T* __restrict__ in, i
   const size_t idx = (size_t)blockIdx.x * 256 + threadIdx.x;
   const size_t total = (size_t)nwin * FE_F3 * d8;
   if (idx >= total) return;
+  const int t3a = (int)((long long)blockIdx.y * T3 / FE_DW2_SEG), t3b = (int)((long long)(blockIdx.y + 1) * T3 / FE_DW2_SEG);
   const int c = (int)(idx % d8) * 8;
   const size_t r = idx / d8;
   const int f3 = r % FE_F3;
@@ -250,8 +254,8 @@ __global__ __launch_bounds__(256) void fe_dw2_kernel(const T* __restrict__ in, i
   T* ob = out + (wn * T3 * FE_F3 + f3) * d + c;
   float top[3][8];   // input row 2*t3 (carried from the previous output row)
 #pragma unroll
-  for (int v = 0; v < 3; ++v) load8(ib + (size_t)v * d, top[v]);
-  for (int t3 = 0; t3 < T3; ++t3) {
+  for (int v = 0; v < 3; ++v) load8(ib + (size_t)(2 * t3a) * FE_F2 * d + (size_t)v * d, top[v]);
+  for (int t3 = t3a; t3 < t3b; ++t3) {
     float mid[3][8], bot[3][8];
     const T* rb = ib + (size_t)(2 * t3 + 1) * FE_F2 * d;
 #pragma unroll
@@ -305,8 +309,8 @@ int frontend_dw2(const T* in, int nwin, int T2, int d, const float* w, const flo
   if (d % 8) return (int)hipErrorInvalidValue;
   const size_t total = (size_t)nwin * FE_F3 * (d / 8);
   if (total == 0 || T3 <= 0) return 0;
-  hipLaunchKernelGGL((fe_dw2_kernel<T>), dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, in, nwin, T2, T3, d,
-                     w, b, out);
+  hipLaunchKernelGGL((fe_dw2_kernel<T>), dim3((unsigned)((total + 255) / 256), FE_DW2_SEG), dim3(256), 0, st, in, nwin,
+                     T2, T3, d, w, b, out);
   CFM_CHECK_LAUNCH();
   return 0;
 }

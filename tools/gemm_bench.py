@@ -19,6 +19,8 @@ SHAPES = [  # (name, N, K, epi, act)
     ("out/pw2", 512, 512, 0, 0),
     ("pw1_glu", 1024, 512, 4, 0),
     ("fe_pw1", 512, 512, 0, 1),
+    ("ffn_w1_noact", 2048, 512, 0, 0),   # A/B: the FFN w1 shape without / with a cheap activation
+    ("ffn_w1_relu", 2048, 512, 0, 1),
 ]
 
 
