@@ -34,10 +34,17 @@ void gemm_set_variant(int v);
 
 // LayerNorm over d (eps) of f32 rows -> T rows; optional 0/1 row mask on the output.
 // fused residual add of the previous sub-block: x += alpha * ymask[row] * y (y null = none)
+// A LayerNorm that defers (defer = true) leaves x unwritten: the next LayerNorm re-applies that
+// branch as its FIRST term (y, alpha, ymask) and adds its own as the second (y2, alpha2, ymask2),
+// in the same order, so x is bit-identical and one f32 write + read of x is saved per pair.
 template <typename T> struct ResidAdd {
   const T* y = nullptr;
   float alpha = 1.f;
   const uint8_t* ymask = nullptr;
+  const T* y2 = nullptr;
+  float alpha2 = 1.f;
+  const uint8_t* ymask2 = nullptr;
+  bool defer = false;
 };
 template <typename T>
 int layernorm(float* x, const ResidAdd<T>& ra, int M, int d, const float* w, const float* b, float eps, T* out,

@@ -173,7 +173,7 @@ struct ModelT : public cfm_model {
 
   struct WS {
     float* x;
-    T *h, *hid, *q, *kv, *ao, *glu, *cv, *y, *P, *pos, *feA, *feB;
+    T *h, *hid, *q, *kv, *ao, *glu, *cv, *y, *y2, *P, *pos, *feA, *feB;
   };
 
   WS carve(void* base, const int32_t* h, size_t* total) const {
@@ -194,6 +194,7 @@ struct ModelT : public cfm_model {
     w.glu = c.take<T>((size_t)h[PH_GLUROWS] * d);
     w.cv = c.take<T>(rows * d);
     w.y = c.take<T>(rows * d);
+    w.y2 = c.take<T>(rows * d);
     w.P = c.take<T>((size_t)nb * prow_pad * d);
     w.pos = c.take<T>(prow_pad * d);
     w.feA = c.take<T>(G * T2 * 19 * d);
@@ -271,27 +272,37 @@ struct ModelT : public cfm_model {
     // Each residual branch's last GEMM writes y = branch + bias (bf16/T); the residual add
     // x += alpha * y (0.5 for the FFNs, encoder_layer.py:196/246; the conv branch masked by
     // the padded path's row mask) is fused into the LayerNorm that reads x next.
-    auto resid = [&](float alpha, const uint8_t* ym) { ResidAdd<T> r; r.y = w.y; r.alpha = alpha; r.ymask = ym; return r; };
+    // Branch outputs alternate between w.y and w.y2, so the LayerNorms after the macaron FFN and
+    // after the conv module defer their x write (ResidAdd::defer): the next LayerNorm applies both
+    // branches in the same order, x is read and written once per pair (bit-identical x).
+    auto resid = [&](const T* y, float alpha, const uint8_t* ym) {
+      ResidAdd<T> r; r.y = y; r.alpha = alpha; r.ymask = ym; return r;
+    };
+    auto resid2 = [&](const T* y, float alpha, const uint8_t* ym, const T* y2, float alpha2, const uint8_t* ym2) {
+      ResidAdd<T> r = resid(y, alpha, ym); r.y2 = y2; r.alpha2 = alpha2; r.ymask2 = ym2; return r;
+    };
     // y = w2 . SiLU(w1 . h + b1) + b2: one fused kernel (bf16, d = 512) or two GEMMs through w.hid
-    auto ffn = [&](const void* w1, const float* b1, const void* w2, const float* b2, const void* stream_w) -> cfm_status {
+    auto ffn = [&](const void* w1, const float* b1, const void* w2, const float* b2, const void* stream_w,
+                   T* yout) -> cfm_status {
       if constexpr (sizeof(T) == 2) {
         if (use_fused_ffn && stream_w) {
-          PROF(PC_FFNF, ffn_fused((const bf16*)w.h, rows, (const bf16*)stream_w, b1, b2, (bf16*)w.y, d, ff, st));
+          PROF(PC_FFNF, ffn_fused((const bf16*)w.h, rows, (const bf16*)stream_w, b1, b2, (bf16*)yout, d, ff, st));
           return CFM_OK;
         }
       }
       { EpiArgs e; e.bias = b1; e.out = w.hid; e.ldo = ff;
         PROF(PC_FFN1, gemm<T>(EPI_STORE, ACT_SILU, w.h, d, (const T*)w1, d, rows, ff, d, e, st)); }
-      { EpiArgs e; e.bias = b2; e.out = w.y; e.ldo = d;
+      { EpiArgs e; e.bias = b2; e.out = yout; e.ldo = d;
         PROF(PC_FFN2, gemm<T>(EPI_STORE, ACT_NONE, w.hid, ff, (const T*)w2, ff, rows, d, ff, e, st)); }
       return CFM_OK;
     };
     for (int l = 0; l < nl; ++l) {
       const LayerW& Lw = layers[l];
       // macaron FFN (x 0.5)
-      { const cfm_status fs = ffn(Lw.ff1m, Lw.b_ff1m, Lw.ff2m, Lw.b_ff2m, Lw.ffs_m); if (fs != CFM_OK) return fs; }
-      // MHSA
-      PROF(PC_LN, layernorm<T>(w.x, resid(0.5f, nullptr), rows, d, Lw.ln_mha_w, Lw.ln_mha_b, eps, w.h, nullptr, st));
+      { const cfm_status fs = ffn(Lw.ff1m, Lw.b_ff1m, Lw.ff2m, Lw.b_ff2m, Lw.ffs_m, w.y); if (fs != CFM_OK) return fs; }
+      // MHSA (x + 0.5 y_ffm is not stored: the conv LayerNorm re-applies it)
+      { ResidAdd<T> r = resid(w.y, 0.5f, nullptr); r.defer = true;
+        PROF(PC_LN, layernorm<T>(w.x, r, rows, d, Lw.ln_mha_w, Lw.ln_mha_b, eps, w.h, nullptr, st)); }
       if (aci) PROF(PC_CACHE, att_cache_in<T>(aci + (size_t)l * L * 2 * d, L, 2 * d, w.kv, st));
       { EpiArgs e; e.bias = Lw.b_qkv; e.out = w.q; e.out2 = w.kv; e.row_off = kvoff; e.d = d;
         PROF(PC_QKV, gemm<T>(EPI_QKV, ACT_NONE, w.h, d, (const T*)Lw.qkv, d, rows, 3 * d, d, e, st)); }
@@ -311,11 +322,11 @@ struct ModelT : public cfm_model {
         KCHK(r);
         prof_end(PC_ATTN, st, pb_);
       }
-      { EpiArgs e; e.bias = Lw.b_o; e.out = w.y; e.ldo = d;
+      { EpiArgs e; e.bias = Lw.b_o; e.out = w.y2; e.ldo = d;
         PROF(PC_OPROJ, gemm<T>(EPI_STORE, ACT_NONE, w.ao, d, (const T*)Lw.wo, d, rows, d, d, e, st)); }
-      // convolution module
-      PROF(PC_LN, layernorm<T>(w.x, resid(1.f, nullptr), rows, d, Lw.ln_conv_w, Lw.ln_conv_b, eps, w.h,
-                               masked ? nullptr : rmask, st));
+      // convolution module: x += 0.5 y_ffm + y_attn, stored
+      PROF(PC_LN, layernorm<T>(w.x, resid2(w.y, 0.5f, nullptr, w.y2, 1.f, nullptr), rows, d, Lw.ln_conv_w, Lw.ln_conv_b,
+                               eps, w.h, masked ? nullptr : rmask, st));
       if (cci) PROF(PC_CACHE, cnn_cache_in<T>(cci + (size_t)l * d * 7, d, 7, w.glu, st));
       { EpiArgs e; e.bias = Lw.b_pw1; e.out = w.glu; e.ldo = d; e.row_off = gluoff;
         PROF(PC_PW1, gemm<T>(EPI_GLU, ACT_NONE, w.h, d, (const T*)Lw.pw1, d, rows, 2 * d, d, e, st)); }
@@ -323,16 +334,17 @@ struct ModelT : public cfm_model {
       PROF(PC_CONV, conv_dw_ln_silu<T>(w.glu, convd, nconv, d, Lw.dw_t, Lw.b_dw, Lw.cn_w, Lw.cn_b, eps, w.cv, st));
       { EpiArgs e; e.bias = Lw.b_pw2; e.out = w.y; e.ldo = d;
         PROF(PC_PW2, gemm<T>(EPI_STORE, ACT_NONE, w.cv, d, (const T*)Lw.pw2, d, rows, d, d, e, st)); }
-      // FFN (x 0.5)
-      PROF(PC_LN, layernorm<T>(w.x, resid(1.f, rmask), rows, d, Lw.ln_ff_w, Lw.ln_ff_b, eps, w.h, nullptr, st));
-      { const cfm_status fs = ffn(Lw.ff1, Lw.b_ff1, Lw.ff2, Lw.b_ff2, Lw.ffs); if (fs != CFM_OK) return fs; }
-      // norm_final (+ next layer's macaron LN, or after_norm)
+      // FFN (x 0.5); x + y_conv is not stored: norm_final re-applies it
+      { ResidAdd<T> r = resid(w.y, 1.f, rmask); r.defer = true;
+        PROF(PC_LN, layernorm<T>(w.x, r, rows, d, Lw.ln_ff_w, Lw.ln_ff_b, eps, w.h, nullptr, st)); }
+      { const cfm_status fs = ffn(Lw.ff1, Lw.b_ff1, Lw.ff2, Lw.b_ff2, Lw.ffs, w.y2); if (fs != CFM_OK) return fs; }
+      // norm_final over x + y_conv + 0.5 y_ffn (+ next layer's macaron LN, or after_norm)
+      const ResidAdd<T> rf = resid2(w.y, 1.f, rmask, w.y2, 0.5f, nullptr);
       if (l + 1 < nl)
-        PROF(PC_LN, layernorm2<T>(w.x, resid(0.5f, nullptr), rows, d, Lw.ln_fin_w, Lw.ln_fin_b, layers[l + 1].ln_ffm_w,
+        PROF(PC_LN, layernorm2<T>(w.x, rf, rows, d, Lw.ln_fin_w, Lw.ln_fin_b, layers[l + 1].ln_ffm_w,
                                   layers[l + 1].ln_ffm_b, eps, w.h, st));
       else
-        PROF(PC_LN, layernorm2_f32<T>(w.x, resid(0.5f, nullptr), rows, d, Lw.ln_fin_w, Lw.ln_fin_b, fe.an_w, fe.an_b, eps,
-                                      out, st));
+        PROF(PC_LN, layernorm2_f32<T>(w.x, rf, rows, d, Lw.ln_fin_w, Lw.ln_fin_b, fe.an_w, fe.an_b, eps, out, st));
     }
     return CFM_OK;
   }

@@ -82,16 +82,27 @@ CFM_DEV void load_row(const bf16* p, float (&v)[VPL]) {
   }
 }
 
-// x += alpha * ymask[row] * y (the sub-block's residual add, encoder_layer.py:196-246), written back
+// x += alpha * ymask[row] * y (the sub-block's residual add, encoder_layer.py:196-246), then the
+// second branch's term when present; written back unless deferred to the next LayerNorm
 template <typename TY, int VPL>
-CFM_DEV void resid_add(float (&v)[VPL], float* xp, const ResidAdd<TY>& ra, int row, int lane) {
-  if (!ra.y) return;
+CFM_DEV void resid_terms(float (&v)[VPL], const ResidAdd<TY>& ra, int row, int lane) {
   float yv[VPL];
   load_row<VPL>(ra.y + (size_t)row * (VPL * 64) + lane * VPL, yv);
   const float a = ra.alpha * (ra.ymask ? (float)ra.ymask[row] : 1.f);
 #pragma unroll
   for (int e = 0; e < VPL; ++e) v[e] = fmaf(a, yv[e], v[e]);
-  store_row<VPL>(xp, v);
+  if (ra.y2) {
+    load_row<VPL>(ra.y2 + (size_t)row * (VPL * 64) + lane * VPL, yv);
+    const float a2 = ra.alpha2 * (ra.ymask2 ? (float)ra.ymask2[row] : 1.f);
+#pragma unroll
+    for (int e = 0; e < VPL; ++e) v[e] = fmaf(a2, yv[e], v[e]);
+  }
+}
+template <typename TY, int VPL>
+CFM_DEV void resid_add(float (&v)[VPL], float* xp, const ResidAdd<TY>& ra, int row, int lane) {
+  if (!ra.y) return;
+  resid_terms<TY, VPL>(v, ra, row, lane);
+  if (!ra.defer) store_row<VPL>(xp, v);
 }
 
 template <typename T, int VPL>
@@ -126,13 +137,7 @@ __global__ __launch_bounds__(256) void ln2_kernel(float* __restrict__ x, ResidAd
   float v[VPL];
   float* xp = x + (size_t)row * d + lane * VPL;
   load_row<VPL>(xp, v);
-  if (ra.y) {
-    float yv[VPL];
-    load_row<VPL>(ra.y + (size_t)row * d + lane * VPL, yv);
-    const float a = ra.alpha * (ra.ymask ? (float)ra.ymask[row] : 1.f);
-#pragma unroll
-    for (int e = 0; e < VPL; ++e) v[e] = fmaf(a, yv[e], v[e]);
-  }
+  if (ra.y) resid_terms<TY, VPL>(v, ra, row, lane);
   ln_row<VPL>(v, d, w1, b1, eps, lane);
   store_row<VPL>(xp, v);
   if (w2) ln_row<VPL>(v, d, w2, b2, eps, lane);
