@@ -21,8 +21,9 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("CFM_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wno-unused-result"]
 # frontend.hip: ReLU on MFMA outputs as a single v_max_f32 (no IEEE-mode canonicalisation);
-# the front-end never sees NaN inputs it would have to propagate
-FILE_FLAGS = {"frontend.hip": ["-fno-honor-nans", "-mno-amdgpu-ieee"]}
+# the front-end never sees NaN inputs it would have to propagate; no SLP packing of the ReLU.w1
+# FMAs into v_pk_fma_f32 (slower issue beside MFMAs)
+FILE_FLAGS = {"frontend.hip": ["-fno-honor-nans", "-mno-amdgpu-ieee", "-fno-slp-vectorize"]}
 
 
 def _sources():

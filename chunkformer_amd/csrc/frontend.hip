@@ -195,16 +195,21 @@ __global__ __launch_bounds__(256, 3) void fe_conv0_dw_mfma_kernel(const float* _
     for (int s = 0; s < 9; ++s) {
       f32x16 nxt;
       if (s + 1 < 9) nxt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xa[s + 1], wcur, seed, 0, 0, 0);
+#ifndef CFM_FE_PK
+      // one v_max_f32 + one v_fma_f32 per value (IEEE mode off in build.py: no canonicalising
+      // max in front; no SLP packing: a v_pk_fma_f32 beside MFMAs issues slower than two v_fma_f32)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) o[r] = fmaf(fmaxf(acc[r], 0.f), wkc[s], o[r]);
+#else
       const f32x2 w2 = (f32x2){wkc[s], wkc[s]};
 #pragma unroll
       for (int r = 0; r < 16; r += 2) {
-        // one v_max_f32 each: this file is built with IEEE mode off (build.py), so no
-        // canonicalising max is added in front
         const f32x2 a2 = (f32x2){fmaxf(acc[r], 0.f), fmaxf(acc[r + 1], 0.f)};
         const f32x2 o2 = __builtin_elementwise_fma(w2, a2, (f32x2){o[r], o[r + 1]});
         o[r] = o2[0];
         o[r + 1] = o2[1];
       }
+#endif
       asm volatile("" : "+v"(wcur), "+v"(o));
       if (s + 1 < 9) acc = nxt;
     }
