@@ -16,6 +16,7 @@
 // in 64-key tiles with an online softmax; tiles entirely outside [KEY_LO,KEY_HI)
 // are skipped (their probabilities are exactly 0 in the reference).  V^T tiles
 // are staged in LDS (144/272-B pitch: conflict-free 16-row fragment reads).
+#include <cstdlib>
 #include "cfm_common.h"
 #include "cfm_kernels.h"
 
@@ -233,6 +234,7 @@ __global__ __launch_bounds__(512, 1) void chunk_attention_ring_kernel(
     const bf16* __restrict__ Q, const bf16* __restrict__ KV, int kv_rows, const bf16* __restrict__ P, int p_rows,
     const float* __restrict__ pos_u, const float* __restrict__ pos_v, const int32_t* __restrict__ desc, int n_chunks,
     int H, int C, int W, bf16* __restrict__ out, int diag, int nch) {
+  const bool reuse_band = diag != 5;   // diag 5: recompute band subtile 0 of every tile (A/B)
   __shared__ __attribute__((aligned(16))) char smem[RING_LDS];
   char* kr = smem;
   char* pl = smem + KR_BYTES;
@@ -373,6 +375,7 @@ __global__ __launch_bounds__(512, 1) void chunk_attention_ring_kernel(
       const bool need_mask = __builtin_amdgcn_readfirstlane((key_lo != (key_lo & ~15)) || ((key_hi - (key_lo & ~15)) & 63)) != 0;
       const int jb = key_lo & ~15;
       f32x4 S[5][4];
+      f32x4 band_next = (f32x4){0.f, 0.f, 0.f, 0.f};
       float mx = -INFINITY;
 #pragma unroll
       for (int t = 0; t < 5; ++t) {
@@ -400,9 +403,13 @@ __global__ __launch_bounds__(512, 1) void chunk_attention_ring_kernel(
           S[t][st] = a;
         }
         const int kb0 = p_base - i0 - 15 + j0;
+        // band subtile 0 of tile t is subtile 4 of tile t - 1 (P rows kb0 .. kb0 + 15, 64 rows on):
+        // carried in registers (tiles past key_hi are skipped only at the end, so tile t - 1 ran)
+        const bool carry = t > 0 && reuse_band;
         if (diag != 2) {
 #pragma unroll
           for (int pt = 0; pt < 5; ++pt) {
+            if (pt == 0 && carry) continue;
             const char* pb_ = pl + (kb0 + 16 * pt) * 128;
 #pragma unroll
             for (int s = 0; s < 2; ++s) pf[pt][s] = *reinterpret_cast<const bf16x8*>(pb_ + frag_lane[s]);
@@ -414,11 +421,16 @@ __global__ __launch_bounds__(512, 1) void chunk_attention_ring_kernel(
         if (diag != 2) {
 #pragma unroll
           for (int pt = 0; pt < 5; ++pt) {
+            if (pt == 0 && carry) {
+              band[0] = band_next;
+              continue;
+            }
             f32x4 a = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
             for (int s = 0; s < 2; ++s) a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pf[pt][s], qv[s], a, 0, 0, 0);
             band[pt] = a;
           }
+          band_next = band[4];
         }
 #pragma unroll
         for (int hh = 0; hh < 2; ++hh) {
@@ -563,6 +575,9 @@ int chunk_attention_masked_bf16(const bf16* q, const bf16* kv, int kv_rows, cons
     (void)hipGetDevice(&dev);
     if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0) n_cu = 256;
   }
+  static int reuse = -1;   // CFM_ATTN_REUSE=0: recompute the shared band subtile (A/B)
+  if (reuse < 0) { const char* e = getenv("CFM_ATTN_REUSE"); reuse = e ? atoi(e) : 1; }
+  if (!reuse && diag == 0) diag = 5;
   int nch = (int)(((long long)n_chunks * H + n_cu - 1) / n_cu);
   nch = max(NCH, (nch + 1) & ~1);
   const dim3 grid((n_chunks + nch - 1) / nch, H);
