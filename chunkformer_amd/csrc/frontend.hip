@@ -14,6 +14,7 @@
 // buffer at meta[PM_SRC_ROW], rows >= meta[PM_NVALID] are zero padding, and
 // CMVN is applied after padding exactly like the reference (padding rows
 // become -mean*istd).
+#include <algorithm>
 #include <cstdlib>
 #include "cfm_common.h"
 #include "cfm_kernels.h"
@@ -246,7 +247,7 @@ __global__ __launch_bounds__(256) void fe_dw2_kernel(const T* __restrict__ in, i
   const size_t idx = (size_t)blockIdx.x * 256 + threadIdx.x;
   const size_t total = (size_t)nwin * FE_F3 * d8;
   if (idx >= total) return;
-  const int t3a = (int)((long long)blockIdx.y * T3 / FE_DW2_SEG), t3b = (int)((long long)(blockIdx.y + 1) * T3 / FE_DW2_SEG);
+  const int t3a = (int)((long long)blockIdx.y * T3 / gridDim.y), t3b = (int)((long long)(blockIdx.y + 1) * T3 / gridDim.y);
   const int c = (int)(idx % d8) * 8;
   const size_t r = idx / d8;
   const int f3 = r % FE_F3;
@@ -314,8 +315,10 @@ int frontend_dw2(const T* in, int nwin, int T2, int d, const float* w, const flo
   if (d % 8) return (int)hipErrorInvalidValue;
   const size_t total = (size_t)nwin * FE_F3 * (d / 8);
   if (total == 0 || T3 <= 0) return 0;
-  hipLaunchKernelGGL((fe_dw2_kernel<T>), dim3((unsigned)((total + 255) / 256), FE_DW2_SEG), dim3(256), 0, st, in, nwin,
-                     T2, T3, d, w, b, out);
+  static int seg = 0;   // CFM_DW2_SEG: row segments per walk (A/B)
+  if (!seg) { const char* e = getenv("CFM_DW2_SEG"); seg = e ? std::max(1, atoi(e)) : FE_DW2_SEG; }
+  hipLaunchKernelGGL((fe_dw2_kernel<T>), dim3((unsigned)((total + 255) / 256), std::min(seg, T3)), dim3(256), 0, st, in,
+                     nwin, T2, T3, d, w, b, out);
   CFM_CHECK_LAUNCH();
   return 0;
 }
