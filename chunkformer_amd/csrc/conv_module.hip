@@ -193,7 +193,7 @@ __global__ __launch_bounds__(512) void conv_dw_ln_silu_dot2_kernel(const bf16* _
                                                                    const float* __restrict__ bdw,
                                                                    const float* __restrict__ lnw,
                                                                    const float* __restrict__ lnb, float eps,
-                                                                   bf16* __restrict__ out) {
+                                                                   bf16* __restrict__ out, int dma) {
   constexpr int d = VPL * 64, NW = VPL / 2;   // NW dwords (channel pairs) per lane per row
   constexpr int MAXJ = 64 + 15;               // window rows + the zero row of the w[15] = 0 tap
   constexpr int RW = 8;                       // output rows per wave
@@ -205,11 +205,24 @@ __global__ __launch_bounds__(512) void conv_dw_ln_silu_dot2_kernel(const bf16* _
   const int nj = nout + 14;
   const int jlo = max(D[CD_J_LO], 0), jhi = min(D[CD_J_HI], nj);
   constexpr int V8 = d / 8;   // 16-B vectors per row
-  for (int idx = tid; idx < MAXJ * V8; idx += 512) {
-    const int j = idx / V8, v = idx % V8;
-    u32x4 val = (u32x4){0u, 0u, 0u, 0u};
-    if (j >= jlo && j < jhi) val = *reinterpret_cast<const u32x4*>(glu + (size_t)(src0 + j) * d + v * 8);
-    *reinterpret_cast<u32x4*>(win + j * d + v * 8) = val;
+  if (VPL == 8 && dma) {
+    // d = 512: a row is 1 KiB = one LDS-DMA instruction (64 lanes x 16 B, lane-linear), all of the
+    // window in flight at once; rows outside [jlo, jhi) are zeroed instead
+    for (int j = __builtin_amdgcn_readfirstlane(w); j < MAXJ; j += 8) {
+      if (j >= jlo && j < jhi)
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(glu + (size_t)(src0 + j) * d + lane * 8),
+                                         (__attribute__((address_space(3))) void*)(win + j * d), 16, 0, 0);
+      else
+        *reinterpret_cast<u32x4*>(win + j * d + lane * 8) = (u32x4){0u, 0u, 0u, 0u};
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  } else {
+    for (int idx = tid; idx < MAXJ * V8; idx += 512) {
+      const int j = idx / V8, v = idx % V8;
+      u32x4 val = (u32x4){0u, 0u, 0u, 0u};
+      if (j >= jlo && j < jhi) val = *reinterpret_cast<const u32x4*>(glu + (size_t)(src0 + j) * d + v * 8);
+      *reinterpret_cast<u32x4*>(win + j * d + v * 8) = val;
+    }
   }
   __syncthreads();
   const int i0 = w * RW;
@@ -305,11 +318,13 @@ int conv_dw_ln_silu(const T* glu, const int32_t* desc, int nblk, int d, const fl
   if (nblk <= 0) return 0;
   static int dot2 = -1;   // CFM_CONV_DOT2=0: the per-tap f32 kernel (A/B)
   if (dot2 < 0) { const char* e = getenv("CFM_CONV_DOT2"); dot2 = e ? atoi(e) : 1; }
+  static int dma = -1;    // CFM_CONV_DMA=0: stage the window through registers (A/B)
+  if (dma < 0) { const char* e = getenv("CFM_CONV_DMA"); dma = e ? atoi(e) : 1; }
   if constexpr (std::is_same<T, bf16>::value) {
     if (dot2) {
-      if (d == 128) hipLaunchKernelGGL((conv_dw_ln_silu_dot2_kernel<2>), dim3(nblk), dim3(512), 0, st, glu, desc, wdw_t, bdw, lnw, lnb, eps, out);
-      else if (d == 256) hipLaunchKernelGGL((conv_dw_ln_silu_dot2_kernel<4>), dim3(nblk), dim3(512), 0, st, glu, desc, wdw_t, bdw, lnw, lnb, eps, out);
-      else if (d == 512) hipLaunchKernelGGL((conv_dw_ln_silu_dot2_kernel<8>), dim3(nblk), dim3(512), 0, st, glu, desc, wdw_t, bdw, lnw, lnb, eps, out);
+      if (d == 128) hipLaunchKernelGGL((conv_dw_ln_silu_dot2_kernel<2>), dim3(nblk), dim3(512), 0, st, glu, desc, wdw_t, bdw, lnw, lnb, eps, out, dma);
+      else if (d == 256) hipLaunchKernelGGL((conv_dw_ln_silu_dot2_kernel<4>), dim3(nblk), dim3(512), 0, st, glu, desc, wdw_t, bdw, lnw, lnb, eps, out, dma);
+      else if (d == 512) hipLaunchKernelGGL((conv_dw_ln_silu_dot2_kernel<8>), dim3(nblk), dim3(512), 0, st, glu, desc, wdw_t, bdw, lnw, lnb, eps, out, dma);
       else return (int)hipErrorInvalidValue;
       CFM_CHECK_LAUNCH();
       return 0;
