@@ -173,7 +173,7 @@ struct ModelT : public cfm_model {
 
   struct WS {
     float* x;
-    T *h, *hid, *q, *kv, *ao, *glu, *cv, *y, *y2, *P, *pos, *feA, *feB;
+    T *h, *hid, *q, *kv, *ao, *glu, *cv, *y, *y2, *P, *pos, *feA, *feB, *feC;
   };
 
   WS carve(void* base, const int32_t* h, size_t* total) const {
@@ -199,6 +199,10 @@ struct ModelT : public cfm_model {
     w.pos = c.take<T>(prow_pad * d);
     w.feA = c.take<T>(G * T2 * 19 * d);
     w.feB = c.take<T>(G * T2 * 19 * d);
+    // the front-end output Linear's input [nwin * T3, 9d] for every window group: one GEMM over
+    // all windows after the group loop (per group it is too small to fill the chip)
+    const int T3 = (T2 - 3) / 2 + 1;
+    w.feC = c.take<T>((size_t)h[PH_NWIN] * T3 * 9 * d);
     if (total) *total = c.off;
     return w;
   }
@@ -242,11 +246,11 @@ struct ModelT : public cfm_model {
       EpiArgs e1; e1.bias = fe.b_pw1; e1.out = w.feB; e1.ldo = d;
       PROF(PC_FE_GEMM, gemm<T>(EPI_STORE, ACT_RELU, w.feA, d, (const T*)fe.pw1, d, ng * T2 * 19, d, d, e1, st));
       PROF(PC_FE_DW2, frontend_dw2<T>(w.feB, ng, T2, d, fe.w2, fe.b2, w.feA, st));
-      EpiArgs e2; e2.bias = fe.b_pw2; e2.out = w.feB; e2.ldo = d;
+      EpiArgs e2; e2.bias = fe.b_pw2; e2.out = w.feC + (size_t)g0 * T3 * 9 * d; e2.ldo = d;
       PROF(PC_FE_GEMM, gemm<T>(EPI_STORE, ACT_RELU, w.feA, d, (const T*)fe.pw2, d, ng * T3 * 9, d, d, e2, st));
-      EpiArgs e3; e3.bias = fe.b_out; e3.out = w.x; e3.ldo = d; e3.row_off = g0 * tout; e3.alpha = std::sqrt((float)d);
-      PROF(PC_FE_GEMM, gemm<T>(EPI_STORE_F32, ACT_NONE, w.feB, 9 * d, (const T*)fe.wout, 9 * d, ng * T3, d, 9 * d, e3, st));
     }
+    { EpiArgs e3; e3.bias = fe.b_out; e3.out = w.x; e3.ldo = d; e3.row_off = 0; e3.alpha = std::sqrt((float)d);
+      PROF(PC_FE_GEMM, gemm<T>(EPI_STORE_F32, ACT_NONE, w.feC, 9 * d, (const T*)fe.wout, 9 * d, nwin * T3, d, 9 * d, e3, st)); }
     // ---------------- relative positions: P_l = pos . W_pos_l^T
     const int nl = (max_layers >= 0 && max_layers < cfg.num_blocks) ? max_layers : cfg.num_blocks;
     PROF(PC_POS, pos_table<T>(d, p_rows, hh[PH_PANCHOR], w.pos, st));
