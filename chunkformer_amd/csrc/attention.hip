@@ -36,7 +36,7 @@ template <typename T>
 __global__ __launch_bounds__(256) void chunk_attention_kernel(
     const T* __restrict__ Q, const T* __restrict__ KV, int kv_rows, const T* __restrict__ P, int p_rows,
     const float* __restrict__ pos_u, const float* __restrict__ pos_v, const int32_t* __restrict__ desc, int H,
-    T* __restrict__ out) {
+    T* __restrict__ out, int p_ld) {
   using LY = AttnLds<T>;
   using FT = typename Frag<T>::type;
   __shared__ __attribute__((aligned(16))) char smem[LY::TOTAL];
@@ -108,7 +108,7 @@ __global__ __launch_bounds__(256) void chunk_attention_kernel(
 #pragma unroll
     for (int n = 0; n < 5; ++n) {
       const int prow = min(max(kb + n * 16 + fr, 0), p_rows - 1);
-      const T* pp = P + (size_t)prow * d + h * 64;
+      const T* pp = P + (size_t)prow * p_ld + h * 64;
       f32x4 a = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int s = 0; s < 2; ++s) a = mma16(qv[s], ld8<T>(pp + s * 32 + 8 * g), a);
@@ -182,18 +182,19 @@ __global__ __launch_bounds__(256) void chunk_attention_kernel(
 
 template <typename T>
 int chunk_attention(const T* q, const T* kv, int kv_rows, const T* P, int p_rows, const float* pos_u,
-                    const float* pos_v, const int32_t* desc, int nblk, int H, T* out, hipStream_t st) {
+                    const float* pos_v, const int32_t* desc, int nblk, int H, T* out, hipStream_t st, int p_ld) {
   if (nblk <= 0) return 0;
+  if (p_ld <= 0) p_ld = H * 64;
   hipLaunchKernelGGL((chunk_attention_kernel<T>), dim3(nblk, H), dim3(256), 0, st, q, kv, kv_rows, P, p_rows, pos_u,
-                     pos_v, desc, H, out);
+                     pos_v, desc, H, out, p_ld);
   CFM_CHECK_LAUNCH();
   return 0;
 }
 
 template int chunk_attention<float>(const float*, const float*, int, const float*, int, const float*, const float*,
-                                    const int32_t*, int, int, float*, hipStream_t);
+                                    const int32_t*, int, int, float*, hipStream_t, int);
 template int chunk_attention<bf16>(const bf16*, const bf16*, int, const bf16*, int, const float*, const float*,
-                                   const int32_t*, int, int, bf16*, hipStream_t);
+                                   const int32_t*, int, int, bf16*, hipStream_t, int);
 
 
 
@@ -233,7 +234,7 @@ CFM_DEV int sw128(int row, int ch) { return row * 128 + ((ch ^ ((row >> 1) & 7))
 __global__ __launch_bounds__(512, 1) void chunk_attention_ring_kernel(
     const bf16* __restrict__ Q, const bf16* __restrict__ KV, int kv_rows, const bf16* __restrict__ P, int p_rows,
     const float* __restrict__ pos_u, const float* __restrict__ pos_v, const int32_t* __restrict__ desc, int n_chunks,
-    int H, int C, int W, bf16* __restrict__ out, int diag, int nch) {
+    int H, int C, int W, bf16* __restrict__ out, int diag, int nch, int p_ld) {
   const bool reuse_band = diag != 5;   // diag 5: recompute band subtile 0 of every tile (A/B)
   __shared__ __attribute__((aligned(16))) char smem[RING_LDS];
   char* kr = smem;
@@ -259,7 +260,7 @@ __global__ __launch_bounds__(512, 1) void chunk_attention_ring_kernel(
   // ---- stage P rows and the first pair's windows (rows [kv0, kv0 + W + C))
   for (int idx = tid; idx < p_rows * 8; idx += 512) {
     const int r = idx >> 3, ch = idx & 7;
-    *reinterpret_cast<u32x4*>(pl + sw128(r, ch)) = *reinterpret_cast<const u32x4*>(P + (size_t)r * d + h * 64 + ch * 8);
+    *reinterpret_cast<u32x4*>(pl + sw128(r, ch)) = *reinterpret_cast<const u32x4*>(P + (size_t)r * p_ld + h * 64 + ch * 8);
   }
   // staging unit = two consecutive (even-aligned) flat rows x one 16-B chunk of K and V: the K halves
   // go to the swizzled K ring, the V halves are interleaved into 8 bf16x2 words of V^T (conflict-free:
@@ -565,7 +566,8 @@ __global__ __launch_bounds__(512, 1) void chunk_attention_ring_kernel(
 // returns -1 when the shape is not eligible for the ring kernel
 int chunk_attention_masked_bf16(const bf16* q, const bf16* kv, int kv_rows, const bf16* P, int p_rows,
                                 const float* pos_u, const float* pos_v, const int32_t* desc, int n_chunks, int H,
-                                int C, int W, bf16* out, hipStream_t st, int diag) {
+                                int C, int W, bf16* out, hipStream_t st, int diag, int p_ld) {
+  if (p_ld <= 0) p_ld = H * 64;
   if (C <= 0 || C > 64 || (C % 16) || (W & 1) || W + C > RING || p_rows > RING || n_chunks <= 0) return -1;
   // one block per CU (LDS-bound), each sweeping a long run of chunks of one head: one prologue
   // (P rows + first window) per block instead of one per 8 chunks
@@ -582,7 +584,7 @@ int chunk_attention_masked_bf16(const bf16* q, const bf16* kv, int kv_rows, cons
   nch = max(NCH, (nch + 1) & ~1);
   const dim3 grid((n_chunks + nch - 1) / nch, H);
   hipLaunchKernelGGL(chunk_attention_ring_kernel, grid, dim3(512), 0, st, q, kv, kv_rows, P, p_rows, pos_u, pos_v,
-                     desc, n_chunks, H, C, W, out, diag, nch);
+                     desc, n_chunks, H, C, W, out, diag, nch, p_ld);
   CFM_CHECK_LAUNCH();
   return 0;
 }

@@ -59,12 +59,13 @@ int layernorm2_f32(float* x, const ResidAdd<T>& ra, int M, int d, const float* w
 // chunk attention (attention.hip)
 template <typename T>
 int chunk_attention(const T* q, const T* kv, int kv_rows, const T* P, int p_rows, const float* pos_u,
-                    const float* pos_v, const int32_t* desc, int nblk, int H, T* out, hipStream_t st);
+                    const float* pos_v, const int32_t* desc, int nblk, int H, T* out, hipStream_t st,
+                    int p_ld = 0);   // P row stride (elements; 0 = H * 64)
 
 // masked-batch ring kernel (bf16); -1 = shape not eligible
 int chunk_attention_masked_bf16(const bf16* q, const bf16* kv, int kv_rows, const bf16* P, int p_rows,
                                 const float* pos_u, const float* pos_v, const int32_t* desc, int n_chunks, int H,
-                                int C, int W, bf16* out, hipStream_t st, int diag = 0);
+                                int C, int W, bf16* out, hipStream_t st, int diag = 0, int p_ld = 0);
 
 // fused FFN (ffn.hip): y = w2 . SiLU(w1 . x + b1) + b2 over a repacked slab stream; -1 = not eligible
 int ffn_fused(const bf16* x, int M, const bf16* wstream, const float* b1, const float* b2, bf16* y, int d, int ff,

@@ -76,6 +76,7 @@ struct FrontW {
   float *an_w, *an_b;
   void* ctc_w = nullptr;
   float* ctc_b = nullptr;
+  void* pos_all = nullptr;   // every layer's linear_pos weight stacked [nb * d, d]: one GEMM per call
 };
 
 }  // namespace cfm
@@ -251,13 +252,13 @@ struct ModelT : public cfm_model {
     }
     { EpiArgs e3; e3.bias = fe.b_out; e3.out = w.x; e3.ldo = d; e3.row_off = 0; e3.alpha = std::sqrt((float)d);
       PROF(PC_FE_GEMM, gemm<T>(EPI_STORE_F32, ACT_NONE, w.feC, 9 * d, (const T*)fe.wout, 9 * d, nwin * T3, d, 9 * d, e3, st)); }
-    // ---------------- relative positions: P_l = pos . W_pos_l^T
+    // ---------------- relative positions: P_l = pos . W_pos_l^T for every layer in ONE GEMM against
+    // the stacked weights: P is [p_rows, nb * d], layer l at column l * d (row stride nb * d)
     const int nl = (max_layers >= 0 && max_layers < cfg.num_blocks) ? max_layers : cfg.num_blocks;
+    const int p_ld = cfg.num_blocks * d;
     PROF(PC_POS, pos_table<T>(d, p_rows, hh[PH_PANCHOR], w.pos, st));
-    for (int l = 0; l < nl; ++l) {
-      EpiArgs e; e.out = w.P + (size_t)l * prow_pad * d; e.ldo = d;
-      PROF(PC_POS, gemm<T>(EPI_STORE, ACT_NONE, w.pos, d, (const T*)layers[l].pos, d, p_rows, d, d, e, st));
-    }
+    { EpiArgs e; e.out = w.P; e.ldo = p_ld;
+      PROF(PC_POS, gemm<T>(EPI_STORE, ACT_NONE, w.pos, d, (const T*)fe.pos_all, d, p_rows, p_ld, d, e, st)); }
     // ---------------- stream padding rows (cache slots and right zero padding)
     if (kvoff > 0) HIPC(hipMemsetAsync(w.kv, 0, (size_t)kvoff * 2 * d * sizeof(T), st));
     if (kv_rows > kvoff + rows)
@@ -317,12 +318,12 @@ struct ModelT : public cfm_model {
         prof_begin(PC_ATTN, st, &pb_);
         if constexpr (sizeof(T) == 2) {
           if (masked && use_ring_attention)
-            r = chunk_attention_masked_bf16(w.q, w.kv, kv_rows, w.P + (size_t)l * prow_pad * d, p_rows, Lw.pu, Lw.pv,
-                                            attd, natt, H, C, hh[PH_L] + C + hh[PH_R], w.ao, st, attn_diag);
+            r = chunk_attention_masked_bf16(w.q, w.kv, kv_rows, w.P + (size_t)l * d, p_rows, Lw.pu, Lw.pv,
+                                            attd, natt, H, C, hh[PH_L] + C + hh[PH_R], w.ao, st, attn_diag, p_ld);
         }
         if (r == -1)
-          r = chunk_attention<T>(w.q, w.kv, kv_rows, w.P + (size_t)l * prow_pad * d, p_rows, Lw.pu, Lw.pv, attd, natt,
-                                 H, w.ao, st);
+          r = chunk_attention<T>(w.q, w.kv, kv_rows, w.P + (size_t)l * d, p_rows, Lw.pu, Lw.pv, attd, natt,
+                                 H, w.ao, st, p_ld);
         KCHK(r);
         prof_end(PC_ATTN, st, pb_);
       }
@@ -569,6 +570,15 @@ static cfm_status build_model(const cfm_config& cfg, const HostW& hw, int device
           {"norm_ff.weight", &Lw.ln_ff_w},          {"norm_ff.bias", &Lw.ln_ff_b},
           {"norm_final.weight", &Lw.ln_fin_w},      {"norm_final.bias", &Lw.ln_fin_b}};
       for (auto& kv : lns) put_f32(hw.get(p + kv.first, d), d, kv.second);
+    }
+    {   // every layer's linear_pos weight stacked [nb * d, d] (ModelT::encode: one P GEMM per call)
+      std::vector<float> all((size_t)nb * d * d);
+      for (int l = 0; l < nb; ++l) {
+        const std::string p = E + "encoders." + std::to_string(l) + ".";
+        std::memcpy(all.data() + (size_t)l * d * d, hw.get(p + "self_attn.linear_pos.weight", (int64_t)d * d),
+                    (size_t)d * d * sizeof(float));
+      }
+      put_T(all, &F.pos_all);
     }
   } catch (const std::string& e) {
     return set_error(CFM_ERR_VALUE, e);
