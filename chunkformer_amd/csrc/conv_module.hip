@@ -12,6 +12,7 @@
 // One wave per output row, lane l owns channels [l*VPL, l*VPL+VPL); the LN
 // statistics are wave reductions.  Depthwise weights are stored tap-major
 // [15][d] so every tap is one coalesced vector load.
+#include <algorithm>
 #include <cstdlib>
 #include <type_traits>
 #include "cfm_common.h"
@@ -186,45 +187,14 @@ CFM_DEV float dot2_bf16(unsigned a, unsigned b, float c) {
 CFM_DEV unsigned pk_bf16(float lo, float hi) {
   return __builtin_bit_cast(unsigned, (bf16x2_t){(__bf16)lo, (__bf16)hi});
 }
+// the compute half of the dot2 kernels: wave w's RW output rows from the staged window `win`
 template <int VPL>
-__global__ __launch_bounds__(512) void conv_dw_ln_silu_dot2_kernel(const bf16* __restrict__ glu,
-                                                                   const int32_t* __restrict__ desc,
-                                                                   const float* __restrict__ wdw,
-                                                                   const float* __restrict__ bdw,
-                                                                   const float* __restrict__ lnw,
-                                                                   const float* __restrict__ lnb, float eps,
-                                                                   bf16* __restrict__ out, int dma) {
-  constexpr int d = VPL * 64, NW = VPL / 2;   // NW dwords (channel pairs) per lane per row
-  constexpr int MAXJ = 64 + 15;               // window rows + the zero row of the w[15] = 0 tap
-  constexpr int RW = 8;                       // output rows per wave
+CFM_DEV void conv_dot2_rows(const bf16* __restrict__ win, int nout, int out_row0, const float* __restrict__ wdw,
+                            const float* __restrict__ bdw, const float* __restrict__ lnw,
+                            const float* __restrict__ lnb, float eps, bf16* __restrict__ out, int w, int lane) {
+  constexpr int d = VPL * 64, NW = VPL / 2;
+  constexpr int RW = 8;
   typedef bf16 bvec __attribute__((ext_vector_type(VPL)));
-  __shared__ __attribute__((aligned(16))) bf16 win[MAXJ * d];
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int32_t* D = desc + (size_t)blockIdx.x * CD_INTS;
-  const int out_row0 = D[CD_OUT_ROW0], nout = D[CD_NOUT], src0 = D[CD_SRC_ROW0];
-  const int nj = nout + 14;
-  const int jlo = max(D[CD_J_LO], 0), jhi = min(D[CD_J_HI], nj);
-  constexpr int V8 = d / 8;   // 16-B vectors per row
-  if (VPL == 8 && dma) {
-    // d = 512: a row is 1 KiB = one LDS-DMA instruction (64 lanes x 16 B, lane-linear), all of the
-    // window in flight at once; rows outside [jlo, jhi) are zeroed instead
-    for (int j = __builtin_amdgcn_readfirstlane(w); j < MAXJ; j += 8) {
-      if (j >= jlo && j < jhi)
-        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(glu + (size_t)(src0 + j) * d + lane * 8),
-                                         (__attribute__((address_space(3))) void*)(win + j * d), 16, 0, 0);
-      else
-        *reinterpret_cast<u32x4*>(win + j * d + lane * 8) = (u32x4){0u, 0u, 0u, 0u};
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  } else {
-    for (int idx = tid; idx < MAXJ * V8; idx += 512) {
-      const int j = idx / V8, v = idx % V8;
-      u32x4 val = (u32x4){0u, 0u, 0u, 0u};
-      if (j >= jlo && j < jhi) val = *reinterpret_cast<const u32x4*>(glu + (size_t)(src0 + j) * d + v * 8);
-      *reinterpret_cast<u32x4*>(win + j * d + v * 8) = val;
-    }
-  }
-  __syncthreads();
   const int i0 = w * RW;
   if (i0 >= nout) return;
   const int c0 = lane * VPL;
@@ -311,6 +281,49 @@ __global__ __launch_bounds__(512) void conv_dw_ln_silu_dot2_kernel(const bf16* _
     *reinterpret_cast<bvec*>(out + (size_t)(out_row0 + i0 + r) * d + c0) = o;
   }
 }
+
+template <int VPL>
+__global__ __launch_bounds__(512) void conv_dw_ln_silu_dot2_kernel(const bf16* __restrict__ glu,
+                                                                   const int32_t* __restrict__ desc,
+                                                                   const float* __restrict__ wdw,
+                                                                   const float* __restrict__ bdw,
+                                                                   const float* __restrict__ lnw,
+                                                                   const float* __restrict__ lnb, float eps,
+                                                                   bf16* __restrict__ out, int dma) {
+  constexpr int d = VPL * 64, NW = VPL / 2;   // NW dwords (channel pairs) per lane per row
+  constexpr int MAXJ = 64 + 15;               // window rows + the zero row of the w[15] = 0 tap
+  constexpr int RW = 8;                       // output rows per wave
+  typedef bf16 bvec __attribute__((ext_vector_type(VPL)));
+  __shared__ __attribute__((aligned(16))) bf16 win[MAXJ * d];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int32_t* D = desc + (size_t)blockIdx.x * CD_INTS;
+  const int out_row0 = D[CD_OUT_ROW0], nout = D[CD_NOUT], src0 = D[CD_SRC_ROW0];
+  const int nj = nout + 14;
+  const int jlo = max(D[CD_J_LO], 0), jhi = min(D[CD_J_HI], nj);
+  constexpr int V8 = d / 8;   // 16-B vectors per row
+  if (VPL == 8 && dma) {
+    // d = 512: a row is 1 KiB = one LDS-DMA instruction (64 lanes x 16 B, lane-linear), all of the
+    // window in flight at once; rows outside [jlo, jhi) are zeroed instead
+    for (int j = __builtin_amdgcn_readfirstlane(w); j < MAXJ; j += 8) {
+      if (j >= jlo && j < jhi)
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(glu + (size_t)(src0 + j) * d + lane * 8),
+                                         (__attribute__((address_space(3))) void*)(win + j * d), 16, 0, 0);
+      else
+        *reinterpret_cast<u32x4*>(win + j * d + lane * 8) = (u32x4){0u, 0u, 0u, 0u};
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  } else {
+    for (int idx = tid; idx < MAXJ * V8; idx += 512) {
+      const int j = idx / V8, v = idx % V8;
+      u32x4 val = (u32x4){0u, 0u, 0u, 0u};
+      if (j >= jlo && j < jhi) val = *reinterpret_cast<const u32x4*>(glu + (size_t)(src0 + j) * d + v * 8);
+      *reinterpret_cast<u32x4*>(win + j * d + v * 8) = val;
+    }
+  }
+  __syncthreads();
+  conv_dot2_rows<VPL>(win, nout, out_row0, wdw, bdw, lnw, lnb, eps, out, w, lane);
+}
+
 
 template <typename T>
 int conv_dw_ln_silu(const T* glu, const int32_t* desc, int nblk, int d, const float* wdw_t, const float* bdw,
