@@ -7,7 +7,9 @@
 //     LN -> FFN_mac (GEMM SiLU, GEMM resid x0.5) -> LN -> QKV GEMM -> chunk attention
 //     -> out-proj GEMM (resid) -> LN -> pw1 GEMM + GLU -> dw/LN/SiLU -> pw2 GEMM (masked resid)
 //     -> LN -> FFN (x0.5) -> norm_final fused with the next layer's first LN / after_norm
+#include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <memory>
