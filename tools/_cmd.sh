@@ -1,10 +1,12 @@
+# Round check on one GPU (run via gpurun from the repo root): GPU parity tests, smoke, bf16 accuracy
+# probe and the default bench line.
 set -e
-R=$GRAFT_REPO_ROOT
-cd $R
+cd $GRAFT_REPO_ROOT
 timeout -k 10 600 python3 -u -m pytest tests/ -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 || { tail -30 gpurun_out/gpu_tests.log; exit 1; }
-tail -2 gpurun_out/gpu_tests.log
+tail -1 gpurun_out/gpu_tests.log
 timeout -k 10 120 python3 -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { tail -20 gpurun_out/smoke.log; exit 1; }
 tail -1 gpurun_out/smoke.log
-bash tools/profile_round.sh r01
-tail -1 gpurun_out/prof_r01/bench.json
-cat gpurun_out/prof_r01/traffic.txt | head -30
+timeout -k 10 120 python3 tools/bf16_err.py > gpurun_out/bf16_err.log 2>&1 || { tail -20 gpurun_out/bf16_err.log; exit 1; }
+grep "rel-L2" gpurun_out/bf16_err.log
+timeout -k 10 300 python3 bench.py > gpurun_out/bench.log 2>&1 || { tail -20 gpurun_out/bench.log; exit 1; }
+tail -1 gpurun_out/bench.log
