@@ -36,7 +36,7 @@ class EncoderConfig:
 
     def validate(self) -> None:
         assert self.d_model % self.n_heads == 0
-        assert self.head_dim == 64, "HIP attention kernel is built for head_dim 64"
+        assert self.head_dim in (64, 128), "HIP attention kernels are built for head_dim 64 or 128"
         assert self.d_model % 64 == 0 and self.ffn_dim % 64 == 0
         assert self.kernel_size == 15, "conv module kernel is built for k=15"
         assert self.input_dim == 80, "front-end kernel is built for 80 mel bins"
@@ -66,5 +66,8 @@ class EncoderConfig:
 
 # chunkformer-large (BASELINE.json configs[1]): 12 layers, d=512, 8 heads, ff 2048, V=5000 (paper BPE)
 LARGE = EncoderConfig()
+# the reference's shipped d=512 recipe family: 4 heads -> head_dim 128
+# (examples/asr/rnnt/conf/chunkformer-rnnt-large-vie.yaml:5-6)
+LARGE_4H = EncoderConfig(n_heads=4)
 # small config used for the committed golden fixtures (tests/golden)
 SMALL = EncoderConfig(d_model=128, n_heads=2, ffn_dim=256, num_blocks=2, vocab=48)

@@ -22,23 +22,28 @@
 
 namespace cfm {
 
-template <typename T> struct AttnLds {
-  static constexpr int VT_PITCH = 64 * sizeof(T) + 16;   // bytes per dim row of V^T
+template <typename T, int DK> struct AttnLds {
+  static constexpr int VT_PITCH = 64 * sizeof(T) + 16;   // bytes per dim row of V^T (64 keys)
   static constexpr int P_PITCH = 64 * sizeof(T) + 16;    // bytes per query row of probabilities
   static constexpr int BD_PITCH = 85;                    // floats per row of the bd band
-  static constexpr int VT_BYTES = 64 * VT_PITCH;
+  static constexpr int VT_BYTES = DK * VT_PITCH;
   static constexpr int P_BYTES = 16 * P_PITCH;           // per wave
   static constexpr int BD_BYTES = 16 * BD_PITCH * 4;     // per wave
   static constexpr int TOTAL = VT_BYTES + 4 * (P_BYTES + BD_BYTES);
 };
 
-template <typename T>
+// DK = head dim (64: 8-head d=512 / 2-head d=128; 128: the 4-head d=512 recipes,
+// examples/asr/rnnt/conf/chunkformer-rnnt-large-vie.yaml:5-6).  KV stream rows are
+// [H][K dk | V dk]; P / pos_u / pos_v per head at h * DK.
+template <typename T, int DK>
 __global__ __launch_bounds__(256) void chunk_attention_kernel(
     const T* __restrict__ Q, const T* __restrict__ KV, int kv_rows, const T* __restrict__ P, int p_rows,
     const float* __restrict__ pos_u, const float* __restrict__ pos_v, const int32_t* __restrict__ desc, int H,
     T* __restrict__ out, int p_ld) {
-  using LY = AttnLds<T>;
+  using LY = AttnLds<T, DK>;
   using FT = typename Frag<T>::type;
+  constexpr int NS = DK / 32;   // 32-deep contraction sub-steps over the head dim
+  constexpr int NO = DK / 16;   // 16-wide output n-blocks
   __shared__ __attribute__((aligned(16))) char smem[LY::TOTAL];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int fr = lane & 15, g = lane >> 4;
@@ -46,50 +51,52 @@ __global__ __launch_bounds__(256) void chunk_attention_kernel(
   const int32_t* D = desc + (size_t)blockIdx.x * AD_INTS;
   const int q_row0 = D[AD_Q_ROW0], nq = D[AD_NQ], kv_row0 = D[AD_KV_ROW0];
   const int key_lo = D[AD_KEY_LO], key_hi = D[AD_KEY_HI], p_base = D[AD_P_BASE], q_valid = D[AD_Q_VALID];
-  const int d = H * 64;
+  const int d = H * DK;
   const int i0 = w * 16;
 
   char* vt = smem;
   char* pb = smem + LY::VT_BYTES + w * (LY::P_BYTES + LY::BD_BYTES);
   float* bd = reinterpret_cast<float*>(pb + LY::P_BYTES);
 
-  // ---- query fragments (row i0 + fr), with u / v biases, two 32-deep sub-steps over dk = 64
-  FT qu[2], qv[2];
+  // ---- query fragments (row i0 + fr), with u / v biases, NS 32-deep sub-steps over dk
+  FT qu[NS], qv[NS];
   {
     const int qi = min(i0 + fr, nq - 1);
-    const T* qp = Q + (size_t)(q_row0 + qi) * d + h * 64;
+    const T* qp = Q + (size_t)(q_row0 + qi) * d + h * DK;
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
+    for (int s = 0; s < NS; ++s) {
       const FT raw = ld8<T>(qp + s * 32 + 8 * g);
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const int dd = s * 32 + 8 * g + e;
         const float qf = to_f32(raw[e]);
-        qu[s][e] = from_f32<T>(qf + pos_u[h * 64 + dd]);
-        qv[s][e] = from_f32<T>(qf + pos_v[h * 64 + dd]);
+        qu[s][e] = from_f32<T>(qf + pos_u[h * DK + dd]);
+        qv[s][e] = from_f32<T>(qf + pos_v[h * DK + dd]);
       }
     }
   }
 
-  f32x4 O[4];
+  f32x4 O[NO];
   float m_r[4], l_r[4];
 #pragma unroll
-  for (int n = 0; n < 4; ++n) O[n] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  for (int n = 0; n < NO; ++n) O[n] = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int r = 0; r < 4; ++r) { m_r[r] = -INFINITY; l_r[r] = 0.f; }
 
-  const float scale = 0.125f;   // 1 / sqrt(64)
+  const float scale = 1.0f / sqrtf((float)DK);
   for (int j0 = key_lo; j0 < key_hi; j0 += 64) {
-    // ---- stage V^T of keys j0 .. j0+63 (each thread: one key, 16 dims)
+    // ---- stage V^T of keys j0 .. j0+63 (each thread: one key, DK/4 dims)
     {
-      const int key = tid >> 2, dq = (tid & 3) * 16;
+      constexpr int DQ = DK / 4;
+      const int key = tid >> 2, dq = (tid & 3) * DQ;
       const int row = min(max(kv_row0 + j0 + key, 0), kv_rows - 1);
-      const T* vp = KV + (size_t)row * (2 * d) + h * 128 + 64 + dq;
-      const FT v0 = ld8<T>(vp), v1 = ld8<T>(vp + 8);
+      const T* vp = KV + (size_t)row * (2 * d) + h * 2 * DK + DK + dq;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        *reinterpret_cast<T*>(vt + (dq + e) * LY::VT_PITCH + key * sizeof(T)) = v0[e];
-        *reinterpret_cast<T*>(vt + (dq + 8 + e) * LY::VT_PITCH + key * sizeof(T)) = v1[e];
+      for (int c8 = 0; c8 < DQ / 8; ++c8) {
+        const FT v0 = ld8<T>(vp + 8 * c8);
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          *reinterpret_cast<T*>(vt + (dq + 8 * c8 + e) * LY::VT_PITCH + key * sizeof(T)) = v0[e];
       }
     }
     // ---- ac = (q+u) K^T  (4 key sub-tiles of 16)
@@ -97,10 +104,10 @@ __global__ __launch_bounds__(256) void chunk_attention_kernel(
 #pragma unroll
     for (int n = 0; n < 4; ++n) {
       const int row = min(max(kv_row0 + j0 + n * 16 + fr, 0), kv_rows - 1);
-      const T* kp = KV + (size_t)row * (2 * d) + h * 128;
+      const T* kp = KV + (size_t)row * (2 * d) + h * 2 * DK;
       f32x4 a = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int s = 0; s < 2; ++s) a = mma16(qu[s], ld8<T>(kp + s * 32 + 8 * g), a);
+      for (int s = 0; s < NS; ++s) a = mma16(qu[s], ld8<T>(kp + s * 32 + 8 * g), a);
       S[n] = a;
     }
     // ---- bd band = (q+v) P^T over rel-pos rows kb .. kb+79
@@ -108,10 +115,10 @@ __global__ __launch_bounds__(256) void chunk_attention_kernel(
 #pragma unroll
     for (int n = 0; n < 5; ++n) {
       const int prow = min(max(kb + n * 16 + fr, 0), p_rows - 1);
-      const T* pp = P + (size_t)prow * p_ld + h * 64;
+      const T* pp = P + (size_t)prow * p_ld + h * DK;
       f32x4 a = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int s = 0; s < 2; ++s) a = mma16(qv[s], ld8<T>(pp + s * 32 + 8 * g), a);
+      for (int s = 0; s < NS; ++s) a = mma16(qv[s], ld8<T>(pp + s * 32 + 8 * g), a);
 #pragma unroll
       for (int r = 0; r < 4; ++r) bd[(4 * g + r) * LY::BD_PITCH + n * 16 + fr] = a[r];
     }
@@ -146,7 +153,7 @@ __global__ __launch_bounds__(256) void chunk_attention_kernel(
       }
       l_r[r] = l_r[r] * alpha + group16_sum(rs);
 #pragma unroll
-      for (int n = 0; n < 4; ++n) O[n][r] *= alpha;
+      for (int n = 0; n < NO; ++n) O[n][r] *= alpha;
     }
     // ---- probabilities -> LDS (row-major [query][key]) -> A fragments
 #pragma unroll
@@ -159,7 +166,7 @@ __global__ __launch_bounds__(256) void chunk_attention_kernel(
     for (int s = 0; s < 2; ++s) {
       const FT pa = *reinterpret_cast<const FT*>(pb + fr * LY::P_PITCH + (s * 32 + 8 * g) * sizeof(T));
 #pragma unroll
-      for (int n = 0; n < 4; ++n) {
+      for (int n = 0; n < NO; ++n) {
         const FT vb = *reinterpret_cast<const FT*>(vt + (n * 16 + fr) * LY::VT_PITCH + (s * 32 + 8 * g) * sizeof(T));
         O[n] = mma16(pa, vb, O[n]);
       }
@@ -167,34 +174,41 @@ __global__ __launch_bounds__(256) void chunk_attention_kernel(
     __syncthreads();
   }
 
-  // ---- normalise and store (head-merged layout [row][h*64 + dim])
+  // ---- normalise and store (head-merged layout [row][h*DK + dim])
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int i = i0 + 4 * g + r;
     if (i >= nq) continue;
     const bool live = (i < q_valid) && (l_r[r] > 0.f);
     const float inv = live ? 1.f / l_r[r] : 0.f;
-    T* op = out + (size_t)(q_row0 + i) * d + h * 64;
+    T* op = out + (size_t)(q_row0 + i) * d + h * DK;
 #pragma unroll
-    for (int n = 0; n < 4; ++n) op[n * 16 + fr] = from_f32<T>(O[n][r] * inv);
+    for (int n = 0; n < NO; ++n) op[n * 16 + fr] = from_f32<T>(O[n][r] * inv);
   }
 }
 
 template <typename T>
 int chunk_attention(const T* q, const T* kv, int kv_rows, const T* P, int p_rows, const float* pos_u,
-                    const float* pos_v, const int32_t* desc, int nblk, int H, T* out, hipStream_t st, int p_ld) {
+                    const float* pos_v, const int32_t* desc, int nblk, int H, int dk, T* out, hipStream_t st,
+                    int p_ld) {
   if (nblk <= 0) return 0;
-  if (p_ld <= 0) p_ld = H * 64;
-  hipLaunchKernelGGL((chunk_attention_kernel<T>), dim3(nblk, H), dim3(256), 0, st, q, kv, kv_rows, P, p_rows, pos_u,
-                     pos_v, desc, H, out, p_ld);
+  if (p_ld <= 0) p_ld = H * dk;
+  if (dk == 64)
+    hipLaunchKernelGGL((chunk_attention_kernel<T, 64>), dim3(nblk, H), dim3(256), 0, st, q, kv, kv_rows, P, p_rows,
+                       pos_u, pos_v, desc, H, out, p_ld);
+  else if (dk == 128)
+    hipLaunchKernelGGL((chunk_attention_kernel<T, 128>), dim3(nblk, H), dim3(256), 0, st, q, kv, kv_rows, P, p_rows,
+                       pos_u, pos_v, desc, H, out, p_ld);
+  else
+    return (int)hipErrorInvalidValue;
   CFM_CHECK_LAUNCH();
   return 0;
 }
 
 template int chunk_attention<float>(const float*, const float*, int, const float*, int, const float*, const float*,
-                                    const int32_t*, int, int, float*, hipStream_t, int);
+                                    const int32_t*, int, int, int, float*, hipStream_t, int);
 template int chunk_attention<bf16>(const bf16*, const bf16*, int, const bf16*, int, const float*, const float*,
-                                   const int32_t*, int, int, bf16*, hipStream_t, int);
+                                   const int32_t*, int, int, int, bf16*, hipStream_t, int);
 
 
 
@@ -568,7 +582,8 @@ int chunk_attention_masked_bf16(const bf16* q, const bf16* kv, int kv_rows, cons
                                 const float* pos_u, const float* pos_v, const int32_t* desc, int n_chunks, int H,
                                 int C, int W, bf16* out, hipStream_t st, int diag, int p_ld) {
   if (p_ld <= 0) p_ld = H * 64;
-  if (C <= 0 || C > 64 || (C % 16) || (W & 1) || W + C > RING || p_rows > RING || n_chunks <= 0) return -1;
+  // W <= 320: a query's scores are 5 tiles of 64 keys held in registers (exact softmax)
+  if (C <= 0 || C > 64 || (C % 16) || (W & 1) || W > 320 || W + C > RING || p_rows > RING || n_chunks <= 0) return -1;
   // one block per CU (LDS-bound), each sweeping a long run of chunks of one head: one prologue
   // (P rows + first window) per block instead of one per 8 chunks
   static int n_cu = 0;

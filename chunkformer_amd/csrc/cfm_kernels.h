@@ -5,6 +5,8 @@
 
 typedef __bf16 bf16;
 
+#define CFM_HD_INLINE __host__ __device__ __forceinline__
+
 namespace cfm {
 
 enum { EPI_STORE = 0, EPI_STORE_F32 = 1, EPI_RESID = 2, EPI_QKV = 3, EPI_GLU = 4 };
@@ -21,6 +23,7 @@ struct EpiArgs {
   int ldx = 0;
   const uint8_t* rowmask = nullptr;  // RESID: per-row 0/1 multiplier (null = all 1)
   int d = 0;                     // QKV: model dim
+  int dk = 64;                   // QKV: head dim (KV stream rows are [H][K dk | V dk])
   int col_group = 0;             // bf16 256-tile walk: column tiles per group (0 = all; tiles ordered group, row, col)
   int store_mode = 0;            // bf16 epilogue stores: 0 = plain, 1 = sc1 (drop the line from L2), 2 = nt
 };
@@ -59,10 +62,13 @@ int layernorm2_f32(float* x, const ResidAdd<T>& ra, int M, int d, const float* w
 // chunk attention (attention.hip)
 template <typename T>
 int chunk_attention(const T* q, const T* kv, int kv_rows, const T* P, int p_rows, const float* pos_u,
-                    const float* pos_v, const int32_t* desc, int nblk, int H, T* out, hipStream_t st,
-                    int p_ld = 0);   // P row stride (elements; 0 = H * 64)
+                    const float* pos_v, const int32_t* desc, int nblk, int H, int dk, T* out, hipStream_t st,
+                    int p_ld = 0);   // P row stride (elements; 0 = H * dk); dk = 64 or 128
 
-// masked-batch ring kernel (bf16); -1 = shape not eligible
+// KV-stream column of K (which = 0) / V (which = 1) column cc (< d) of the QKV projection
+CFM_HD_INLINE int qkv_kv_col(int cc, int which, int dk) { return (cc / dk) * 2 * dk + which * dk + (cc & (dk - 1)); }
+
+// masked-batch ring kernel (bf16, head dim 64); -1 = shape not eligible
 int chunk_attention_masked_bf16(const bf16* q, const bf16* kv, int kv_rows, const bf16* P, int p_rows,
                                 const float* pos_u, const float* pos_v, const int32_t* desc, int n_chunks, int H,
                                 int C, int W, bf16* out, hipStream_t st, int diag = 0, int p_ld = 0);

@@ -178,8 +178,7 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const T* __restrict__ A, i
               reinterpret_cast<T*>(ep.out)[(size_t)row * d + col] = from_f32<T>(v);
             } else {
               const int c2 = col - d, which = c2 >= d ? 1 : 0, cc = c2 - which * d;
-              const int h = cc >> 6, dd = cc & 63;
-              reinterpret_cast<T*>(ep.out2)[(size_t)(row + ep.row_off) * (2 * d) + h * 128 + which * 64 + dd] =
+              reinterpret_cast<T*>(ep.out2)[(size_t)(row + ep.row_off) * (2 * d) + qkv_kv_col(cc, which, ep.dk)] =
                   from_f32<T>(v);
             }
           }

@@ -560,8 +560,7 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_spread_kernel(const bf16* __
           ld = d;
         } else {
           const int c2 = n - d, which = c2 >= d ? 1 : 0, cc = c2 - which * d;
-          base = reinterpret_cast<bf16*>(ep.out2) + (size_t)(ep.row_off + tm * 256) * 2 * d + (cc >> 6) * 128 +
-                 which * 64 + (cc & 63);
+          base = reinterpret_cast<bf16*>(ep.out2) + (size_t)(ep.row_off + tm * 256) * 2 * d + qkv_kv_col(cc, which, ep.dk);
           ld = 2 * d;
         }
       } else {

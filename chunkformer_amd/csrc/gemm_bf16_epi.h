@@ -107,7 +107,7 @@ CFM_DEV void wave_epilogue(f32x4 (&acc)[4][MB], int m0, int nw, int g, int M, co
   } else {   // EPI_STORE / EPI_QKV: bf16 out, pairs (0,1) and (2,3)
 #pragma unroll
     for (int p = 0; p < 2; ++p) {
-      const int n = nw + 32 * p;   // a 32-column span never crosses a 64-column head group
+      const int n = nw + 32 * p;   // a 32-column span never crosses a head group (dk = 64 or 128)
       bf16* base;
       size_t ld;
       if constexpr (EPI == EPI_QKV) {
@@ -117,7 +117,7 @@ CFM_DEV void wave_epilogue(f32x4 (&acc)[4][MB], int m0, int nw, int g, int M, co
           ld = d;
         } else {
           const int c2 = n - d, which = c2 >= d ? 1 : 0, cc = c2 - which * d;
-          base = reinterpret_cast<bf16*>(ep.out2) + (size_t)ep.row_off * 2 * d + (cc >> 6) * 128 + which * 64 + (cc & 63);
+          base = reinterpret_cast<bf16*>(ep.out2) + (size_t)ep.row_off * 2 * d + qkv_kv_col(cc, which, ep.dk);
           ld = 2 * (size_t)d;
         }
       } else {

@@ -171,7 +171,7 @@ __global__ __launch_bounds__(256, 1) void gemm_wsp_kernel(const bf16* __restrict
         old[p] = d;
       } else {
         const int c2 = n - d, which = c2 >= d ? 1 : 0, cc = c2 - which * d;
-        obase[p] = reinterpret_cast<bf16*>(ep.out2) + (size_t)ep.row_off * 2 * d + (cc >> 6) * 128 + which * 64 + (cc & 63);
+        obase[p] = reinterpret_cast<bf16*>(ep.out2) + (size_t)ep.row_off * 2 * d + qkv_kv_col(cc, which, ep.dk);
         old[p] = 2 * d;
       }
     } else if constexpr (EPI == EPI_GLU) {

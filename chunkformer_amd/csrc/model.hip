@@ -100,6 +100,7 @@ struct cfm_model {
   std::vector<cfm::LayerW> layers;
   cfm::FrontW fe;
   int max_layers = -1;
+  int fe_group_windows = 0;         // "fe_group_windows": cap on front-end windows per group (0 = by memory)
   bool use_ring_attention = true;
   bool use_fused_ffn = false;       // "fused_ffn": bf16 d=512 FFN as one kernel (ffn.hip) instead of two GEMMs (A/B: 16% slower)
   int attn_diag = 0;                // "attn_diag": 1 = ring kernel without compute (staging only)   // "ring_attention" option (A/B against the generic kernel)
@@ -163,14 +164,14 @@ namespace cfm {
 
 template <typename T>
 struct ModelT : public cfm_model {
-  // front-end window group size: bounds the [G, T2, 19, d] intermediates
+  // front-end window group size: bounds the [G, T2, 19, d] intermediates to 768 MiB each (measured:
+  // 48-192 MiB groups are slower, 1.5-8 GiB equal); the "fe_group_windows" option caps it further
   int fe_group(const int32_t* h) const {
     const int W = h[PH_W];
     const int T1 = (W - 3) / 2 + 1, T2 = (T1 - 3) / 2 + 1;
     const size_t per = (size_t)T2 * 19 * cfg.d_model * sizeof(T);
-    static size_t cap = 0;   // 768 MiB per intermediate buffer (CFM_FE_CAP_MB: experiments)
-    if (!cap) { const char* e = getenv("CFM_FE_CAP_MB"); cap = (size_t)(e ? atoi(e) : 768) << 20; }
-    int g = (int)std::max<size_t>(1, cap / per);
+    int g = (int)std::max<size_t>(1, ((size_t)768 << 20) / per);
+    if (fe_group_windows > 0) g = std::min(g, fe_group_windows);
     return std::min(g, h[PH_NWIN]);
   }
 
@@ -222,7 +223,7 @@ struct ModelT : public cfm_model {
   cfm_status encode(const float* feats, const int32_t* plan_dev, const int32_t* hh, const float* aci, const float* cci,
                     int trunc, float* aco, float* cco, float* out, void* ws, size_t wsb,
                     hipStream_t st) const override {
-    const int d = cfg.d_model, ff = cfg.ffn_dim, H = cfg.n_heads;
+    const int d = cfg.d_model, ff = cfg.ffn_dim, H = cfg.n_heads, dk = d / H;
     const float eps = cfg.norm_eps;
     const int rows = hh[PH_ROWS], C = hh[PH_C], L = hh[PH_L];
     const int nwin = hh[PH_NWIN], Wn = hh[PH_W], tout = hh[PH_TOUT];
@@ -311,7 +312,7 @@ struct ModelT : public cfm_model {
       { ResidAdd<T> r = resid(w.y, 0.5f, nullptr); r.defer = true;
         PROF(PC_LN, layernorm<T>(w.x, r, rows, d, Lw.ln_mha_w, Lw.ln_mha_b, eps, w.h, nullptr, st)); }
       if (aci) PROF(PC_CACHE, att_cache_in<T>(aci + (size_t)l * L * 2 * d, L, 2 * d, w.kv, st));
-      { EpiArgs e; e.bias = Lw.b_qkv; e.out = w.q; e.out2 = w.kv; e.row_off = kvoff; e.d = d;
+      { EpiArgs e; e.bias = Lw.b_qkv; e.out = w.q; e.out2 = w.kv; e.row_off = kvoff; e.d = d; e.dk = dk;
         PROF(PC_QKV, gemm<T>(EPI_QKV, ACT_NONE, w.h, d, (const T*)Lw.qkv, d, rows, 3 * d, d, e, st)); }
       if (aci && aco) PROF(PC_CACHE, att_cache_out<T>(w.kv, cache_start, L, 2 * d, aco + (size_t)l * L * 2 * d, st));
       {
@@ -319,13 +320,13 @@ struct ModelT : public cfm_model {
         hipEvent_t pb_;
         prof_begin(PC_ATTN, st, &pb_);
         if constexpr (sizeof(T) == 2) {
-          if (masked && use_ring_attention)
+          if (masked && use_ring_attention && dk == 64)
             r = chunk_attention_masked_bf16(w.q, w.kv, kv_rows, w.P + (size_t)l * d, p_rows, Lw.pu, Lw.pv,
                                             attd, natt, H, C, hh[PH_L] + C + hh[PH_R], w.ao, st, attn_diag, p_ld);
         }
         if (r == -1)
           r = chunk_attention<T>(w.q, w.kv, kv_rows, w.P + (size_t)l * d, p_rows, Lw.pu, Lw.pv, attd, natt,
-                                 H, w.ao, st, p_ld);
+                                 H, dk, w.ao, st, p_ld);
         KCHK(r);
         prof_end(PC_ATTN, st, pb_);
       }
@@ -536,8 +537,8 @@ static cfm_status build_model(const cfm_config& cfg, const HostW& hw, int device
       put_T(vec(p + "self_attn.linear_pos.weight", (int64_t)d * d), &Lw.pos);
       put_T(vec(p + "self_attn.linear_out.weight", (int64_t)d * d), &Lw.wo);
       put_f32(hw.get(p + "self_attn.linear_out.bias", d), d, &Lw.b_o);
-      put_f32(hw.get(p + "self_attn.pos_bias_u", (int64_t)H * 64), (size_t)H * 64, &Lw.pu);
-      put_f32(hw.get(p + "self_attn.pos_bias_v", (int64_t)H * 64), (size_t)H * 64, &Lw.pv);
+      put_f32(hw.get(p + "self_attn.pos_bias_u", (int64_t)d), (size_t)d, &Lw.pu);   // [H, dk]
+      put_f32(hw.get(p + "self_attn.pos_bias_v", (int64_t)d), (size_t)d, &Lw.pv);
       {   // pointwise_conv1 rows interleaved per 16: [a(16t..16t+15) | gate(d+16t..)] for the fused GLU
         const float* s = hw.get(p + "conv_module.pointwise_conv1.weight", (int64_t)2 * d * d);
         const float* sb = hw.get(p + "conv_module.pointwise_conv1.bias", 2 * d);
@@ -609,7 +610,8 @@ cfm_status cfm_model_create(const cfm_config* cfg, const cfm_tensor_view* weight
   if (cfg->input_dim != 80) return set_error(CFM_ERR_ASSERT, "front-end kernel supports input_dim == 80");
   if (cfg->d_model != 128 && cfg->d_model != 256 && cfg->d_model != 512)
     return set_error(CFM_ERR_ASSERT, "d_model must be 128, 256 or 512");
-  if (cfg->n_heads <= 0 || cfg->d_model != 64 * cfg->n_heads) return set_error(CFM_ERR_ASSERT, "head_dim must be 64");
+  if (cfg->n_heads <= 0 || (cfg->d_model != 64 * cfg->n_heads && cfg->d_model != 128 * cfg->n_heads))
+    return set_error(CFM_ERR_ASSERT, "head_dim (d_model / attention_heads) must be 64 or 128");
   if (cfg->ffn_dim % 128) return set_error(CFM_ERR_ASSERT, "ffn_dim must be a multiple of 128");
   if (cfg->kernel_size != 15) return set_error(CFM_ERR_ASSERT, "cnn_module_kernel must be 15");
   if (cfg->num_blocks <= 0 || cfg->vocab < 0) return set_error(CFM_ERR_VALUE, "bad num_blocks / vocab");
@@ -625,6 +627,7 @@ void cfm_model_destroy(cfm_model* m) { delete m; }
 cfm_status cfm_model_set_option(cfm_model* m, const char* key, int64_t value) {
   if (!m || !key) return set_error(CFM_ERR_VALUE, "null argument");
   if (!std::strcmp(key, "max_layers")) { m->max_layers = (int)value; return CFM_OK; }
+  if (!std::strcmp(key, "fe_group_windows")) { m->fe_group_windows = (int)std::max<int64_t>(0, value); return CFM_OK; }
   if (!std::strcmp(key, "profile")) { m->prof_mask = (uint32_t)value; return CFM_OK; }
   if (!std::strcmp(key, "ring_attention")) { m->use_ring_attention = value != 0; return CFM_OK; }
   if (!std::strcmp(key, "fused_ffn")) { m->use_fused_ffn = value != 0; return CFM_OK; }

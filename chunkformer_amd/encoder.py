@@ -15,6 +15,7 @@ torch's current stream.
 from __future__ import annotations
 
 import ctypes
+import weakref
 from typing import Dict, List, Optional, Tuple
 
 import torch
@@ -63,12 +64,9 @@ class ChunkFormerEncoder:
                                              ctypes.byref(h)))
         self._h = h
         self._ws: Optional[torch.Tensor] = None
-
-    def __del__(self):
-        h = getattr(self, "_h", None)
-        if h is not None and h.value:
-            _lib.cfm_model_destroy(h)
-            self._h = None
+        # destroy the native handle when this object is collected or at interpreter exit (a finalizer
+        # holds its own reference to the bound ctypes function, unlike __del__ at shutdown)
+        self._finalizer = weakref.finalize(self, _lib.cfm_model_destroy, ctypes.c_void_p(h.value))
 
     def output_size(self) -> int:
         return self._output_size

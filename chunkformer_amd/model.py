@@ -180,33 +180,50 @@ class ChunkFormerModel:
     @classmethod
     def from_pretrained(cls, path: str, dtype: str = "bf16", device=None) -> "ChunkFormerModel":
         """Local checkpoint directory in the reference layout (chunkformer_model.py:107-200):
-        config.yaml (yaml.safe_load), global_cmvn (JSON stats, utils/cmvn.py:23-45),
-        pytorch_model.{bin,pt,ckpt} (torch.load weights_only=True) or model.safetensors,
-        vocab.txt ("token id" per line, file_utils.py:62-69)."""
+
+        * config.yaml (yaml.safe_load): encoder_conf, input_dim, output_dim, cmvn / cmvn_conf;
+        * global_cmvn: JSON {mean_stat, var_stat, frame_num} or kaldi text stats
+          (cmvn_conf.is_json_cmvn, utils/cmvn.py:23-98), used when config `cmvn: global_cmvn`
+          (init_model.py:63-69);
+        * pytorch_model.{bin,pt,ckpt} (torch.load weights_only=True: plain tensors only), loaded
+          like load_checkpoint(strict=False) (checkpoint.py:26-41): keys present in the
+          checkpoint win, so its `encoder.global_cmvn.{mean,istd}` buffers override the stats file
+          exactly as load_state_dict does in the reference; model.safetensors is also accepted;
+        * vocab.txt ("token id" per line, file_utils.py:62-69) -> char_dict for text output.
+        There is no hub access: `path` must be a local directory."""
         import yaml
         if not os.path.isdir(path):
             raise FileNotFoundError(f"{path}: only local checkpoint directories are supported (no hub access)")
-        with open(os.path.join(path, "config.yaml")) as f:
+        cfg_path = os.path.join(path, "config.yaml")
+        if not os.path.exists(cfg_path):
+            raise ValueError(f"No config found in {path}")
+        with open(cfg_path) as f:
             conf = yaml.safe_load(f)
-        sd: Dict[str, torch.Tensor] = {}
         st = os.path.join(path, "model.safetensors")
         if os.path.exists(st):
             from safetensors.torch import load_file
-            sd = dict(load_file(st))
+            sd: Dict[str, torch.Tensor] = dict(load_file(st))
         else:
-            for nm in ("pytorch_model.bin", "pytorch_model.pt", "pytorch_model.ckpt"):
+            cands = ["pytorch_model.bin", "pytorch_model.pt", "pytorch_model.ckpt"]
+            for nm in cands:
                 p = os.path.join(path, nm)
                 if os.path.exists(p):
                     sd = torch.load(p, map_location="cpu", weights_only=True)
                     break
             else:
-                raise FileNotFoundError(f"no checkpoint in {path}")
+                raise ValueError(f"No checkpoint found in {path}. Expected one of: {cands}")
         cmvn_path = os.path.join(path, "global_cmvn")
-        has_cmvn = os.path.exists(cmvn_path)
+        has_cmvn = conf.get("cmvn", None) == "global_cmvn"
         if has_cmvn:
-            mean, istd = load_json_cmvn(cmvn_path)
-            sd["encoder.global_cmvn.mean"] = torch.tensor(mean, dtype=torch.float32)
-            sd["encoder.global_cmvn.istd"] = torch.tensor(istd, dtype=torch.float32)
+            if not os.path.exists(cmvn_path):
+                raise FileNotFoundError(f"config asks for global_cmvn but {cmvn_path} is missing")
+            is_json = bool((conf.get("cmvn_conf") or {}).get("is_json_cmvn", True))
+            mean, istd = load_json_cmvn(cmvn_path) if is_json else load_kaldi_cmvn(cmvn_path)
+            sd.setdefault("encoder.global_cmvn.mean", torch.tensor(mean, dtype=torch.float64).float())
+            sd.setdefault("encoder.global_cmvn.istd", torch.tensor(istd, dtype=torch.float64).float())
+        else:   # no GlobalCMVN module: checkpoint buffers would be unexpected keys (ignored)
+            sd.pop("encoder.global_cmvn.mean", None)
+            sd.pop("encoder.global_cmvn.istd", None)
         vocab = int(conf.get("output_dim", sd["ctc.ctc_lo.weight"].shape[0] if "ctc.ctc_lo.weight" in sd else 0))
         cfg = EncoderConfig.from_encoder_conf(conf.get("encoder_conf", {}), input_dim=int(conf.get("input_dim", 80)),
                                               output_dim=vocab, cmvn=has_cmvn)
@@ -269,6 +286,9 @@ class ChunkFormerModel:
                 ids.append(tok)
             if eo is not None:
                 outs.append(eo)
+        # the caches carried out of the last segment (r_att_cache / r_cnn_cache of its
+        # forward_parallel_chunk call, chunkformer_model.py:407-417)
+        self.last_endless_caches = (runner.att[runner.cur], runner.cnn[runner.cur])
         tokens = torch.cat(ids).long().reshape(1, -1, 1) if ids else None
         if self.char_dict is not None and tokens is not None:
             res = get_output_with_timestamps(tokens, self.char_dict, max_silence_duration)[0]
@@ -304,14 +324,37 @@ class ChunkFormerModel:
         return decodes
 
 
+def _cmvn_from_stats(mean_stat, var_stat, count):
+    mean = [m / count for m in mean_stat]
+    istd = []
+    for m, v in zip(mean, var_stat):
+        var = v / count - m * m
+        if var < 1.0e-20:
+            var = 1.0e-20
+        istd.append(1.0 / math.sqrt(var))
+    return mean, istd
+
+
 def load_json_cmvn(path: str):
     """utils/cmvn.py:23-45: JSON {mean_stat, var_stat, frame_num} -> (mean, istd)."""
     with open(path) as f:
         st = json.load(f)
-    cnt = st["frame_num"]
-    mean = [m / cnt for m in st["mean_stat"]]
-    istd = []
-    for m, v in zip(mean, st["var_stat"]):
-        var = max(v / cnt - m * m, 1.0e-20)
-        istd.append(1.0 / math.sqrt(var))
-    return mean, istd
+    return _cmvn_from_stats(st["mean_stat"], st["var_stat"], st["frame_num"])
+
+
+def load_kaldi_cmvn(path: str):
+    """utils/cmvn.py:48-90: kaldi text stats `[ m_1 .. m_F count v_1 .. v_F 0 ]` -> (mean, istd);
+    the binary kaldi form is rejected like the reference."""
+    with open(path, "r") as f:
+        if f.read(2) == "\0B":
+            raise ValueError("kaldi cmvn binary file is not supported; recompute it with "
+                             "compute-cmvn-stats --binary=false")
+        f.seek(0)
+        arr = f.read().split()
+    if not (arr[0] == "[" and arr[-2] == "0" and arr[-1] == "]"):
+        raise AssertionError(f"{path}: not a kaldi text cmvn file")
+    F = (len(arr) - 4) // 2
+    means = [float(a) for a in arr[1: F + 1]]
+    count = float(arr[F + 1])
+    var = [float(a) for a in arr[F + 2: 2 * F + 2]]
+    return _cmvn_from_stats(means, var, count)

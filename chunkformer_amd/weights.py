@@ -112,3 +112,20 @@ def synthetic_features(lens, seed: int):
     (BASELINE.md §3 synthetic inputs)."""
     g = torch.Generator().manual_seed(seed)
     return [torch.randn(int(t), 80, generator=g) for t in lens]
+
+
+def synthetic_vocab(V: int) -> Dict[int, str]:
+    """Deterministic `vocab.txt` stand-in (no real vocabulary is reachable offline): id 0 is
+    <blank>, id 1 <unk>, the rest short letter strings, every 5th a word start ('▁' prefix, turned
+    into a space by class2str, model_utils.py:135-139)."""
+    out = {0: "<blank>", 1: "<unk>"}
+    letters = "abcdefghijklmnopqrstuvwxyz"
+    for i in range(2, V):
+        s, n = "", i
+        while True:
+            s = letters[n % 26] + s
+            n //= 26
+            if n == 0:
+                break
+        out[i] = ("▁" + s) if i % 5 == 0 else s
+    return out

@@ -33,8 +33,8 @@ from chunkformer.modules.cmvn import GlobalCMVN  # noqa: E402
 from chunkformer.modules.ctc import CTC  # noqa: E402
 from chunkformer.modules.encoder import ChunkFormerEncoder  # noqa: E402
 
-from chunkformer_amd.config import LARGE, SMALL, EncoderConfig  # noqa: E402
-from chunkformer_amd.weights import synthetic_features, synthetic_state_dict  # noqa: E402
+from chunkformer_amd.config import LARGE, LARGE_4H, SMALL, EncoderConfig  # noqa: E402
+from chunkformer_amd.weights import synthetic_features, synthetic_state_dict, synthetic_vocab  # noqa: E402
 
 torch.set_num_threads(8)
 
@@ -199,9 +199,11 @@ def gen_small(path, cfg=SMALL, seed=1):
 
 
 def gen_large(path, seed=0):
+    """chunkformer-large, 12 layers: a 30 s utterance (configs[0]'s shape, 3000 frames) next to two
+    shorter ones in one masked batch (C=64, L=R=128), plus CTC ids and top-2 margins."""
     cfg = LARGE
     enc, ctc, sd = build_reference(cfg, seed)
-    lens = [1234, 600]
+    lens = [3000, 1234, 600]
     xs = feats(lens, 5)
     with torch.no_grad():
         r = enc.forward_parallel_chunk(xs, torch.tensor(lens), 64, 128, 128)
@@ -213,12 +215,114 @@ def gen_large(path, seed=0):
                         top2=top2.numpy(), lse_row0=logp[0, 0].numpy())
 
 
+def gen_large_4h(path, seed=0):
+    """d=512 with 4 heads (head_dim 128), the family of the reference's large vie recipe."""
+    cfg = LARGE_4H
+    enc, ctc, sd = build_reference(cfg, seed)
+    lens = [1234, 600]
+    xs = feats(lens, 6)
+    with torch.no_grad():
+        r = enc.forward_parallel_chunk(xs, torch.tensor(lens), 64, 128, 128)
+        logp = ctc.log_softmax(r[0])
+        # padded chunked path (encode()) on the same utterances
+        xp = torch.zeros(len(lens), max(lens), 80)
+        for i, t in enumerate(xs):
+            xp[i, : t.shape[0]] = t
+        y, masks = enc.forward_encoder(xp, torch.tensor(lens), 64, 128, 128)
+    top2 = torch.topk(logp, 2, dim=-1).values
+    np.savez_compressed(path, sd_digest=sd_digest(sd), seed=np.array(seed), lens=np.array(lens, np.int32),
+                        feat_seed=np.array(6), out=r[0].numpy(), outlens=r[1].numpy(),
+                        nchunks=np.array(r[2], np.int32), ids=logp.argmax(-1).numpy().astype(np.int32),
+                        top2=top2.numpy(), pc_out=y.numpy(), pc_mask=masks.numpy())
+
+
+ENDLESS_LAYERS = [0, 6, 11]   # att_cache layers stored (the full [12,128,8,128] stack is 6 MB)
+
+
+def gen_large_endless(path, seed=0):
+    """configs[3] geometry on chunkformer-large: C=64, L=R=128, 12 layers, tbd=20 -> 4 segments of
+    <= 12,807 frames with the att/cnn caches and offset carried; final caches recorded."""
+    cfg = LARGE
+    enc, ctc, sd = build_reference(cfg, seed)
+    x = feats([13500], 12)[0]
+    with torch.no_grad():
+        eo, ids, ac, cc, nseg = endless_reference(enc, ctc, x, 64, 128, 128, tbd=20)
+    assert nseg >= 3, nseg
+    np.savez_compressed(path, sd_digest=sd_digest(sd), seed=np.array(seed), feat_seed=np.array(12),
+                        T=np.array(13500), clrt=np.array([64, 128, 128, 20], np.int32), nseg=np.array(nseg),
+                        out=eo.numpy(), ids=ids.numpy().astype(np.int32),
+                        att_layers=np.array(ENDLESS_LAYERS, np.int32),
+                        att=ac[ENDLESS_LAYERS].numpy(), cnn=cc.numpy())
+
+
+def gen_large_full(path, seed=0):
+    """configs[4] geometry on chunkformer-large: full attention (chunk_size 0 -> T'), padded batch of a
+    30 s utterance and a 21 s one (key padding mask), 12 layers."""
+    cfg = LARGE
+    enc, _, sd = build_reference(cfg, seed)
+    lens = [3000, 2100]
+    xs = feats(lens, 13)
+    xp = torch.zeros(len(lens), max(lens), 80)
+    for i, t in enumerate(xs):
+        xp[i, : t.shape[0]] = t
+    with torch.no_grad():
+        y, masks = enc.forward_encoder(xp, torch.tensor(lens), 0, 0, 0)
+    np.savez_compressed(path, sd_digest=sd_digest(sd), seed=np.array(seed), feat_seed=np.array(13),
+                        lens=np.array(lens, np.int32), out=y.numpy(), mask=masks.numpy())
+
+
+def gen_text(path):
+    """Text post-processing of the reference (utils/model_utils.py: get_output 164-171,
+    get_output_with_timestamps 174-221) on (a) seeded id streams with long blank runs and repeats,
+    (b) the CTC ids of large_4h.npz per utterance (the checkpoint-loader test decodes them);
+    vocabulary: chunkformer_amd.weights.synthetic_vocab.  model_utils imports torchaudio.functional
+    at module level (unused by these functions): an empty stub module stands in for it."""
+    import json
+    ta = types.ModuleType("torchaudio")
+    taf = types.ModuleType("torchaudio.functional")
+    ta.functional = taf
+    sys.modules.setdefault("torchaudio", ta)
+    sys.modules.setdefault("torchaudio.functional", taf)
+    from chunkformer.utils import model_utils as mu
+    V = 5000
+    cd = synthetic_vocab(V)
+    rng = np.random.default_rng(7)
+    streams = []
+    for n in (1, 7, 40, 150, 400, 999):
+        ids, t = [], 0
+        while len(ids) < n:
+            if rng.random() < 0.55:
+                ids += [0] * int(rng.integers(1, 14))
+            else:
+                ids += [int(rng.integers(1, V))] * int(rng.integers(1, 4))
+        streams.append(ids[:n])
+    out = {"V": V, "streams": streams,
+           "get_output": mu.get_output(streams, cd, "asr_model"),
+           "timestamps": {str(ms): mu.get_output_with_timestamps([torch.tensor(s).reshape(-1, 1) for s in streams],
+                                                                 cd, "asr_model", ms)
+                          for ms in (0.5, 0.24, 1.0)}}
+    g = np.load(os.path.join(HERE, "large_4h.npz"))
+    starts = np.cumsum([0] + g["nchunks"].tolist())
+    hyps = [g["ids"][starts[u]: starts[u + 1]].reshape(-1)[: int(n)].tolist() for u, n in enumerate(g["outlens"])]
+    out["large_4h_decode"] = mu.get_output(hyps, cd, "asr_model")
+    with open(path, "w", encoding="utf8") as f:
+        json.dump(out, f, ensure_ascii=False)
+
+
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["masks", "small", "large"]
+    which = sys.argv[1:] or ["masks", "small", "large", "large_4h", "large_endless", "large_full", "text"]
     if "masks" in which:
         gen_masks(os.path.join(HERE, "masks.npz"))
     if "small" in which:
         gen_small(os.path.join(HERE, "small.npz"))
     if "large" in which:
         gen_large(os.path.join(HERE, "large.npz"))
+    if "large_4h" in which:
+        gen_large_4h(os.path.join(HERE, "large_4h.npz"))
+    if "large_endless" in which:
+        gen_large_endless(os.path.join(HERE, "large_endless.npz"))
+    if "text" in which:
+        gen_text(os.path.join(HERE, "text.json"))
+    if "large_full" in which:
+        gen_large_full(os.path.join(HERE, "large_full.npz"))
     print("ok", which)

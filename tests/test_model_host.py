@@ -1,7 +1,10 @@
 """Host logic of the ChunkFormerModel mirror (chunkformer_amd/model.py) -- no GPU:
 endless_decode segment schedule, batch_decode budget grouping, CTC text helpers."""
+import os
+
 import numpy as np
 import pytest
+import torch
 
 from chunkformer_amd.model import (budget_groups, endless_segments, get_output, get_output_with_timestamps,
                                    milliseconds_to_hhmmssms, remove_duplicates_and_blank, load_json_cmvn)
@@ -83,3 +86,36 @@ def test_json_cmvn(tmp_path):
     mean, istd = load_json_cmvn(str(p))
     assert mean == [1.0, 2.0]
     assert istd == pytest.approx([1 / np.sqrt(3.0), 1 / np.sqrt(6.0)])
+
+
+def test_text_helpers_match_reference_golden(golden_dir):
+    """get_output / get_output_with_timestamps against the reference's own model_utils run on the
+    same id streams (tests/golden/text.json, written by gen_golden.py)."""
+    import json
+
+    from chunkformer_amd.model import get_output, get_output_with_timestamps
+    from chunkformer_amd.weights import synthetic_vocab
+    with open(os.path.join(golden_dir, "text.json"), encoding="utf8") as f:
+        g = json.load(f)
+    cd = synthetic_vocab(int(g["V"]))
+    assert get_output(g["streams"], cd) == g["get_output"]
+    for ms, exp in g["timestamps"].items():
+        got = get_output_with_timestamps([torch.tensor(s).reshape(-1, 1) for s in g["streams"]], cd, float(ms))
+        assert got == exp, ms
+
+
+def test_cmvn_loaders_agree(tmp_path):
+    """JSON and kaldi-text global_cmvn stats give the same (mean, istd) (utils/cmvn.py:23-98)."""
+    import json
+
+    from chunkformer_amd.model import load_json_cmvn, load_kaldi_cmvn
+    rng = np.random.default_rng(3)
+    cnt = 12345.0
+    m = rng.normal(size=80) * cnt
+    v = (rng.random(80) + 0.5) * cnt + m * m / cnt
+    (tmp_path / "j").write_text(json.dumps({"mean_stat": m.tolist(), "var_stat": v.tolist(), "frame_num": cnt}))
+    (tmp_path / "k").write_text("[ " + " ".join(repr(float(x)) for x in m) + f" {cnt!r}\n"
+                                + " ".join(repr(float(x)) for x in v) + " 0 ]\n")
+    a, b = load_json_cmvn(str(tmp_path / "j")), load_kaldi_cmvn(str(tmp_path / "k"))
+    np.testing.assert_allclose(a[0], b[0], rtol=1e-12)
+    np.testing.assert_allclose(a[1], b[1], rtol=1e-12)

@@ -99,3 +99,68 @@ def test_large_matches_reference(golden_dir):
     ids = logp.argmax(-1).numpy()
     sure = margin > 1e-4
     np.testing.assert_array_equal(ids[sure], g["ids"][sure])
+
+
+def test_large_4h_matches_reference(golden_dir):
+    """d=512 with 4 heads (head_dim 128): masked batch and the padded chunked path."""
+    from chunkformer_amd.config import LARGE_4H
+    g = _load(golden_dir, "large_4h.npz")
+    sd = synthetic_state_dict(LARGE_4H, int(g["seed"]))
+    lens = g["lens"].tolist()
+    xs = synthetic_features(lens, int(g["feat_seed"]))
+    out, _, nch, _, _, _ = ref.forward_parallel_chunk(sd, LARGE_4H, xs, lens, 64, 128, 128)
+    assert nch == g["nchunks"].tolist()
+    np.testing.assert_allclose(out.numpy(), g["out"], atol=1e-4, rtol=0)
+    xp = torch.zeros(len(lens), max(lens), 80)
+    for i, t in enumerate(xs):
+        xp[i, : t.shape[0]] = t
+    y, masks = ref.forward_encoder(sd, LARGE_4H, xp, lens, 64, 128, 128)
+    np.testing.assert_array_equal(masks.numpy(), g["pc_mask"])
+    np.testing.assert_allclose(y.numpy(), g["pc_out"], atol=1e-4, rtol=0)
+
+
+def oracle_endless(sd, cfg, x, C, L, R, tbd):
+    """endless_decode's segment loop (chunkformer_model.py:344-435) driven on the oracle, with the
+    host segment schedule of chunkformer_amd.model.endless_segments."""
+    from chunkformer_amd.model import endless_segments
+    trunc, segs = endless_segments(x.shape[0], C, L, R, tbd, cfg.num_blocks, cfg.kernel_size)
+    ac = torch.zeros(cfg.num_blocks, L, cfg.n_heads, 2 * cfg.head_dim)
+    cc = torch.zeros(cfg.num_blocks, cfg.d_model, cfg.conv_lorder)
+    offset, outs = 0, []
+    for start, stop, keep_trunc, _ in segs:
+        seg = x[start:stop]
+        out, el, _, ac, cc, _ = ref.forward_parallel_chunk(sd, cfg, [seg], [seg.shape[0]], C, L, R, ac, cc, trunc,
+                                                           [offset])
+        eo = out.reshape(-1, cfg.d_model)[: int(el[0])]
+        if keep_trunc:
+            eo = eo[:trunc]
+        offset += eo.shape[0]
+        outs.append(eo)
+    return torch.cat(outs), ac, cc, len(segs)
+
+
+def test_large_endless_matches_reference(golden_dir):
+    """configs[3] geometry (C=64, L=R=128, 12 layers), >= 3 segments with caches carried."""
+    g = _load(golden_dir, "large_endless.npz")
+    sd = synthetic_state_dict(LARGE, int(g["seed"]))
+    C, L, R, tbd = (int(v) for v in g["clrt"])
+    x = synthetic_features([int(g["T"])], int(g["feat_seed"]))[0]
+    eo, ac, cc, nseg = oracle_endless(sd, LARGE, x, C, L, R, tbd)
+    assert nseg == int(g["nseg"]) >= 3
+    np.testing.assert_allclose(eo.numpy(), g["out"], atol=1e-4, rtol=0)
+    np.testing.assert_allclose(ac[g["att_layers"]].numpy(), g["att"], atol=1e-4, rtol=0)
+    np.testing.assert_allclose(cc.numpy(), g["cnn"], atol=1e-4, rtol=0)
+
+
+def test_large_full_attention_matches_reference(golden_dir):
+    """configs[4] geometry: full attention over a padded 30 s + 21 s batch, 12 layers."""
+    g = _load(golden_dir, "large_full.npz")
+    sd = synthetic_state_dict(LARGE, int(g["seed"]))
+    lens = g["lens"].tolist()
+    xs = synthetic_features(lens, int(g["feat_seed"]))
+    xp = torch.zeros(len(lens), max(lens), 80)
+    for i, t in enumerate(xs):
+        xp[i, : t.shape[0]] = t
+    y, masks = ref.forward_encoder(sd, LARGE, xp, lens, 0, 0, 0)
+    np.testing.assert_array_equal(masks.numpy(), g["mask"])
+    np.testing.assert_allclose(y.numpy(), g["out"], atol=1e-4, rtol=0)
