@@ -68,6 +68,9 @@ cfm_masks_from_plan = _sig("cfm_masks_from_plan", I32, P, P, P, P, P)
 cfm_profile_read = _sig("cfm_profile_read", I32, P, P, P, P, I32)
 cfm_ctc_workspace_bytes = _sig("cfm_ctc_workspace_bytes", SZ, P, I32)
 cfm_ctc_logprobs = _sig("cfm_ctc_logprobs", I32, P, P, I32, P, P, P, SZ, P)
+cfm_ctc_ids_workspace_bytes = _sig("cfm_ctc_ids_workspace_bytes", SZ, P, I32)
+cfm_ctc_ids = _sig("cfm_ctc_ids", I32, P, P, I32, P, P, SZ, P)
+cfm_ctc_collapse = _sig("cfm_ctc_collapse", I32, P, P, P, I32, I32, I32, P, P, P, P, P, P)
 # include/cfm_ops.h
 cfm_op_gemm = _sig("cfm_op_gemm", I32, I32, I32, I32, P, I32, P, I32, I32, I32, I32, P, ctypes.c_float, P, I32, I32, P,
                    I32, P, I32, P, I32, P)
@@ -77,7 +80,7 @@ EXPORTED_OPS = ["cfm_op_gemm", "cfm_op_ffn"]
 EXPORTED = ["cfm_version", "cfm_last_error", "cfm_model_create", "cfm_model_destroy", "cfm_model_set_option",
             "cfm_plan_masked", "cfm_plan_padded", "cfm_workspace_bytes_masked", "cfm_workspace_bytes_padded",
             "cfm_encode_masked", "cfm_encode_padded", "cfm_masks_from_plan", "cfm_profile_read", "cfm_ctc_workspace_bytes",
-            "cfm_ctc_logprobs"]
+            "cfm_ctc_logprobs", "cfm_ctc_ids_workspace_bytes", "cfm_ctc_ids", "cfm_ctc_collapse"]
 
 
 def profile_read(h):

@@ -106,6 +106,13 @@ int cnn_cache_in(const float* cache /*[d][7]*/, int d, int lorder, T* glu, hipSt
 template <typename T>
 int cnn_cache_out(const T* glu, int start_row, int d, int lorder, float* cache, hipStream_t st);
 int masks_from_plan(const int32_t* meta, int n, int C, int L, int R, uint8_t* att, uint8_t* pad, hipStream_t st);
+// CTC head (ctc.hip): ids-only argmax of enc . W^T + b without a logit tensor (bf16 W with rows padded
+// to a multiple of 64, d = 512; -1 = not eligible), and the collapse / silence segmentation of ids
+bool ctc_argmax_eligible(int V, int d);
+int ctc_argmax_bf16(const float* enc, int M, const bf16* W, const float* bias, int V, int d, int32_t* ids,
+                    hipStream_t st);
+int ctc_collapse(const int32_t* ids, const int32_t* row_start, const int32_t* row_len, int B, int blank, int max_sil,
+                 int32_t* tok, int32_t* tok_frame, int32_t* n_tok, int32_t* seg, int32_t* n_seg, hipStream_t st);
 int log_softmax_rows(float* logits, int M, int V, int write_logp, int32_t* ids, hipStream_t st);
 
 }  // namespace cfm

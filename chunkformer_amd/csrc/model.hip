@@ -102,6 +102,7 @@ struct cfm_model {
   int max_layers = -1;
   int fe_group_windows = 0;         // "fe_group_windows": cap on front-end windows per group (0 = by memory)
   bool use_ring_attention = true;
+  bool use_fused_ctc = true;        // "ctc_fused": bf16 ids-only CTC head as one argmax kernel (ctc.hip), no [rows, V] logits
   bool use_fused_ffn = false;       // "fused_ffn": bf16 d=512 FFN as one kernel (ffn.hip) instead of two GEMMs (A/B: 16% slower)
   int attn_diag = 0;                // "attn_diag": 1 = ring kernel without compute (staging only)   // "ring_attention" option (A/B against the generic kernel)
   // profiler: bitmask of PC_* classes to bracket with events on the launch stream
@@ -158,6 +159,8 @@ struct cfm_model {
                          hipStream_t st) const = 0;
   virtual size_t ws_bytes(const int32_t* hdr) const = 0;
   virtual size_t ctc_ws_bytes(int rows) const = 0;
+  // ids-only CTC (logp == nullptr): 0 bytes on the fused argmax path
+  virtual size_t ctc_ids_ws_bytes(int rows) const = 0;
 };
 
 namespace cfm {
@@ -219,6 +222,8 @@ struct ModelT : public cfm_model {
   size_t ctc_ws_bytes(int rows) const override {
     return align_up((size_t)rows * cfg.vocab * sizeof(float)) + align_up((size_t)rows * cfg.d_model * sizeof(T)) + 4096;
   }
+  bool fused_ctc_ok() const { return sizeof(T) == 2 && use_fused_ctc && ctc_argmax_eligible(cfg.vocab, cfg.d_model); }
+  size_t ctc_ids_ws_bytes(int rows) const override { return fused_ctc_ok() ? 0 : ctc_ws_bytes(rows); }
 
   cfm_status encode(const float* feats, const int32_t* plan_dev, const int32_t* hh, const float* aci, const float* cci,
                     int trunc, float* aco, float* cco, float* out, void* ws, size_t wsb,
@@ -360,8 +365,16 @@ struct ModelT : public cfm_model {
   cfm_status ctc(const float* enc, int rows, float* logp, int32_t* ids, void* ws, size_t wsb,
                  hipStream_t st) const override {
     if (!fe.ctc_w) return set_error(CFM_ERR_ASSERT, "model has no CTC head (vocab == 0)");
-    if (wsb < ctc_ws_bytes(rows)) return set_error(CFM_ERR_VALUE, "ctc workspace too small");
     const int d = cfg.d_model, V = cfg.vocab;
+    if constexpr (sizeof(T) == 2) {
+      // ids only: the fused argmax head (ctc.hip) keeps every logit in registers
+      if (!logp && ids && fused_ctc_ok()) {
+        int r;
+        PROF(PC_CTC, (r = ctc_argmax_bf16(enc, rows, (const bf16*)fe.ctc_w, fe.ctc_b, V, d, ids, st)) < 0 ? 0 : r);
+        if (r == 0) return CFM_OK;
+      }
+    }
+    if (wsb < ctc_ws_bytes(rows)) return set_error(CFM_ERR_VALUE, "ctc workspace too small");
     Carver c(ws);
     float* logits = c.take<float>((size_t)rows * V);
     T* a = c.take<T>((size_t)rows * d);
@@ -502,7 +515,10 @@ static cfm_status build_model(const cfm_config& cfg, const HostW& hw, int device
     put_f32(hw.get(E + "after_norm.weight", d), d, &F.an_w);
     put_f32(hw.get(E + "after_norm.bias", d), d, &F.an_b);
     if (V > 0) {
-      put_T(vec("ctc.ctc_lo.weight", (int64_t)V * d), &F.ctc_w);
+      // rows padded with zeros to a multiple of 64 (the fused argmax head streams 64-row tiles)
+      std::vector<float> w = vec("ctc.ctc_lo.weight", (int64_t)V * d);
+      w.resize((size_t)(V + 63) / 64 * 64 * d, 0.f);
+      put_T(w, &F.ctc_w);
       put_f32(hw.get("ctc.ctc_lo.bias", V), V, &F.ctc_b);
     }
     M->layers.resize(nb);
@@ -630,6 +646,7 @@ cfm_status cfm_model_set_option(cfm_model* m, const char* key, int64_t value) {
   if (!std::strcmp(key, "fe_group_windows")) { m->fe_group_windows = (int)std::max<int64_t>(0, value); return CFM_OK; }
   if (!std::strcmp(key, "profile")) { m->prof_mask = (uint32_t)value; return CFM_OK; }
   if (!std::strcmp(key, "ring_attention")) { m->use_ring_attention = value != 0; return CFM_OK; }
+  if (!std::strcmp(key, "ctc_fused")) { m->use_fused_ctc = value != 0; return CFM_OK; }
   if (!std::strcmp(key, "fused_ffn")) { m->use_fused_ffn = value != 0; return CFM_OK; }
   if (!std::strcmp(key, "ffn_variant")) { ffn_set_variant((int)value); return CFM_OK; }
   if (!std::strcmp(key, "gemm_variant")) { gemm_set_variant((int)value); return CFM_OK; }
@@ -745,6 +762,30 @@ cfm_status cfm_ctc_logprobs(const cfm_model* m, const float* enc, int32_t rows, 
   if (rows <= 0) return CFM_OK;
   HIPC(hipSetDevice(m->device));
   return m->ctc(enc, rows, logp, ids, ws, wsb, (hipStream_t)stream);
+}
+
+size_t cfm_ctc_ids_workspace_bytes(const cfm_model* m, int32_t rows) { return m ? m->ctc_ids_ws_bytes(rows) : 0; }
+
+cfm_status cfm_ctc_ids(const cfm_model* m, const float* enc, int32_t rows, int32_t* ids, void* ws, size_t wsb,
+                       cfm_stream stream) {
+  if (!m || !enc || !ids) return set_error(CFM_ERR_VALUE, "null argument");
+  if (rows <= 0) return CFM_OK;
+  HIPC(hipSetDevice(m->device));
+  return m->ctc(enc, rows, nullptr, ids, ws, wsb, (hipStream_t)stream);
+}
+
+cfm_status cfm_ctc_collapse(const int32_t* ids, const int32_t* row_start, const int32_t* row_len, int32_t B,
+                            int32_t blank_id, int32_t max_silence, int32_t* tokens, int32_t* token_frames,
+                            int32_t* n_tokens, int32_t* segments, int32_t* n_segments, cfm_stream stream) {
+  if (B < 0) return set_error(CFM_ERR_VALUE, "B < 0");
+  if (B == 0) return CFM_OK;
+  if (!ids || !row_start || !row_len || !tokens || !token_frames || !n_tokens)
+    return set_error(CFM_ERR_VALUE, "null argument");
+  if (max_silence >= 0 && (!segments || !n_segments))
+    return set_error(CFM_ERR_VALUE, "segmentation needs segments and n_segments");
+  KCHK(ctc_collapse(ids, row_start, row_len, B, blank_id, max_silence, tokens, token_frames, n_tokens, segments,
+                    n_segments, (hipStream_t)stream));
+  return CFM_OK;
 }
 
 }  // extern "C"

@@ -6,7 +6,8 @@ reference; every tensor op of the hot path runs in libcfm.so (HIP, gfx950):
   forward_parallel_chunk  encoder.py:503-681   -> cfm_plan_masked + cfm_encode_masked
   forward_encoder         encoder.py:220-274   -> cfm_plan_padded + cfm_encode_padded
   forward                 encoder.py:461-501   (eval branch: negative sizes -> 0/0/0)
-  ctc_log_softmax/argmax  ctc.py:73-91          -> cfm_ctc_logprobs
+  ctc_log_softmax/argmax  ctc.py:73-91          -> cfm_ctc_logprobs / cfm_ctc_ids (fused argmax)
+  ctc_collapse            model_utils.py:23-58, 174-221 -> cfm_ctc_collapse
 
 Python only moves pointers: it builds the host plan (C++ planner), uploads it,
 allocates outputs/workspace with torch on the current device and launches on
@@ -147,13 +148,25 @@ class ChunkFormerEncoder:
                                           _lib.ptr(aci), _lib.ptr(cci), int(trunc), _lib.ptr(aco), _lib.ptr(cco),
                                           out.data_ptr(), ws.data_ptr(), ws_bytes, self._stream()))
 
+    def ctc_ws_bytes(self, rows: int, want_logp: bool) -> int:
+        """Workspace of the CTC head over `rows` rows: 0 for ids only on the fused argmax head."""
+        if want_logp:
+            return int(_lib.cfm_ctc_workspace_bytes(self._h, rows))
+        return int(_lib.cfm_ctc_ids_workspace_bytes(self._h, rows))
+
     def _ctc_raw(self, enc: torch.Tensor, rows: int, logp, ids, ws) -> None:
-        """cfm_ctc_logprobs over the first `rows` rows of enc [*, d] (graph-capturable)."""
-        nbytes = _lib.cfm_ctc_workspace_bytes(self._h, rows)
-        if ws.numel() < nbytes:
-            raise ValueError(f"CTC workspace {ws.numel()} B < {nbytes} B")
-        _lib.check(_lib.cfm_ctc_logprobs(self._h, enc.data_ptr(), rows, _lib.ptr(logp), _lib.ptr(ids), ws.data_ptr(),
-                                         nbytes, self._stream()))
+        """CTC head over the first `rows` rows of enc [*, d] (graph-capturable): cfm_ctc_logprobs,
+        or the fused ids-only cfm_ctc_ids when no log-probs are asked for."""
+        nbytes = self.ctc_ws_bytes(rows, logp is not None)
+        wsz = 0 if ws is None else ws.numel()
+        if wsz < nbytes:
+            raise ValueError(f"CTC workspace {wsz} B < {nbytes} B")
+        wp = _lib.ptr(ws) if nbytes > 0 else None
+        if logp is None:
+            _lib.check(_lib.cfm_ctc_ids(self._h, enc.data_ptr(), rows, ids.data_ptr(), wp, nbytes, self._stream()))
+        else:
+            _lib.check(_lib.cfm_ctc_logprobs(self._h, enc.data_ptr(), rows, logp.data_ptr(), _lib.ptr(ids), wp,
+                                             nbytes, self._stream()))
 
     @torch.no_grad()
     def masks(self, xs_origin_lens, chunk_size: int, left_context_size: int, right_context_size: int,
@@ -214,10 +227,61 @@ class ChunkFormerEncoder:
         shape = hs.shape[:-1]
         enc = hs.reshape(-1, self.cfg.d_model).to(self.device, torch.float32).contiguous()
         rows = enc.shape[0]
+        if not want_logp and not want_ids:
+            return None, None
         logp = torch.empty(rows, self.cfg.vocab, dtype=torch.float32, device=self.device) if want_logp else None
         ids = torch.empty(rows, dtype=torch.int32, device=self.device) if want_ids else None
-        nbytes = _lib.cfm_ctc_workspace_bytes(self._h, rows)
-        ws = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
-        _lib.check(_lib.cfm_ctc_logprobs(self._h, enc.data_ptr(), rows, _lib.ptr(logp), _lib.ptr(ids), ws.data_ptr(),
-                                         nbytes, self._stream()))
+        nbytes = self.ctc_ws_bytes(rows, want_logp)
+        ws = torch.empty(nbytes, dtype=torch.uint8, device=self.device) if nbytes > 0 else None
+        if rows > 0:
+            self._ctc_raw(enc, rows, logp, ids, ws)
         return (logp.view(*shape, -1) if logp is not None else None), (ids.view(*shape) if ids is not None else None)
+
+    @torch.no_grad()
+    def ctc_collapse(self, ids: torch.Tensor, row_start, row_len, max_silence: Optional[int] = None,
+                     blank_id: int = 0):
+        """CTC post-processing on device over utterance b = ids[row_start[b] : row_start[b] + row_len[b]].
+
+        max_silence None: remove_duplicates_and_blank (model_utils.py:23-32) -> per utterance
+        (tokens, peak frames) lists.  max_silence >= 0: the sentence split of
+        get_output_with_timestamps (model_utils.py:174-221) -> per utterance a list of
+        (tokens, start_frame, end_frame) segments (80 ms frames).  One kernel launch and one
+        device -> host copy of the compacted results."""
+        B = len(row_start)
+        dev = self.device
+        ids = ids.reshape(-1).to(dev, torch.int32).contiguous()
+        rows = ids.numel()
+        rs = torch.tensor([int(v) for v in row_start], dtype=torch.int32)
+        rl = torch.tensor([int(v) for v in row_len], dtype=torch.int32)
+        if B and (int((rs + rl).max()) > rows or int(rs.min()) < 0 or int(rl.min()) < 0):
+            raise ValueError("utterance row ranges exceed the id tensor")
+        seg_mode = max_silence is not None
+        ms = int(max_silence) if seg_mode else -1
+        if seg_mode and ms < 0:
+            raise ValueError("max_silence must be >= 0")
+        tok = torch.empty(max(rows, 1), dtype=torch.int32, device=dev)
+        tfr = torch.empty(max(rows, 1), dtype=torch.int32, device=dev)
+        ntok = torch.zeros(max(B, 1), dtype=torch.int32, device=dev)
+        seg = torch.empty(max(rows, 1), 3, dtype=torch.int32, device=dev) if seg_mode else None
+        nseg = torch.zeros(max(B, 1), dtype=torch.int32, device=dev) if seg_mode else None
+        rs_d, rl_d = rs.to(dev), rl.to(dev)
+        _lib.check(_lib.cfm_ctc_collapse(ids.data_ptr(), rs_d.data_ptr(), rl_d.data_ptr(), B, int(blank_id), ms,
+                                         tok.data_ptr(), tfr.data_ptr(), ntok.data_ptr(), _lib.ptr(seg),
+                                         _lib.ptr(nseg), self._stream()))
+        tok_h, tfr_h, ntok_h = tok.cpu().tolist(), tfr.cpu().tolist(), ntok.cpu().tolist()
+        out = []
+        if not seg_mode:
+            for b in range(B):
+                s0, n = int(rs[b]), ntok_h[b]
+                out.append((tok_h[s0: s0 + n], tfr_h[s0: s0 + n]))
+            return out
+        seg_h, nseg_h = seg.cpu().tolist(), nseg.cpu().tolist()
+        for b in range(B):
+            s0, n, ns = int(rs[b]), ntok_h[b], nseg_h[b]
+            segs = []
+            for k in range(ns):
+                t0, start, end = seg_h[s0 + k]
+                t1 = seg_h[s0 + k + 1][0] if k + 1 < ns else n
+                segs.append((tok_h[s0 + t0: s0 + t1], start, end))
+            out.append(segs)
+        return out

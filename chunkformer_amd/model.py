@@ -11,8 +11,9 @@ path and its dependencies (pydub, torchaudio) are absent: wherever the reference
 `audio_path`, this mirror takes 80-dim fbank features -- a `[T, 80]` tensor, or a path to
 a `.npy` (loaded with allow_pickle=False) / `.pt` (torch.load weights_only=True) file.
 
-Text post-processing (remove_duplicates_and_blank, class2str, get_output,
-get_output_with_timestamps: chunkformer/utils/model_utils.py:23-221) is restated here so
+CTC post-processing (remove_duplicates_and_blank and get_output_with_timestamps' sentence
+split, chunkformer/utils/model_utils.py:23-221) runs on the device (cfm_ctc_collapse); only
+the id -> text mapping (class2str) and the hh:mm:ss:ms formatting stay on the host, so
 `char_dict` models return strings like the reference.
 """
 from __future__ import annotations
@@ -63,40 +64,18 @@ def milliseconds_to_hhmmssms(ms: int) -> str:
     return f"{h:02}:{m:02}:{s:02}:{rem:03}"
 
 
-def get_output_with_timestamps(hyps, char_dict: Dict[int, str], max_silence_duration: float) -> List[List[dict]]:
-    """model_utils.py:174-221: split a frame-level id stream (80 ms frames) into sentences at
-    silences of `max_silence_duration`.  `hyps` is a list of [T] or [T, 1] id tensors."""
-    decodes = []
-    max_silence = max_silence_duration // 0.08
-    for tokens in hyps:
-        tok = torch.as_tensor(tokens).cpu().reshape(len(tokens), -1)
-        start = end = prev_end = -1
-        silence = 0
-        per_time: List[int] = []
-        items: List[dict] = []
-        t = -1
-        for t in range(tok.shape[0]):
-            row = tok[t]
-            blank = row == 0
-            if bool(blank.all()):
-                silence += 1
-            else:
-                if start == -1 and end == -1:
-                    start = max(math.ceil((t + prev_end) / 2), t - 2) if prev_end != -1 else max(t - 2, 0)
-                silence = 0
-                per_time.extend(row[~blank].tolist())
-            if silence == max_silence and start != -1:
-                end = prev_end = t
-                items.append({"decode": get_output([per_time], char_dict)[0],
-                              "start": milliseconds_to_hhmmssms(start * 80),
-                              "end": milliseconds_to_hhmmssms(end * 80)})
-                per_time, start, end, silence = [], -1, -1, 0
-        if start != -1 and end == -1 and per_time:
-            items.append({"decode": get_output([per_time], char_dict)[0],
-                          "start": milliseconds_to_hhmmssms(start * 80),
-                          "end": milliseconds_to_hhmmssms(t * 80)})
-        decodes.append(items)
-    return decodes
+def max_silence_frames(max_silence_duration: float) -> int:
+    """model_utils.py:176: max_silence = max_silence_duration // 0.08 (80 ms frames); a negative
+    value never closes a sentence, i.e. one segment per utterance."""
+    ms = max_silence_duration // 0.08
+    return int(ms) if ms >= 0 else 1 << 30
+
+
+def format_segments(segs, char_dict: Dict[int, str]) -> List[dict]:
+    """Device segments (tokens, start frame, end frame) -> the reference's items
+    {"decode", "start", "end"} (model_utils.py:203-218: class2str(...).strip(), 80 ms frames)."""
+    return [{"decode": class2str(toks, char_dict).strip(), "start": milliseconds_to_hhmmssms(st * 80),
+             "end": milliseconds_to_hhmmssms(en * 80)} for toks, st, en in segs]
 
 
 # ----------------------------------------------------------------------------- segment math
@@ -291,7 +270,11 @@ class ChunkFormerModel:
         self.last_endless_caches = (runner.att[runner.cur], runner.cnn[runner.cur])
         tokens = torch.cat(ids).long().reshape(1, -1, 1) if ids else None
         if self.char_dict is not None and tokens is not None:
-            res = get_output_with_timestamps(tokens, self.char_dict, max_silence_duration)[0]
+            # get_output_with_timestamps (model_utils.py:174-221) on the device: sentence split at
+            # max_silence blank frames, de-duplicated tokens per sentence
+            segs = enc.ctc_collapse(tokens, [0], [tokens.shape[1]],
+                                    max_silence=max_silence_frames(max_silence_duration))[0]
+            res = format_segments(segs, self.char_dict)
             if not return_timestamps:
                 res = " ".join(item["decode"] for item in res).strip()
         else:
@@ -316,11 +299,14 @@ class ChunkFormerModel:
             lens = torch.tensor([x.shape[0] for x in xs], dtype=torch.int)
             offset = torch.zeros(len(xs), dtype=torch.int)
             eo, el, n_chunks, _, _, _ = self.encoder.forward_parallel_chunk(xs, lens, C, L, R, offset=offset)
-            _, hyp = self.encoder.ctc_log_softmax(eo, want_logp=False)
-            hyps = [h.flatten()[: int(n)].long() for h, n in zip(hyp.split(n_chunks, dim=0), el.tolist())]
+            _, hyp = self.encoder.ctc_log_softmax(eo, want_logp=False)   # fused argmax head
             if self.char_dict is not None:
-                hyps = get_output(hyps, self.char_dict)
-            decodes.extend(hyps)
+                # remove_duplicates_and_blank on the device, per utterance rows [64 * chunk0, +len)
+                starts = np.cumsum([0] + list(n_chunks[:-1])) * C
+                toks = self.encoder.ctc_collapse(hyp, starts.tolist(), el.tolist())
+                decodes.extend(class2str(t, self.char_dict).strip() for t, _ in toks)
+            else:
+                decodes.extend(h.flatten()[: int(n)].long() for h, n in zip(hyp.split(n_chunks, dim=0), el.tolist()))
         return decodes
 
 

@@ -86,8 +86,8 @@ class EndlessGraphRunner:
                                 dtype=torch.uint8, device=self.dev)
         if self.vocab > 0:
             self.g_ids = torch.empty(self.g_rows, dtype=torch.int32, device=self.dev)
-            self.g_ctc_ws = torch.empty(_lib.cfm_ctc_workspace_bytes(enc._h, self.g_rows), dtype=torch.uint8,
-                                        device=self.dev)
+            nb = enc.ctc_ws_bytes(self.g_rows, False)   # 0 on the fused argmax head
+            self.g_ctc_ws = torch.empty(nb, dtype=torch.uint8, device=self.dev) if nb > 0 else None
         torch.cuda.current_stream(self.dev).synchronize()
 
         def body(src: int):

@@ -143,6 +143,28 @@ size_t cfm_ctc_workspace_bytes(const cfm_model* m, int32_t rows);
 cfm_status cfm_ctc_logprobs(const cfm_model* m, const float* enc_dev, int32_t rows, float* logp_dev, int32_t* ids_dev,
                             void* workspace, size_t workspace_bytes, cfm_stream stream);
 
+/* Fused CTC tail, ids only: ids_dev[rows] = argmax of CTC.log_softmax (ctc.py:73-81) as
+ * chunkformer_model.py:437-438 / 526-527 take it.  On bf16 models with d_model 512 the logits never
+ * leave registers (no [rows, V] tensor; workspace 0 bytes); otherwise it runs the log-softmax path
+ * in the workspace (cfm_ctc_ids_workspace_bytes). */
+size_t cfm_ctc_ids_workspace_bytes(const cfm_model* m, int32_t rows);
+cfm_status cfm_ctc_ids(const cfm_model* m, const float* enc_dev, int32_t rows, int32_t* ids_dev, void* workspace,
+                       size_t workspace_bytes, cfm_stream stream);
+
+/* CTC post-processing on device, one utterance b = frames [row_start[b], row_start[b] + row_len[b])
+ * of ids_dev (device int32 arrays; regions must not overlap).  Outputs are written compacted at
+ * the start of each utterance's region:
+ *   max_silence < 0: remove_duplicates_and_blank (utils/model_utils.py:23-32): tokens[] and the
+ *     frame of each token (gen_ctc_peak_time, model_utils.py:49-58), n_tokens[b];
+ *   max_silence >= 0: the sentence split of get_output_with_timestamps (model_utils.py:174-221)
+ *     at max_silence (= max_silence_duration // 0.08) blank frames: per segment the de-duplicated
+ *     non-blank tokens (tokens[], token_frames[]) and segments[s] = {first token, start frame,
+ *     end frame} (80 ms frames), n_tokens[b], n_segments[b]. */
+cfm_status cfm_ctc_collapse(const int32_t* ids_dev, const int32_t* row_start_dev, const int32_t* row_len_dev, int32_t B,
+                            int32_t blank_id, int32_t max_silence, int32_t* tokens_dev, int32_t* token_frames_dev,
+                            int32_t* n_tokens_dev, int32_t* segments_dev /* [rows, 3] or NULL */,
+                            int32_t* n_segments_dev /* [B] or NULL */, cfm_stream stream);
+
 #ifdef __cplusplus
 }
 #endif

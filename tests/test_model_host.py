@@ -6,7 +6,7 @@ import numpy as np
 import pytest
 import torch
 
-from chunkformer_amd.model import (budget_groups, endless_segments, get_output, get_output_with_timestamps,
+from chunkformer_amd.model import (budget_groups, endless_segments, format_segments, get_output, max_silence_frames,
                                    milliseconds_to_hhmmssms, remove_duplicates_and_blank, load_json_cmvn)
 
 
@@ -71,8 +71,9 @@ def test_text_helpers():
     assert get_output([[1, 1, 0, 2]], cd) == ["xin chào"]
     assert milliseconds_to_hhmmssms(3_723_004) == "01:02:03:004"
     toks = [0, 0, 1, 0, 0, 0, 0, 0, 0, 0, 0, 2, 2, 0]
-    import torch
-    res = get_output_with_timestamps([torch.tensor(toks).view(-1, 1)], cd, 0.5)[0]
+    from oracle.ctc_ref import segments_with_timestamps
+    assert max_silence_frames(0.5) == 6 and max_silence_frames(0.24) == 2 and max_silence_frames(-1) == 1 << 30
+    res = format_segments(segments_with_timestamps(toks, max_silence_frames(0.5)), cd)
     # max_silence = 0.5 // 0.08 = 6 frames -> first sentence ends at t=8, second runs to the end
     assert [r["decode"] for r in res] == ["xin", "chào"]
     assert res[0]["start"] == "00:00:00:000" and res[0]["end"] == milliseconds_to_hhmmssms(8 * 80)
@@ -89,18 +90,22 @@ def test_json_cmvn(tmp_path):
 
 
 def test_text_helpers_match_reference_golden(golden_dir):
-    """get_output / get_output_with_timestamps against the reference's own model_utils run on the
-    same id streams (tests/golden/text.json, written by gen_golden.py)."""
+    """get_output and the CTC oracle's sentence split (oracle/ctc_ref.py, the checker of the device
+    collapse kernel) + format_segments against the reference's own model_utils run on the same id
+    streams (tests/golden/text.json, written by gen_golden.py)."""
     import json
 
-    from chunkformer_amd.model import get_output, get_output_with_timestamps
+    from chunkformer_amd.model import get_output
     from chunkformer_amd.weights import synthetic_vocab
+    from oracle.ctc_ref import remove_duplicates_and_blank as ref_rdb, segments_with_timestamps
     with open(os.path.join(golden_dir, "text.json"), encoding="utf8") as f:
         g = json.load(f)
     cd = synthetic_vocab(int(g["V"]))
     assert get_output(g["streams"], cd) == g["get_output"]
+    for s in g["streams"]:
+        assert ref_rdb(s) == remove_duplicates_and_blank(s)
     for ms, exp in g["timestamps"].items():
-        got = get_output_with_timestamps([torch.tensor(s).reshape(-1, 1) for s in g["streams"]], cd, float(ms))
+        got = [format_segments(segments_with_timestamps(s, float(ms) // 0.08), cd) for s in g["streams"]]
         assert got == exp, ms
 
 
