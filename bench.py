@@ -2,13 +2,20 @@
 
     python bench.py --gpus N --steps K --warmup W            (N>1: launched by torch.distributed.run)
 
-Workload (BASELINE.json configs[1]): chunkformer-large (12 layers, d=512,
-8 heads, ff=2048, conv k=15, V=5000) with seeded synthetic weights, a 240-min masked
-batch PER GPU of synthetic N(0,1) 80-dim fbank: utterance lengths log-uniform in
-[1 s, 30 min] from torch.Generator seed 0 (B=70, N=2,845 chunks at one GPU),
-chunk 64 / left 128 / right 128.  For N GPUs the generator draws N x 240 min and the
-utterances are LPT-sharded over the ranks by chunk count (no data-path collective:
-weak scaling); after timing, CTC ids are all-gathered over RCCL and timed separately.
+Workload: chunkformer-large (12 layers, d=512, 8 heads, ff=2048, conv k=15,
+V=5000) with seeded synthetic weights, synthetic N(0,1) 80-dim fbank, utterance lengths
+log-uniform in [1 s, 30 min] from torch.Generator seed 0, chunk 64 / left 128 / right 128.
+
+  --config auto (default): masked at N = 1, sharded at N > 1
+  --config masked   BASELINE configs[1]: a 240-min masked batch (B=70, N=2,845 chunks) PER GPU
+                    (weak scaling)
+  --config sharded  BASELINE configs[2]: ONE 980-min masked batch (B=284, N=11,625 chunks)
+                    sharded over the ranks (strong scaling): distributed.plan_shards cuts it into
+                    per-rank pieces (LPT over chunk counts; utterances longer than a rank's share
+                    are split with recomputed halos), no exchange during the encoder; after timing
+                    the CTC ids (fused argmax head) go through ONE all_gather_into_tensor over
+                    RCCL/xGMI, and the bf16 log-probs through another, each timed separately
+  --config endless / full   configs[3] / configs[4] (one GPU)
 
 A step = ChunkFormerEncoder.forward_parallel_chunk over the rank's whole batch:
 host packer (C++ planner) + plan upload + front-end + 12 blocks + after_norm, with
@@ -38,7 +45,8 @@ sys.path.insert(0, ROOT)
 
 from chunkformer_amd import _lib  # noqa: E402
 from chunkformer_amd.config import LARGE  # noqa: E402
-from chunkformer_amd.distributed import chunks_of, gather_ids, init_from_env, lpt_shard  # noqa: E402
+from chunkformer_amd.distributed import (chunks_of, gather_ids, gather_logp, init_from_env,  # noqa: E402
+                                         plan_shards, rank_rows)
 from chunkformer_amd.encoder import ChunkFormerEncoder  # noqa: E402
 from chunkformer_amd.weights import synthetic_state_dict  # noqa: E402
 
@@ -115,31 +123,48 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
-    ap.add_argument("--minutes", type=float, default=240.0, help="audio minutes per GPU")
+    ap.add_argument("--minutes", type=float, default=None,
+                    help="audio minutes: per GPU for masked (240), of the whole batch for sharded (980)")
+    ap.add_argument("--no-gather-logp", action="store_true", help="sharded: skip the bf16 log-prob all-gather")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-breakdown", action="store_true")
-    ap.add_argument("--config", default="masked", choices=["masked", "endless", "full"],
-                    help="masked = configs[1] (default, the headline line); endless = configs[3] (16 h "
-                         "endless_decode, graph-replayed segments); full = configs[4] (full attention, B=256)")
+    ap.add_argument("--config", default="auto", choices=["auto", "masked", "sharded", "endless", "full"],
+                    help="auto = masked at 1 GPU, sharded at N > 1; masked = configs[1] (240 min per GPU, the "
+                         "headline line); sharded = configs[2] (one 980-min batch over all ranks); endless = "
+                         "configs[3] (16 h endless_decode, graph-replayed segments); full = configs[4] (full "
+                         "attention, B=256)")
     ap.add_argument("--hours", type=float, default=16.0, help="endless: audio hours")
     ap.add_argument("--tbd", type=int, default=1800, help="endless: total_batch_duration (s)")
     ap.add_argument("--batch", type=int, default=256, help="full: utterances of T=3000 frames")
     args = ap.parse_args()
-    if args.config != "masked":
+    if args.config in ("endless", "full"):
         return bench_single(args)
 
     rank, world, local = init_from_env()
+    local = local % torch.cuda.device_count()   # (rehearsal of several ranks on one GPU: gloo backend)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    per_gpu = int(args.minutes * 60 * 100)
-    lens_all = workload_lengths(per_gpu * world, seed=0)
-    shards = lpt_shard(lens_all, world, C) if world > 1 else [list(range(len(lens_all)))]
+    sharded = args.config == "sharded" or (args.config == "auto" and world > 1)
+    minutes = args.minutes if args.minutes is not None else (980.0 if sharded else 240.0)
+    if sharded:   # configs[2]: one batch of `minutes` over all ranks
+        lens_all = workload_lengths(int(minutes * 60 * 100), seed=0)
+        shards = plan_shards(lens_all, world, C, L, R, LARGE.num_blocks)
+    else:         # configs[1]: `minutes` per rank, whole utterances LPT-placed
+        lens_all = workload_lengths(int(minutes * 60 * 100) * world, seed=0)
+        shards = plan_shards(lens_all, world, C, L, R, LARGE.num_blocks, split=False)
     mine = shards[rank]
-    lens = [lens_all[i] for i in mine]
-    g = torch.Generator(device=dev).manual_seed(1234 + rank)
-    xs = [torch.randn(t, 80, generator=g, device=dev) for t in lens]
+    # features: utterance u from its own seed, so every rank sees the same audio for u
+    need = sorted({p.utt for p in mine})
+    full = {u: torch.randn(lens_all[u], 80, generator=torch.Generator(device=dev).manual_seed(1234 + u), device=dev)
+            for u in need}
+    xs = [full[p.utt][p.frame0: p.frame0 + p.frames] for p in mine]
+    lens = [p.frames for p in mine]
     xs_lens = torch.tensor(lens, dtype=torch.int32)
     n_chunks = sum(chunks_of(t, C) for t in lens)
+    # real audio frames this rank answers for: its kept chunks' frames (halo frames recomputed
+    # around cuts are not counted); over all ranks this sums to the batch's frames exactly
+    real_frames = sum((lens_all[p.utt] if p.k1 == chunks_of(lens_all[p.utt], C) else p.k1 * 8 * C) - p.k0 * 8 * C
+                      for p in mine)
 
     enc = ChunkFormerEncoder(LARGE, synthetic_state_dict(LARGE, 0), device=dev, dtype=args.dtype)
 
@@ -165,7 +190,7 @@ def main():
     enc.set_option("profile", 0)
     prof = _lib.profile_read(enc._h)
     t = torch.tensor([dt], dtype=torch.float64, device=dev)
-    frames = torch.tensor([float(sum(lens))], dtype=torch.float64, device=dev)
+    frames = torch.tensor([float(real_frames)], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dist.all_reduce(frames, op=dist.ReduceOp.SUM)
@@ -198,7 +223,7 @@ def main():
     traffic, traffic_src = committed_traffic(roof_cls) if args.dtype == "bf16" else (None, None)
     step_flops = n_chunks * flops_per_chunk(LARGE) + LARGE.num_blocks * 2 * (L + 2 * C + R - 1) * LARGE.d_model ** 2
 
-    # ---- CTC head + the one collective (timed separately; not part of `value`)
+    # ---- CTC head + the collectives (timed separately; not part of `value`)
     enc_out = out[0]
     enc.ctc_log_softmax(enc_out, want_logp=False)   # first call loads the kernel
     torch.cuda.synchronize()
@@ -206,17 +231,29 @@ def main():
     _, ids = enc.ctc_log_softmax(enc_out, want_logp=False)   # fused argmax head (ids only)
     torch.cuda.synchronize()
     ctc_ms = (time.perf_counter() - tc) * 1e3
-    gather_ms = None
+    gather_ms = gather_lp_ms = None
     if world > 1:
-        out_lens = [max(0, int(v)) for v in out[1].tolist()]
-        segs = ids.view(-1, C).split(out[2], 0)
-        flat = torch.cat([s.reshape(-1)[:ol] for s, ol in zip(segs, out_lens)])
+        # the kept rows of every piece, in shard order (the layout gather_* expects)
+        starts = torch.tensor([0] + list(out[2][:-1])).cumsum(0) * C
+        idx = torch.cat([torch.arange(int(s) + p.skip, int(s) + p.skip + p.rows) for s, p in zip(starts, mine)])
+        idx = idx.to(dev)
+        flat = ids.reshape(-1).index_select(0, idx)
         dist.barrier()
         torch.cuda.synchronize()
         tg = time.perf_counter()
-        gather_ids(flat, out_lens, shards)
+        gather_ids(flat, shards, lens_all)
         torch.cuda.synchronize()
         gather_ms = (time.perf_counter() - tg) * 1e3
+        if sharded and not args.no_gather_logp:
+            logp, _ = enc.ctc_log_softmax(enc_out.reshape(-1, LARGE.d_model).index_select(0, idx), want_logp=True,
+                                          want_ids=False)
+            dist.barrier()
+            torch.cuda.synchronize()
+            tg = time.perf_counter()
+            gather_logp(logp, shards, lens_all)
+            torch.cuda.synchronize()
+            gather_lp_ms = (time.perf_counter() - tg) * 1e3
+            del logp
 
     breakdown = None
     if not args.no_breakdown:
@@ -237,14 +274,18 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(dt_max / args.steps * 1e3, 3),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if sharded else "weak",
             "vs_baseline": None,
             "dtype": args.dtype,
             "data": "synthetic (N(0,1) 80-dim fbank, seeded random chunkformer-large weights; no checkpoint offline)",
-            "config": {"workload": f"masked batch, {args.minutes:g} min of audio per GPU (log-uniform 1 s-30 min "
-                                   f"utterances, seed 0), forward_parallel_chunk C=64 L=128 R=128",
-                       "utterances_rank0": len(lens), "chunks_rank0": n_chunks, "frames_total": int(total_frames),
-                       "parallelism": f"dp{world} (LPT utterance sharding)"},
+            "config": {"workload": (f"configs[2]: one {minutes:g}-min masked batch (log-uniform 1 s-30 min utterances, "
+                                    f"seed 0, B={len(lens_all)}) sharded over {world} GPU(s) by plan_shards, "
+                                    f"forward_parallel_chunk C=64 L=128 R=128" if sharded else
+                                    f"configs[1]: masked batch, {minutes:g} min of audio per GPU (log-uniform 1 s-30 "
+                                    f"min utterances, seed 0), forward_parallel_chunk C=64 L=128 R=128"),
+                       "config_index": 2 if sharded else 1,
+                       "pieces_rank0": len(mine), "chunks_rank0": n_chunks, "frames_total": int(total_frames),
+                       "parallelism": f"dp{world} ({'plan_shards: LPT pieces, halo cuts' if sharded else 'LPT utterance sharding'})"},
             "roofline": {"bound": "mfma", "kernel": roof_name,
                          "achieved": round(achieved, 1) if achieved else None, "peak": peak, "unit": "TFLOP/s",
                          "frac": round(achieved / peak, 4) if achieved else None, "traffic": traffic,
@@ -255,6 +296,7 @@ def main():
             "step_tflops_algorithmic": round(step_flops / (dt_max / args.steps) / 1e12, 1),
             "ctc_ms": round(ctc_ms, 3),
             "allgather_ids_ms": round(gather_ms, 3) if gather_ms is not None else None,
+            "allgather_logp_bf16_ms": round(gather_lp_ms, 3) if gather_lp_ms is not None else None,
             "breakdown_ms": breakdown,
         }
         if world == 1 and not args.no_cpu_baseline:

@@ -1,0 +1,92 @@
+"""§8(e) on one GPU: every rank's pieces of a sharded masked batch (distributed.plan_shards) run
+one after another through the same encoder, and the reassembled per-utterance rows equal the
+unsharded call -- across halo cuts of a long utterance too (exact receptive-field halos: the kept
+chunks see bit-identical inputs at every layer).  The collective itself is covered by the gloo
+test (tests/test_distributed_cpu.py); here the reassembly is the same `_assemble` it uses.
+
+Tolerances: fp32 max-abs 2e-6 (measured batch-composition invariance), CTC ids
+identical; bf16 rel-L2 <= 1e-2 against the unsharded bf16 run (the GEMM tile path can change with
+the batch's row count)."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _run_sharded(enc, xs, lens, world, C, L, R, nb):
+    from chunkformer_amd.distributed import _assemble, plan_shards, run_pieces
+    shards = plan_shards(lens, world, C, L, R, nb)
+    outs, idss = [], []
+    for shard in shards:
+        kept, ids, _ = run_pieces(enc, xs, shard, C, L, R)
+        outs.append(kept)
+        idss.append(ids)
+    mx = max(1, max(o.shape[0] for o in outs))
+    d = outs[0].shape[1]
+    buf = torch.zeros(world, mx, d, device=enc.device)
+    ibuf = torch.zeros(world, mx, dtype=torch.int32, device=enc.device)
+    for r, (o, i) in enumerate(zip(outs, idss)):
+        buf[r, : o.shape[0]] = o
+        ibuf[r, : i.shape[0]] = i
+    return shards, _assemble(buf, shards, len(lens), lens), _assemble(ibuf, shards, len(lens), lens)
+
+
+def _unsharded(enc, xs, lens, C, L, R):
+    out, olens, nch, _, _, _ = enc.forward_parallel_chunk(xs, torch.tensor(lens, dtype=torch.int32), C, L, R)
+    _, ids = enc.ctc_log_softmax(out, want_logp=False)
+    flat, fid = out.reshape(-1, out.shape[-1]), ids.reshape(-1)
+    res, rid, o = [], [], 0
+    for nc, ol in zip(nch, olens.tolist()):
+        res.append(flat[o: o + ol])
+        rid.append(fid[o: o + ol])
+        o += nc * C
+    return res, rid
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+@pytest.mark.parametrize("world", [2, 3])
+def test_small_model_halo_cuts(dtype, world):
+    """2-layer model, C=16 L=R=32 (halo 6 chunks): one long utterance cut into pieces + clips."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from chunkformer_amd.config import SMALL
+    from chunkformer_amd.encoder import ChunkFormerEncoder
+    from chunkformer_amd.weights import synthetic_features, synthetic_state_dict
+    C, L, R = 16, 32, 32
+    enc = ChunkFormerEncoder(SMALL, synthetic_state_dict(SMALL, 1), dtype=dtype)
+    lens = [12_007, 300, 1000, 129, 2222]
+    xs = [x.cuda() for x in synthetic_features(lens, 21)]
+    shards, outs, ids = _run_sharded(enc, xs, lens, world, C, L, R, SMALL.num_blocks)
+    assert any(p.k0 > 0 for s in shards for p in s), "the long utterance must be cut"
+    ref, rid = _unsharded(enc, xs, lens, C, L, R)
+    for u in range(len(lens)):
+        assert outs[u].shape == ref[u].shape
+        if dtype == "fp32":
+            assert float((outs[u] - ref[u]).abs().max()) <= 2e-6, u
+            assert torch.equal(ids[u], rid[u])
+        else:
+            rel = float((outs[u] - ref[u]).norm() / ref[u].norm())
+            assert rel <= 1e-2, (u, rel)
+
+
+def test_large_model_halo_cuts():
+    """chunkformer-large (12 layers, 36-chunk halos), fp32: a 30-min utterance cut 3 ways among
+    short clips reassembles to the unsharded rows."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from chunkformer_amd.config import LARGE
+    from chunkformer_amd.encoder import ChunkFormerEncoder
+    from chunkformer_amd.weights import synthetic_state_dict
+    C, L, R = 64, 128, 128
+    enc = ChunkFormerEncoder(LARGE, synthetic_state_dict(LARGE, 0), dtype="fp32")
+    lens = [180_000, 3000, 12_345, 700, 40_000]
+    g = torch.Generator(device="cuda").manual_seed(9)
+    xs = [torch.randn(t, 80, generator=g, device="cuda") for t in lens]
+    shards, outs, ids = _run_sharded(enc, xs, lens, 3, C, L, R, LARGE.num_blocks)
+    assert sum(1 for s in shards for p in s if p.utt == 0) >= 2
+    ref, rid = _unsharded(enc, xs, lens, C, L, R)
+    for u in range(len(lens)):
+        err = float((outs[u] - ref[u]).abs().max())
+        assert err <= 2e-6, (u, err)
+        assert float((ids[u] != rid[u]).float().mean()) <= 1e-3
