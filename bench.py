@@ -78,11 +78,38 @@ def flops_per_chunk(cfg) -> float:
     return front + cfg.num_blocks * layer
 
 
+def host_cpu():
+    """(CPU model, physical cores this process may run on): /proc/cpuinfo over the affinity set,
+    capped by the box's thread share (OMP_NUM_THREADS) when it is set."""
+    allowed = set(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else set(range(os.cpu_count() or 1))
+    model, cores, cur = "unknown", set(), {}
+    try:
+        with open("/proc/cpuinfo") as f:
+            lines = f.read().split("\n") + [""]
+    except OSError:
+        lines = []
+    for line in lines:
+        if not line.strip():
+            if cur.get("processor", "").isdigit() and int(cur["processor"]) in allowed:
+                cores.add((cur.get("physical id", "0"), cur.get("core id", cur["processor"])))
+                model = cur.get("model name", model)
+            cur = {}
+            continue
+        k, _, v = line.partition(":")
+        cur[k.strip()] = v.strip()
+    n = len(cores) or len(allowed)
+    cap = os.environ.get("OMP_NUM_THREADS", "")
+    if cap.isdigit() and int(cap) > 0:
+        n = min(n, int(cap))
+    return model, max(1, n)
+
+
 def cpu_baseline(lens_all, budget_s: float = 12.0):
-    """Time the CPU oracle (torch fp32) on consecutive utterance groups until the budget."""
+    """Time the CPU oracle (torch fp32) on consecutive utterance groups until the budget, on every
+    physical core of the process's CPU share."""
     from chunkformer_amd.weights import synthetic_features
     from oracle import encoder_ref as ref
-    threads = min(16, os.cpu_count() or 1)
+    model, threads = host_cpu()
     torch.set_num_threads(threads)
     sd = synthetic_state_dict(LARGE, 0)
     frames, t_tot, groups, i = 0, 0.0, 0, 0
@@ -174,7 +201,7 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    roof_bits = (1 << _lib.PROFILE_CLASSES.index("ffn_w1_gemm")) | (1 << _lib.PROFILE_CLASSES.index("ffn_fused"))
+    roof_bits = 1 << _lib.PROFILE_CLASSES.index("ffn_w1_gemm")
     enc.set_option("profile_reset", 1)
     enc.set_option("profile", roof_bits)
     if world > 1:
@@ -202,20 +229,12 @@ def main():
     # per-launch time from in-stream HIP events on the launch stream (libcfm profiler)
     rows = n_chunks * C
     d_, ff_ = LARGE.d_model, LARGE.ffn_dim
-    fused = prof.get("ffn_fused", (0.0, 0))[1] > 0
-    if fused:
-        roof_cls = "ffn_fused"
-        roof_name = "ffn_fused (ffn_fused_kernel: w_2 . SiLU(w_1 . x + b_1) + b_2, hidden kept on-chip)"
-        fl_launch = 2.0 * 2.0 * rows * ff_ * d_
-        # compulsory bytes: x [rows, d] in + y [rows, d] out (bf16) + the 4 MiB weight slab stream + biases
-        alg_bytes = 2.0 * (2 * rows * d_ + 2 * ff_ * d_) + 4 * (ff_ + d_)
-    else:
-        roof_cls = "ffn_w1_gemm"
-        roof_name = ("ffn_w1_gemm (gemm_wsp_kernel<EPI_STORE,SiLU>: K=512 weight-stationary bf16 MFMA)"
-                     if args.dtype == "bf16" else "ffn_w1_gemm (gemm_kernel<float,EPI_STORE,SiLU>)")
-        fl_launch = 2.0 * rows * ff_ * d_
-        # compulsory bytes of one w_1 launch: A [rows, d] + out [rows, ff] bf16 + W [ff, d] bf16 + bias
-        alg_bytes = 2.0 * (rows * d_ + rows * ff_ + ff_ * d_) + 4 * ff_
+    roof_cls = "ffn_w1_gemm"
+    roof_name = ("ffn_w1_gemm (gemm_wsp_kernel<EPI_STORE,SiLU>: K=512 weight-stationary bf16 MFMA)"
+                 if args.dtype == "bf16" else "ffn_w1_gemm (gemm_kernel<float,EPI_STORE,SiLU>)")
+    fl_launch = 2.0 * rows * ff_ * d_
+    # compulsory bytes of one w_1 launch: A [rows, d] + out [rows, ff] bf16 + W [ff, d] bf16 + bias
+    alg_bytes = 2.0 * (rows * d_ + rows * ff_ + ff_ * d_) + 4 * ff_
     ms1, n1 = prof[roof_cls]
     avg_s = (ms1 / max(n1, 1)) / 1e3
     achieved = fl_launch / avg_s / 1e12 if n1 else None

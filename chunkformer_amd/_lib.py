@@ -60,6 +60,9 @@ cfm_model_destroy = _sig("cfm_model_destroy", None, P)
 cfm_model_set_option = _sig("cfm_model_set_option", I32, P, ctypes.c_char_p, I64)
 cfm_plan_masked = _sig("cfm_plan_masked", I32, P, P, I32, I32, I32, I32, P, P, PI32, P, PI64)
 cfm_plan_padded = _sig("cfm_plan_padded", I32, P, I32, I32, I32, I32, I32, PI32, P, PI64)
+cfm_plan_stream = _sig("cfm_plan_stream", I32, I32, I32, I32, I32, I32, PI32, P, PI64)
+cfm_workspace_bytes_stream = _sig("cfm_workspace_bytes_stream", SZ, P, I32, I32, I32, I32)
+cfm_encode_stream = _sig("cfm_encode_stream", I32, P, P, I32, P, P, P, P, P, P, P, P, SZ, P)
 cfm_workspace_bytes_masked = _sig("cfm_workspace_bytes_masked", SZ, P, I32, I32, I32, I32)
 cfm_workspace_bytes_padded = _sig("cfm_workspace_bytes_padded", SZ, P, I32, I32, I32, I32, I32)
 cfm_encode_masked = _sig("cfm_encode_masked", I32, P, P, P, P, P, P, I32, P, P, P, P, SZ, P)
@@ -74,13 +77,13 @@ cfm_ctc_collapse = _sig("cfm_ctc_collapse", I32, P, P, P, I32, I32, I32, P, P, P
 # include/cfm_ops.h
 cfm_op_gemm = _sig("cfm_op_gemm", I32, I32, I32, I32, P, I32, P, I32, I32, I32, I32, P, ctypes.c_float, P, I32, I32, P,
                    I32, P, I32, P, I32, P)
-cfm_op_ffn = _sig("cfm_op_ffn", I32, P, P, P, P, P, P, I32, I32, I32, P)
-EXPORTED_OPS = ["cfm_op_gemm", "cfm_op_ffn"]
+EXPORTED_OPS = ["cfm_op_gemm"]
 
 EXPORTED = ["cfm_version", "cfm_last_error", "cfm_model_create", "cfm_model_destroy", "cfm_model_set_option",
             "cfm_plan_masked", "cfm_plan_padded", "cfm_workspace_bytes_masked", "cfm_workspace_bytes_padded",
             "cfm_encode_masked", "cfm_encode_padded", "cfm_masks_from_plan", "cfm_profile_read", "cfm_ctc_workspace_bytes",
-            "cfm_ctc_logprobs", "cfm_ctc_ids_workspace_bytes", "cfm_ctc_ids", "cfm_ctc_collapse"]
+            "cfm_ctc_logprobs", "cfm_ctc_ids_workspace_bytes", "cfm_ctc_ids", "cfm_ctc_collapse",
+            "cfm_plan_stream", "cfm_workspace_bytes_stream", "cfm_encode_stream"]
 
 
 def profile_read(h):
@@ -95,7 +98,7 @@ def profile_read(h):
 
 PROFILE_CLASSES = ["frontend_conv0_dw", "frontend_pw_gemm", "frontend_dw2", "pos_gemm", "layernorm", "ffn_w1_gemm",
                    "ffn_w2_gemm", "qkv_gemm", "chunk_attention", "out_proj_gemm", "pw1_glu_gemm", "conv_dw_ln_silu",
-                   "pw2_gemm", "cache_copy", "ctc", "ffn_fused"]
+                   "pw2_gemm", "cache_copy", "ctc"]
 
 
 def check(status: int) -> None:
@@ -129,6 +132,17 @@ def plan_masked(lens, offsets, C: int, L: int, R: int):
     check(cfm_plan_masked(lens_t.data_ptr(), ptr(offs_t), B, C, L, R, None, None, ctypes.byref(total),
                           plan.data_ptr(), ctypes.byref(n)))
     return plan, nch.tolist(), olen.tolist()
+
+
+def plan_stream(T: int, C: int, L: int, R: int, offset: int):
+    """Host planner of one forward_chunk step (no GPU): returns (plan int32 CPU tensor, T')."""
+    tout = I32(0)
+    n = I64(0)
+    check(cfm_plan_stream(int(T), int(C), int(L), int(R), int(offset), ctypes.byref(tout), None, ctypes.byref(n)))
+    plan = torch.zeros(n.value, dtype=torch.int32)
+    check(cfm_plan_stream(int(T), int(C), int(L), int(R), int(offset), ctypes.byref(tout), plan.data_ptr(),
+                          ctypes.byref(n)))
+    return plan, tout.value
 
 
 def plan_padded(lens, T: int, C: int, L: int, R: int):

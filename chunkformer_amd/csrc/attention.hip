@@ -580,7 +580,7 @@ __global__ __launch_bounds__(512, 1) void chunk_attention_ring_kernel(
 // returns -1 when the shape is not eligible for the ring kernel
 int chunk_attention_masked_bf16(const bf16* q, const bf16* kv, int kv_rows, const bf16* P, int p_rows,
                                 const float* pos_u, const float* pos_v, const int32_t* desc, int n_chunks, int H,
-                                int C, int W, bf16* out, hipStream_t st, int diag, int p_ld) {
+                                int C, int W, bf16* out, hipStream_t st, int diag, int p_ld, int reuse) {
   if (p_ld <= 0) p_ld = H * 64;
   // W <= 320: a query's scores are 5 tiles of 64 keys held in registers (exact softmax)
   if (C <= 0 || C > 64 || (C % 16) || (W & 1) || W > 320 || W + C > RING || p_rows > RING || n_chunks <= 0) return -1;
@@ -592,9 +592,7 @@ int chunk_attention_masked_bf16(const bf16* q, const bf16* kv, int kv_rows, cons
     (void)hipGetDevice(&dev);
     if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0) n_cu = 256;
   }
-  static int reuse = -1;   // CFM_ATTN_REUSE=0: recompute the shared band subtile (A/B)
-  if (reuse < 0) { const char* e = getenv("CFM_ATTN_REUSE"); reuse = e ? atoi(e) : 1; }
-  if (!reuse && diag == 0) diag = 5;
+  if (!reuse && diag == 0) diag = 5;   // "attn_reuse" 0: recompute the shared band subtile (A/B)
   int nch = (int)(((long long)n_chunks * H + n_cu - 1) / n_cu);
   nch = max(NCH, (nch + 1) & ~1);
   const dim3 grid((n_chunks + nch - 1) / nch, H);

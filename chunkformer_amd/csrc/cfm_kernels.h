@@ -26,14 +26,31 @@ struct EpiArgs {
   int dk = 64;                   // QKV: head dim (KV stream rows are [H][K dk | V dk])
   int col_group = 0;             // bf16 256-tile walk: column tiles per group (0 = all; tiles ordered group, row, col)
   int store_mode = 0;            // bf16 epilogue stores: 0 = plain, 1 = sc1 (drop the line from L2), 2 = nt
+  // kernel selection / diagnostics (per model: cfm_model_set_option, never process-global)
+  int diag = 0;                  // timing diagnostics of the bf16 kernels ("gemm_diag"; 0 = normal)
+  int wst = 1;                   // K = 512 weight-stationary kernel ("gemm_wst")
+  int small_tiles = 0;           // force the 128 x 128 kernel (cfm_op_gemm A/B)
+};
+
+// Per-model kernel tuning (cfm_model_set_option); the defaults are the measured best
+struct Tuning {
+  int gemm_diag = 0, gemm_wst = 1, store_mode = 0, col_group = 0;
+  int attn_reuse = 1;            // ring attention: band subtile carried between key tiles
+  int conv_dot2 = 1;             // conv module: bf16 dot2 kernel (0: per-tap f32 kernel)
+  int conv_dma = 1;              // conv module: LDS-DMA window staging (0: register staging)
+  int dw2_seg = 4;               // front-end dw2: row segments per walk
+  void apply(EpiArgs& e) const {
+    e.diag = gemm_diag;
+    e.wst = gemm_wst;
+    e.store_mode = store_mode;
+    e.col_group = col_group;
+  }
 };
 
 template <typename T>
 int gemm(int epi, int act, const T* A, int lda, const T* W, int ldw, int M, int N, int K, const EpiArgs& ep,
          hipStream_t st);
 
-void gemm_force_small_tiles(int v);
-void gemm_set_variant(int v);
 
 // LayerNorm over d (eps) of f32 rows -> T rows; optional 0/1 row mask on the output.
 // fused residual add of the previous sub-block: x += alpha * ymask[row] * y (y null = none)
@@ -71,18 +88,14 @@ CFM_HD_INLINE int qkv_kv_col(int cc, int which, int dk) { return (cc / dk) * 2 *
 // masked-batch ring kernel (bf16, head dim 64); -1 = shape not eligible
 int chunk_attention_masked_bf16(const bf16* q, const bf16* kv, int kv_rows, const bf16* P, int p_rows,
                                 const float* pos_u, const float* pos_v, const int32_t* desc, int n_chunks, int H,
-                                int C, int W, bf16* out, hipStream_t st, int diag = 0, int p_ld = 0);
+                                int C, int W, bf16* out, hipStream_t st, int diag = 0, int p_ld = 0, int reuse = 1);
 
-// fused FFN (ffn.hip): y = w2 . SiLU(w1 . x + b1) + b2 over a repacked slab stream; -1 = not eligible
-int ffn_fused(const bf16* x, int M, const bf16* wstream, const float* b1, const float* b2, bf16* y, int d, int ff,
-              hipStream_t st);
-void ffn_set_variant(int v);
-void ffn_pack_stream(const float* w1, const float* w2, int d, int ff, uint16_t* out, uint16_t (*to_bf16)(float));
 
 // conv module: depthwise k=15 + bias + LayerNorm + SiLU (conv_module.hip)
 template <typename T>
 int conv_dw_ln_silu(const T* glu, const int32_t* desc, int nblk, int d, const float* wdw_t /*[15][d]*/,
-                    const float* bdw, const float* lnw, const float* lnb, float eps, T* out, hipStream_t st);
+                    const float* bdw, const float* lnw, const float* lnb, float eps, T* out, hipStream_t st,
+                    int dot2 = 1, int dma = 1);
 
 // front-end (frontend.hip): meta rows give (src_row, nvalid) per window at PM_SRC_ROW / PM_NVALID
 template <typename T>
@@ -92,7 +105,8 @@ int frontend_conv0_dw(const float* feats, const int32_t* meta, int meta_stride, 
 // per-channel [w0 taps 0..8 | w1 taps 0..8 | b0 | b1 | pad 2] (FE_WPACK floats) for the bf16 MFMA front-end
 constexpr int FE_WPACK = 24;
 template <typename T>
-int frontend_dw2(const T* in, int nwin, int T2, int d, const float* w, const float* b, T* out, hipStream_t st);
+int frontend_dw2(const T* in, int nwin, int T2, int d, const float* w, const float* b, T* out, hipStream_t st,
+                 int seg = 4);
 
 // misc (misc.hip)
 template <typename T>
@@ -101,6 +115,10 @@ template <typename T>
 int att_cache_in(const float* cache, int L, int row_elems, T* kv, hipStream_t st);
 template <typename T>
 int att_cache_out(const T* kv, int start_row, int L, int row_elems, float* cache, hipStream_t st);
+template <typename T>
+int att_cache_in_hl(const float* cache /*[H][L][2dk]*/, int H, int L, int dk, T* kv, hipStream_t st);
+template <typename T>
+int att_cache_out_hl(const T* kv, int start_row, int H, int L, int dk, float* cache /*[H][L][2dk]*/, hipStream_t st);
 template <typename T>
 int cnn_cache_in(const float* cache /*[d][7]*/, int d, int lorder, T* glu, hipStream_t st);
 template <typename T>

@@ -327,12 +327,9 @@ __global__ __launch_bounds__(512) void conv_dw_ln_silu_dot2_kernel(const bf16* _
 
 template <typename T>
 int conv_dw_ln_silu(const T* glu, const int32_t* desc, int nblk, int d, const float* wdw_t, const float* bdw,
-                    const float* lnw, const float* lnb, float eps, T* out, hipStream_t st) {
+                    const float* lnw, const float* lnb, float eps, T* out, hipStream_t st, int dot2, int dma) {
   if (nblk <= 0) return 0;
-  static int dot2 = -1;   // CFM_CONV_DOT2=0: the per-tap f32 kernel (A/B)
-  if (dot2 < 0) { const char* e = getenv("CFM_CONV_DOT2"); dot2 = e ? atoi(e) : 1; }
-  static int dma = -1;    // CFM_CONV_DMA=0: stage the window through registers (A/B)
-  if (dma < 0) { const char* e = getenv("CFM_CONV_DMA"); dma = e ? atoi(e) : 1; }
+  // dot2 = 0: the per-tap f32 kernel; dma = 0: stage the window through registers (A/B, model options)
   if constexpr (std::is_same<T, bf16>::value) {
     if (dot2) {
       if (d == 128) hipLaunchKernelGGL((conv_dw_ln_silu_dot2_kernel<2>), dim3(nblk), dim3(512), 0, st, glu, desc, wdw_t, bdw, lnw, lnb, eps, out, dma);
@@ -359,8 +356,8 @@ int conv_dw_ln_silu(const T* glu, const int32_t* desc, int nblk, int d, const fl
 }
 
 template int conv_dw_ln_silu<float>(const float*, const int32_t*, int, int, const float*, const float*, const float*,
-                                    const float*, float, float*, hipStream_t);
+                                    const float*, float, float*, hipStream_t, int, int);
 template int conv_dw_ln_silu<bf16>(const bf16*, const int32_t*, int, int, const float*, const float*, const float*,
-                                   const float*, float, bf16*, hipStream_t);
+                                   const float*, float, bf16*, hipStream_t, int, int);
 
 }  // namespace cfm

@@ -310,13 +310,13 @@ int frontend_conv0_dw(const float* feats, const int32_t* meta, int meta_stride, 
 }
 
 template <typename T>
-int frontend_dw2(const T* in, int nwin, int T2, int d, const float* w, const float* b, T* out, hipStream_t st) {
+int frontend_dw2(const T* in, int nwin, int T2, int d, const float* w, const float* b, T* out, hipStream_t st,
+                 int seg) {
   const int T3 = (T2 - 3) / 2 + 1;
   if (d % 8) return (int)hipErrorInvalidValue;
   const size_t total = (size_t)nwin * FE_F3 * (d / 8);
   if (total == 0 || T3 <= 0) return 0;
-  static int seg = 0;   // CFM_DW2_SEG: row segments per walk (A/B)
-  if (!seg) { const char* e = getenv("CFM_DW2_SEG"); seg = e ? std::max(1, atoi(e)) : FE_DW2_SEG; }
+  seg = std::max(1, seg);   // row segments per walk ("dw2_seg" model option)
   hipLaunchKernelGGL((fe_dw2_kernel<T>), dim3((unsigned)((total + 255) / 256), std::min(seg, T3)), dim3(256), 0, st, in,
                      nwin, T2, T3, d, w, b, out);
   CFM_CHECK_LAUNCH();
@@ -327,7 +327,7 @@ template int frontend_conv0_dw<float>(const float*, const int32_t*, int, int, in
                                       const float*, const float*, const float*, const float*, const float*, int, float*, hipStream_t);
 template int frontend_conv0_dw<bf16>(const float*, const int32_t*, int, int, int, const float*, const float*,
                                      const float*, const float*, const float*, const float*, const float*, int, bf16*, hipStream_t);
-template int frontend_dw2<float>(const float*, int, int, int, const float*, const float*, float*, hipStream_t);
-template int frontend_dw2<bf16>(const bf16*, int, int, int, const float*, const float*, bf16*, hipStream_t);
+template int frontend_dw2<float>(const float*, int, int, int, const float*, const float*, float*, hipStream_t, int);
+template int frontend_dw2<bf16>(const bf16*, int, int, int, const float*, const float*, bf16*, hipStream_t, int);
 
 }  // namespace cfm

@@ -201,21 +201,11 @@ static int launch(const T* A, int lda, const T* W, int ldw, int M, int N, int K,
 int gemm_bf16_big(int epi, int act, const bf16* A, int lda, const bf16* W, int ldw, int M, int N, int K,
                   const EpiArgs& ep, hipStream_t st);
 
-static int g_force_small = -1;
-static bool use_big_tiles() {
-  if (g_force_small < 0) {
-    const char* e = getenv("CFM_GEMM_SMALL_TILES");
-    g_force_small = (e && e[0] == '1') ? 1 : 0;
-  }
-  return g_force_small == 0;
-}
-void gemm_force_small_tiles(int v) { g_force_small = v ? 1 : 0; }
-
 template <typename T>
 int gemm(int epi, int act, const T* A, int lda, const T* W, int ldw, int M, int N, int K, const EpiArgs& ep,
          hipStream_t st) {
   if constexpr (sizeof(T) == 2) {
-    if (use_big_tiles()) {
+    if (!ep.small_tiles) {
       const int r = gemm_bf16_big(epi, act, A, lda, W, ldw, M, N, K, ep, st);
       if (r != -1) return r;
     }

@@ -234,442 +234,8 @@ CFM_DEV void seed_bias_smem(f32x4 (&acc)[4][8], const float* bias, int col0, int
   }
 }
 
-template <int EPI> struct EpiStores { static constexpr int n = 16; };   // bf16 out: 2 x 8 16-B stores
-template <> struct EpiStores<EPI_STORE_F32> { static constexpr int n = 32; };
-template <> struct EpiStores<EPI_GLU> { static constexpr int n = 8; };
-
-#define CFM_VMCNT(N) asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory")
-
-template <int EPI, int ACT, int DIAG = 0>
-__global__ __launch_bounds__(512, 1) void gemm_bf16_ring_kernel(const bf16* __restrict__ A, int lda,
-                                                                const bf16* __restrict__ W, int ldw, int M, int N,
-                                                                int K, EpiArgs ep) {
-  __shared__ __attribute__((aligned(16))) char smem[5 * 32768];
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wm = wid >> 2, wn = wid & 3;
-  const int fr = lane & 15, g = lane >> 4;
-  const int wid_u = __builtin_amdgcn_readfirstlane(wid);
-  const int grp = wid_u >> 2;
-  const int wn_u = wid_u & 3;
-
-  const int nbn = N >> 8, nbm = (M + 255) >> 8, T = nbn * nbm;
-  const int G = gridDim.x;
-  int t_first, t_step, t_end;
-  if (G >= T) {
-    const int b = blockIdx.x, xcd = b & 7, q8 = T >> 3, r8 = T & 7;
-    t_first = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b >> 3);
-    t_step = T;
-    t_end = T;
-  } else {
-    const int xcd = blockIdx.x & 7, j = blockIdx.x >> 3, per = T >> 3, rem = T & 7;
-    const int start = xcd * per + min(xcd, rem), size = per + (xcd < rem ? 1 : 0);
-    t_first = start + j;
-    t_step = G >> 3;
-    t_end = start + size;
-  }
-  if (t_first >= t_end) return;
-  const int nk = K >> 5;                                          // K-32 steps per tile (>= 4)
-  const int n_mine = (t_end - t_first + t_step - 1) / t_step;    // tiles of this block
-  const int Y = n_mine * nk;                                      // ring steps
-
-  // ---- per-lane DMA offsets: wave w stages rows 32w + 16i + lane/4 of A and W, chunk pre-swizzled
-  const int drow = lane >> 2;
-  const int dch = (lane & 3) ^ ((4 - (lane >> 4)) & 3);
-  int voffA[2], voffW[2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int row = 32 * wid + 16 * i + drow;
-    voffA[i] = (row * lda + 8 * dch) * 2;
-    voffW[i] = (row * ldw + 8 * dch) * 2;
-  }
-  // issue cursor: step (it, ik) with descriptors of tile it
-  int it = t_first, ik = 0;
-  __amdgpu_buffer_rsrc_t rA, rW;
-  auto set_rsrc = [&](int t) {
-    const int tm = t / nbn, tn = t - tm * nbn;
-    const int rows = min(256, M - tm * 256);
-    rA = __builtin_amdgcn_make_buffer_rsrc((void*)(A + (size_t)tm * 256 * lda), (short)0, rows * lda * 2, 0x00020000);
-    rW = __builtin_amdgcn_make_buffer_rsrc((void*)(W + (size_t)tn * 256 * ldw), (short)0, 256 * ldw * 2, 0x00020000);
-  };
-  auto issue = [&](int slot) {
-    char* sb = smem + slot * 32768 + wid_u * 2048;
-    const int soff = ik * 64;
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (__attribute__((address_space(3))) void*)(sb + i * 1024), 16,
-                                               voffA[i], soff, 0, 0);
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rW, (__attribute__((address_space(3))) void*)(sb + 16384 + i * 1024),
-                                               16, voffW[i], soff, 0, 0);
-    if (++ik == nk) {
-      ik = 0;
-      it += t_step;
-      if (it < t_end) set_rsrc(it);
-    }
-  };
-
-  f32x4 acc[4][8];
-  // fragment read offsets: row (16-row block base) + fr, chunk g at its swizzled position
-  const int cpos = (g ^ ((4 - ((fr >> 2) & 3)) & 3)) << 4;
-  const unsigned lds_base = (unsigned)(size_t)(__attribute__((address_space(3))) char*)smem;
-  const unsigned offW = 16384 + (wn * 64 + fr) * 64 + cpos;
-  const unsigned offA = (wm * 128 + fr) * 64 + cpos;
-  bf16x8 wf[4], af[8];
-
-  // prologue: slots 0..3
-  set_rsrc(it);
-#pragma unroll
-  for (int p = 0; p < 4; ++p)
-    if (p < Y) issue(p);
-  if (Y >= 4) CFM_VMCNT(12); else CFM_VMCNT(0);
-  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-  if (grp == 1) asm volatile("s_barrier" ::: "memory");
-
-  int epi_t = -1;
-  bool epi_full = false;   // the last epilogue stored every row (counted stores outstanding)
-  int y = 0, slot = 0, slot4 = 4;
-  for (int t = t_first; t < t_end; t += t_step) {
-    for (int kc = 0; kc < nk; ++kc, ++y) {
-      // ================= LOAD segment
-      const unsigned sa = lds_base + (unsigned)slot * 32768u;
-      const unsigned wa = sa + offW, aa = sa + offA;
-      wf[0] = lds_read_b128<0>(wa); wf[1] = lds_read_b128<1024>(wa);
-      wf[2] = lds_read_b128<2048>(wa); wf[3] = lds_read_b128<3072>(wa);
-      af[0] = lds_read_b128<0>(aa); af[1] = lds_read_b128<1024>(aa);
-      af[2] = lds_read_b128<2048>(aa); af[3] = lds_read_b128<3072>(aa);
-      af[4] = lds_read_b128<4096>(aa); af[5] = lds_read_b128<5120>(aa);
-      af[6] = lds_read_b128<6144>(aa); af[7] = lds_read_b128<7168>(aa);
-      if (y + 4 < Y) {
-        if (DIAG != 2) issue(slot4);
-        // slot y+1 landed: younger are y+2..y+4 (12) and, for 3 steps after a full epilogue, its stores
-        if (DIAG != 2 && epi_full && kc >= 1 && kc <= 3) {
-          if constexpr (EpiStores<EPI>::n == 32) CFM_VMCNT(44);
-          else if constexpr (EpiStores<EPI>::n == 16) CFM_VMCNT(28);
-          else CFM_VMCNT(20);
-        } else if (DIAG != 2) {
-          CFM_VMCNT(12);
-        }
-      } else {
-        CFM_VMCNT(0);
-      }
-      if (kc == 0) {
-        epi_full = false;
-        if (epi_t >= 0) {
-          const int etm = epi_t / nbn;
-          tile_epilogue<EPI, DIAG == 4 ? ACT_NONE : ACT, DIAG == 3>(acc, etm, epi_t - etm * nbn, wm, wn, fr, g, M, ep);
-          epi_full = DIAG != 3 && etm * 256 + 256 <= M;
-          epi_t = -1;
-        }
-        seed_bias_smem(acc, ep.bias, (t % nbn) * 256 + wn_u * 64, g);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-      __builtin_amdgcn_sched_barrier(0);
-      // ================= MFMA segment
-      if constexpr (DIAG == 1) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) asm volatile("" ::"v"(wf[i]));
-#pragma unroll
-        for (int j = 0; j < 8; ++j) asm volatile("" ::"v"(af[j]));
-      } else {
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < 8; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[i], af[j], acc[i][j], 0, 0, 0);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      asm volatile("s_barrier" ::: "memory");
-      __builtin_amdgcn_sched_barrier(0);
-      slot = slot == 4 ? 0 : slot + 1;
-      slot4 = slot4 == 4 ? 0 : slot4 + 1;
-    }
-    epi_t = t;
-  }
-  if (epi_t >= 0) tile_epilogue<EPI, DIAG == 4 ? ACT_NONE : ACT, DIAG == 3>(acc, epi_t / nbn, epi_t % nbn, wm, wn, fr, g, M, ep);
-  if (grp == 0) asm volatile("s_barrier" ::: "memory");
-}
-
-// =====================================================================================
-// Spread-store variant of the ring kernel (bf16 outputs, K % 512 == 0).
-//
-// The bunched tile epilogue issues 16 KiB of stores per wave in one segment; the CU's store
-// path takes them at ~10-20 B/cycle, so the partner wave group idles at the next barrier for
-// several MFMA segments (no-store diagnostic: FFN w1 582 -> 427 us).  Here the finished tile
-// is packed to bf16 at once (64 VGPRs per lane: activation, permlane16 swap into 16-B row
-// pieces) and its 16 stores are issued one per load segment across the next tile's first 16
-// K-steps, beside the other group's MFMAs.  Stores go through a buffer descriptor per output
-// block, so rows past M are dropped by the range check while the instruction still issues:
-// every load segment's store count is exact and the DMA waits stay counted
-// (vmcnt = 12 + stores issued in the three previous load segments).
-// =====================================================================================
-// entries kept packed in registers and stored one per load segment (the rest of the tile is stored at
-// once at the tile end: VGPR budget 2 waves/SIMD = 256 with the 128-register accumulator)
-// s_waitcnt vmcnt(n) for the counts the spread kernel uses (n folds to a constant per unrolled step)
-CFM_DEV void wait_vm(int n) {
-  switch (n) {
-#define CFM_VMCASE(N) case N: CFM_VMCNT(N); break;
-    CFM_VMCASE(13) CFM_VMCASE(14) CFM_VMCASE(15) CFM_VMCASE(16) CFM_VMCASE(17) CFM_VMCASE(18) CFM_VMCASE(19)
-    CFM_VMCASE(20) CFM_VMCASE(21) CFM_VMCASE(22) CFM_VMCASE(23) CFM_VMCASE(24) CFM_VMCASE(25) CFM_VMCASE(26)
-    CFM_VMCASE(27) CFM_VMCASE(28) CFM_VMCASE(29) CFM_VMCASE(30) CFM_VMCASE(31)
-#undef CFM_VMCASE
-    default: CFM_VMCNT(12); break;
-  }
-}
-
-
-template <int EPI> struct PendN {
-  static constexpr int total = EPI == EPI_GLU ? 8 : 16;   // 16-B stores per wave per tile
-  static constexpr int n = 4;                              // of which spread (the rest at the tile end)
-};
-
-// packs the finished tile: GLU -> pend[0..7] (one 16-B store per row block j); STORE / QKV:
-// half p = 0 -> pend[0..7], half p = 1 stored now through rO[1]
 template <int EPI, int ACT>
-CFM_DEV void pack_tile(f32x4 (&acc)[4][8], u32x4 (&pend)[PendN<EPI>::n], __amdgpu_buffer_rsrc_t r0,
-                       __amdgpu_buffer_rsrc_t r1, int ld0, int ld1, int rowq, int col_g) {
-  constexpr int NP = PendN<EPI>::n;
-  if constexpr (EPI == EPI_GLU) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      u32x2_t o[2];
-#pragma unroll
-      for (int p = 0; p < 2; ++p) {
-        const f32x4 a = acc[2 * p][j], gt = acc[2 * p + 1][j];
-        o[p] = (u32x2_t){pack_bf16x2(a[0] * fast_sigmoid(gt[0]), a[1] * fast_sigmoid(gt[1])),
-                         pack_bf16x2(a[2] * fast_sigmoid(gt[2]), a[3] * fast_sigmoid(gt[3]))};
-      }
-      const auto s0 = __builtin_amdgcn_permlane16_swap(o[0][0], o[1][0], false, false);
-      const auto s1 = __builtin_amdgcn_permlane16_swap(o[0][1], o[1][1], false, false);
-      const u32x4 v = (u32x4){s0[0], s1[0], s0[1], s1[1]};
-      if (j < NP) {
-        pend[j] = v;
-      } else {
-        int r = rowq;
-        asm volatile("" : "+v"(r));
-        __builtin_amdgcn_raw_buffer_store_b128(v, r0, ((r + 16 * j) * ld0 + col_g) * 2, 0, 0);
-      }
-    }
-  } else {
-#pragma unroll
-    for (int p = 1; p >= 0; --p)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const f32x4 v0 = act4<ACT>(acc[2 * p][j]), v1 = act4<ACT>(acc[2 * p + 1][j]);
-        const auto s0 = __builtin_amdgcn_permlane16_swap(pack_bf16x2(v0[0], v0[1]), pack_bf16x2(v1[0], v1[1]), false, false);
-        const auto s1 = __builtin_amdgcn_permlane16_swap(pack_bf16x2(v0[2], v0[3]), pack_bf16x2(v1[2], v1[3]), false, false);
-        const u32x4 v = (u32x4){s0[0], s1[0], s0[1], s1[1]};
-        if (p == 0 && j < NP) {
-          pend[j] = v;
-        } else {
-          int r = rowq;
-          asm volatile("" : "+v"(r));   // recompute the offset here: hoisted, 16 such offsets spill
-          __builtin_amdgcn_raw_buffer_store_b128(v, p ? r1 : r0, ((r + 16 * j) * (p ? ld1 : ld0) + col_g) * 2, 0, 0);
-        }
-      }
-  }
-}
-
-template <int EPI, int ACT>
-__global__ __launch_bounds__(512, 1) void gemm_bf16_spread_kernel(const bf16* __restrict__ A, int lda,
-                                                                  const bf16* __restrict__ W, int ldw, int M, int N,
-                                                                  int K, EpiArgs ep) {
-  __shared__ __attribute__((aligned(16))) char smem[5 * 32768];
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wm = wid >> 2, wn = wid & 3;
-  const int fr = lane & 15, g = lane >> 4;
-  const int wid_u = __builtin_amdgcn_readfirstlane(wid);
-  const int grp = wid_u >> 2;
-  const int wn_u = wid_u & 3;
-  constexpr int NP = PendN<EPI>::n;
-
-  const int nbn = N >> 8, nbm = (M + 255) >> 8, T = nbn * nbm;
-  const int G = gridDim.x;
-  int t_first, t_step, t_end;
-  if (G >= T) {
-    const int b = blockIdx.x, xcd = b & 7, q8 = T >> 3, r8 = T & 7;
-    t_first = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b >> 3);
-    t_step = T;
-    t_end = T;
-  } else {
-    const int xcd = blockIdx.x & 7, j = blockIdx.x >> 3, per = T >> 3, rem = T & 7;
-    const int start = xcd * per + min(xcd, rem), size = per + (xcd < rem ? 1 : 0);
-    t_first = start + j;
-    t_step = G >> 3;
-    t_end = start + size;
-  }
-  if (t_first >= t_end) return;
-  const int nk = K >> 5;                                          // K-32 steps per tile, % 16 == 0
-  const int n_mine = (t_end - t_first + t_step - 1) / t_step;
-  const int Y = n_mine * nk;
-
-  const int drow = lane >> 2;
-  const int dch = (lane & 3) ^ ((4 - (lane >> 4)) & 3);
-  int voffA[2], voffW[2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int row = 32 * wid + 16 * i + drow;
-    voffA[i] = (row * lda + 8 * dch) * 2;
-    voffW[i] = (row * ldw + 8 * dch) * 2;
-  }
-  int it = t_first, ik = 0;
-  __amdgpu_buffer_rsrc_t rA, rW;
-  auto set_rsrc = [&](int t) {
-    const int tm = t / nbn, tn = t - tm * nbn;
-    const int rows = min(256, M - tm * 256);
-    rA = __builtin_amdgcn_make_buffer_rsrc((void*)(A + (size_t)tm * 256 * lda), (short)0, rows * lda * 2, 0x00020000);
-    rW = __builtin_amdgcn_make_buffer_rsrc((void*)(W + (size_t)tn * 256 * ldw), (short)0, 256 * ldw * 2, 0x00020000);
-  };
-  auto issue = [&](int slot) {
-    char* sb = smem + slot * 32768 + wid_u * 2048;
-    const int soff = ik * 64;
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (__attribute__((address_space(3))) void*)(sb + i * 1024), 16,
-                                               voffA[i], soff, 0, 0);
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rW, (__attribute__((address_space(3))) void*)(sb + 16384 + i * 1024),
-                                               16, voffW[i], soff, 0, 0);
-    if (++ik == nk) {
-      ik = 0;
-      it += t_step;
-      if (it < t_end) set_rsrc(it);
-    }
-  };
-
-  // output descriptors of the pending (packed) tile, one per 32-column half p (GLU: one)
-  __amdgpu_buffer_rsrc_t rO[2];
-  int ldO[2];
-  auto set_out = [&](int t) {
-    const int tm = t / nbn, tn = t - tm * nbn;
-    const int rows = min(256, M - tm * 256);
-    const int nw = tn * 256 + wn_u * 64;
-#pragma unroll
-    for (int p = 0; p < 2; ++p) {
-      bf16* base;
-      int ld;
-      if constexpr (EPI == EPI_GLU) {
-        base = reinterpret_cast<bf16*>(ep.out) + (size_t)(ep.row_off + tm * 256) * ep.ldo + nw / 2;
-        ld = ep.ldo;
-      } else if constexpr (EPI == EPI_QKV) {
-        const int n = nw + 32 * p, d = ep.d;
-        if (n < d) {
-          base = reinterpret_cast<bf16*>(ep.out) + (size_t)tm * 256 * d + n;
-          ld = d;
-        } else {
-          const int c2 = n - d, which = c2 >= d ? 1 : 0, cc = c2 - which * d;
-          base = reinterpret_cast<bf16*>(ep.out2) + (size_t)(ep.row_off + tm * 256) * 2 * d + qkv_kv_col(cc, which, ep.dk);
-          ld = 2 * d;
-        }
-      } else {
-        base = reinterpret_cast<bf16*>(ep.out) + (size_t)(ep.row_off + tm * 256) * ep.ldo + nw + 32 * p;
-        ld = ep.ldo;
-      }
-      rO[p] = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, rows * ld * 2, 0x00020000);
-      ldO[p] = ld;
-    }
-  };
-  const int col_g = 16 * (g & 1) + 8 * (g >> 1);
-  const int rowq = wm * 128 + fr;
-
-  f32x4 acc[4][8];
-  u32x4 pend[NP];
-  const int cpos = (g ^ ((4 - ((fr >> 2) & 3)) & 3)) << 4;
-  const unsigned lds_base = (unsigned)(size_t)(__attribute__((address_space(3))) char*)smem;
-  const unsigned offW = 16384 + (wn * 64 + fr) * 64 + cpos;
-  const unsigned offA = (wm * 128 + fr) * 64 + cpos;
-  bf16x8 wf[4], af[8];
-
-  set_rsrc(it);
-#pragma unroll
-  for (int p = 0; p < 4; ++p)
-    if (p < Y) issue(p);
-  if (Y >= 4) CFM_VMCNT(12); else CFM_VMCNT(0);
-  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-  if (grp == 1) asm volatile("s_barrier" ::: "memory");
-
-  int epi_t = -1;
-  bool pend_on = false;   // this tile's first 16-step block stores the previous tile (packed at e = 0)
-  int y = 0, slot = 0, slot4 = 4;
-  for (int t = t_first; t < t_end; t += t_step) {
-    for (int kc0 = 0; kc0 < nk; kc0 += 16) {
-#pragma unroll
-      for (int e = 0; e < 16; ++e, ++y) {
-        // ================= LOAD segment
-        if (e == 0 && kc0 == 0) {
-          pend_on = false;
-          if (epi_t >= 0) {
-            set_out(epi_t);
-            pack_tile<EPI, ACT>(acc, pend, rO[0], rO[1], ldO[0], ldO[1], rowq, col_g);
-            pend_on = true;
-            epi_t = -1;
-          }
-          seed_bias_smem(acc, ep.bias, (t % nbn) * 256 + wn_u * 64, g);
-        }
-        __builtin_amdgcn_sched_barrier(0);   // keep the pack's temporaries out of the fragment reads
-        const unsigned sa = lds_base + (unsigned)slot * 32768u;
-        const unsigned wa = sa + offW, aa = sa + offA;
-        wf[0] = lds_read_b128<0>(wa); wf[1] = lds_read_b128<1024>(wa);
-        wf[2] = lds_read_b128<2048>(wa); wf[3] = lds_read_b128<3072>(wa);
-        af[0] = lds_read_b128<0>(aa); af[1] = lds_read_b128<1024>(aa);
-        af[2] = lds_read_b128<2048>(aa); af[3] = lds_read_b128<3072>(aa);
-        af[4] = lds_read_b128<4096>(aa); af[5] = lds_read_b128<5120>(aa);
-        af[6] = lds_read_b128<6144>(aa); af[7] = lds_read_b128<7168>(aa);
-        if (y + 4 < Y) {
-          issue(slot4);
-          // slot y+1 landed.  Younger than its DMA (issued 3 segments back, before that segment's
-          // spread store): 12 DMA + the spread stores of segments y-3..y-1 + the 8 tile-end stores
-          // if the tile was packed in segments y-2..y.  Spread stores run at e = 0..7 of a packed
-          // tile's first 16-step block, so the count is a constant per unrolled e.
-          const bool sp = pend_on && kc0 == 0;
-          const int n_sp = !sp ? 0 : max(0, min(e, NP) - max(0, e - 3));
-          const int n_b = (sp && e <= 2) ? PendN<EPI>::total - NP : 0;
-          wait_vm(12 + n_sp + n_b);
-        } else {
-          CFM_VMCNT(0);
-        }
-        if (e < NP && pend_on && kc0 == 0) {
-          int r = rowq;
-          asm volatile("" : "+v"(r));   // (see pack_tile)
-          __builtin_amdgcn_raw_buffer_store_b128(pend[e], rO[0], ((r + 16 * e) * ldO[0] + col_g) * 2, 0, 0);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        __builtin_amdgcn_sched_barrier(0);
-        // ================= MFMA segment
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < 8; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[i], af[j], acc[i][j], 0, 0, 0);
-        __builtin_amdgcn_sched_barrier(0);
-        asm volatile("s_barrier" ::: "memory");
-        __builtin_amdgcn_sched_barrier(0);
-        slot = slot == 4 ? 0 : slot + 1;
-        slot4 = slot4 == 4 ? 0 : slot4 + 1;
-      }
-    }
-    epi_t = t;
-  }
-  if (epi_t >= 0) tile_epilogue<EPI, ACT>(acc, epi_t / nbn, epi_t % nbn, wm, wn, fr, g, M, ep);
-  if (grp == 0) asm volatile("s_barrier" ::: "memory");
-}
-
-// A/B switch for in-process experiments ("gemm_variant" model option): 5 = s_setprio(1) around each
-// MFMA segment, 6 = static priority 1 for the later wave group (MI355X_MICROARCH.md, two waves per SIMD)
-static int g_gemm_variant = 0;
-void gemm_set_variant(int v) { g_gemm_variant = v; }
-
-static int ring_mode() {
-  static int v = -1;
-  if (v < 0) { const char* e = getenv("CFM_GEMM_RING"); v = e ? atoi(e) : 0; }
-  return v;
-}
-
-template <int EPI, int ACT>
-static int launch256(const bf16* A, int lda, const bf16* W, int ldw, int M, int N, int K, const EpiArgs& ep_in,
+static int launch256(const bf16* A, int lda, const bf16* W, int ldw, int M, int N, int K, const EpiArgs& ep,
                      hipStream_t st) {
   const int tiles = ((M + 255) / 256) * (N / 256);
   static int n_cu = 0;
@@ -680,50 +246,18 @@ static int launch256(const bf16* A, int lda, const bf16* W, int ldw, int M, int 
     n_cu = (n_cu + 7) / 8 * 8;
   }
   const int grid = tiles <= n_cu ? tiles : n_cu;   // persistent: one 512-thread block per CU
-  static int diag_env = -1;
-  if (diag_env < 0) { const char* e = getenv("CFM_GEMM_DIAG"); diag_env = e ? atoi(e) : 0; }
-  const int diag = g_gemm_variant ? g_gemm_variant : diag_env;
-  EpiArgs ep = ep_in;
-  static int store_env = -1;
-  if (store_env < 0) { const char* e = getenv("CFM_STORE_MODE"); store_env = e ? atoi(e) : 0; }
-  if (store_env) ep.store_mode = store_env;
-  static int cg_env = -1;
-  if (cg_env < 0) { const char* e = getenv("CFM_GEMM_COLGROUP"); cg_env = e ? atoi(e) : 0; }
-  if (cg_env) ep.col_group = cg_env;
-  if constexpr (EPI == EPI_STORE || EPI == EPI_QKV || EPI == EPI_GLU) {
-    if (ring_mode() == 2 && diag == 0 && K % 512 == 0 && (size_t)256 * ldw * 2 < (1u << 31) &&
-        (size_t)256 * lda * 2 < (1u << 31)) {
-      hipLaunchKernelGGL((gemm_bf16_spread_kernel<EPI, ACT>), dim3(grid), dim3(512), 0, st, A, lda, W, ldw, M, N, K, ep);
-      CFM_CHECK_LAUNCH();
-      return 0;
-    }
+  // ep.diag (timing diagnostics, model option "gemm_diag"): 1 no MFMA, 2 no DMA in the loop, 3 no
+  // epilogue, 5 / 6 wave-group priorities
+#define G256(D) hipLaunchKernelGGL((gemm_bf16_256_kernel<EPI, ACT, D>), dim3(grid), dim3(512), 0, st, A, lda, W, ldw, M, N, K, ep)
+  switch (ep.diag) {
+    case 1: G256(1); break;
+    case 2: G256(2); break;
+    case 3: G256(3); break;
+    case 5: G256(5); break;
+    case 6: G256(6); break;
+    default: G256(0); break;
   }
-  if constexpr (EPI != EPI_RESID) {
-    if (ring_mode() == 1 && K % 128 == 0 && (size_t)256 * ldw * 2 < (1u << 31) && (size_t)256 * lda * 2 < (1u << 31)) {
-      if (diag == 1)
-        hipLaunchKernelGGL((gemm_bf16_ring_kernel<EPI, ACT, 1>), dim3(grid), dim3(512), 0, st, A, lda, W, ldw, M, N, K, ep);
-      else if (diag == 3)
-        hipLaunchKernelGGL((gemm_bf16_ring_kernel<EPI, ACT, 3>), dim3(grid), dim3(512), 0, st, A, lda, W, ldw, M, N, K, ep);
-      else if (diag == 4)
-        hipLaunchKernelGGL((gemm_bf16_ring_kernel<EPI, ACT, 4>), dim3(grid), dim3(512), 0, st, A, lda, W, ldw, M, N, K, ep);
-      else if (diag == 2)
-        hipLaunchKernelGGL((gemm_bf16_ring_kernel<EPI, ACT, 2>), dim3(grid), dim3(512), 0, st, A, lda, W, ldw, M, N, K, ep);
-      else
-        hipLaunchKernelGGL((gemm_bf16_ring_kernel<EPI, ACT, 0>), dim3(grid), dim3(512), 0, st, A, lda, W, ldw, M, N, K, ep);
-      CFM_CHECK_LAUNCH();
-      return 0;
-    }
-  }
-  if (diag == 1)
-    hipLaunchKernelGGL((gemm_bf16_256_kernel<EPI, ACT, 1>), dim3(grid), dim3(512), 0, st, A, lda, W, ldw, M, N, K, ep);
-  else if (diag == 2)
-    hipLaunchKernelGGL((gemm_bf16_256_kernel<EPI, ACT, 2>), dim3(grid), dim3(512), 0, st, A, lda, W, ldw, M, N, K, ep);
-  else if (diag == 5)
-    hipLaunchKernelGGL((gemm_bf16_256_kernel<EPI, ACT, 5>), dim3(grid), dim3(512), 0, st, A, lda, W, ldw, M, N, K, ep);
-  else if (diag == 6)
-    hipLaunchKernelGGL((gemm_bf16_256_kernel<EPI, ACT, 6>), dim3(grid), dim3(512), 0, st, A, lda, W, ldw, M, N, K, ep);
-  else
-    hipLaunchKernelGGL((gemm_bf16_256_kernel<EPI, ACT, 0>), dim3(grid), dim3(512), 0, st, A, lda, W, ldw, M, N, K, ep);
+#undef G256
   CFM_CHECK_LAUNCH();
   return 0;
 }
@@ -735,9 +269,8 @@ int gemm_bf16_wst(int epi, int act, const bf16* A, int lda, const bf16* W, int l
 int gemm_bf16_big(int epi, int act, const bf16* A, int lda, const bf16* W, int ldw, int M, int N, int K,
                   const EpiArgs& ep, hipStream_t st) {
   if (M <= 0) return 0;
-  {
-    EpiArgs e2 = ep;
-    const int r = gemm_bf16_wst(epi, act, A, lda, W, ldw, M, N, K, e2, st);   // K = 512: weight tile in registers
+  if (ep.wst) {
+    const int r = gemm_bf16_wst(epi, act, A, lda, W, ldw, M, N, K, ep, st);   // K = 512: weight tile in registers
     if (r != -1) return r;
   }
   if (N % 256 || K % 64 || lda % 8 || ldw % 8) return -1;

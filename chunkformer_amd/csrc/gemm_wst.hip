@@ -398,12 +398,6 @@ __global__ __launch_bounds__(256, 1) void gemm_wsp_kernel(const bf16* __restrict
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
 }
 
-static int wst_enabled() {
-  static int v = -1;
-  if (v < 0) { const char* e = getenv("CFM_GEMM_WST"); v = e ? atoi(e) : 1; }
-  return v;
-}
-
 template <int EPI, int ACT>
 static int launch_wst(const bf16* A, int lda, const bf16* W, int ldw, int M, int N, const EpiArgs& ep,
                       hipStream_t st) {
@@ -414,15 +408,13 @@ static int launch_wst(const bf16* A, int lda, const bf16* W, int ldw, int M, int
     if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0) n_cu = 256;
     n_cu = n_cu / 8 * 8;
   }
-  static int diag = -1;
-  if (diag < 0) { const char* e = getenv("CFM_GEMM_DIAG"); diag = e ? atoi(e) : 0; }
   // 32-bit buffer-store offsets: every output row offset must stay below 2^31 bytes
   const size_t ld = EPI == EPI_QKV ? 2 * (size_t)ep.d : (size_t)ep.ldo;
   if ((size_t)M * ld * 2 >= (1ull << 31)) return -1;
 #define WSP_LAUNCH(D) hipLaunchKernelGGL((gemm_wsp_kernel<EPI, ACT, D>), dim3(n_cu), dim3(256), 0, st, A, lda, W, ldw, M, N, ep)
-  // DIAG (timing experiments only, CFM_GEMM_DIAG): 1 = no MFMAs, 2 = no DMA wait (stale LDS),
+  // DIAG (timing experiments only, model option "gemm_diag"): 1 = no MFMAs, 2 = no DMA wait (stale LDS),
   // 3 = no epilogue (re-seeds only), 5 = no stores, 8 / 9 = nt / sc1 store policy
-  switch (diag) {
+  switch (ep.diag) {
     case 1: WSP_LAUNCH(1); break;
     case 2: WSP_LAUNCH(2); break;
     case 3: WSP_LAUNCH(3); break;
@@ -439,7 +431,7 @@ static int launch_wst(const bf16* A, int lda, const bf16* W, int ldw, int M, int
 // -1 = not eligible (caller uses the 256 x 256 kernel)
 int gemm_bf16_wst(int epi, int act, const bf16* A, int lda, const bf16* W, int ldw, int M, int N, int K,
                   const EpiArgs& ep, hipStream_t st) {
-  if (!wst_enabled() || K != WST_K || N % 256 || lda % 8 || ldw % 8 || M <= 0) return -1;
+  if (K != WST_K || N % 256 || lda % 8 || ldw % 8 || M <= 0) return -1;
   // enough rows for every CU of an XCD's column tiles to own several tiles
   if ((M + WST_MT - 1) / WST_MT < 8 * 32 * 2) return -1;
   if (N / 256 > 32) return -1;

@@ -50,6 +50,39 @@ int att_cache_out(const T* kv, int start_row, int L, int row_elems, float* cache
   return 0;
 }
 
+// forward_chunk attention cache [H][L][2dk] (head-major, encoder.py:310-385 layout
+// [n_layers, batch, head, cache_t, 2dk]) <-> KV stream rows [t][H][2dk]
+template <typename T, bool IN>
+__global__ void att_cache_hl_kernel(float* cache, int H, int L, int dk2, T* kv) {
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  const size_t n = (size_t)H * L * dk2;
+  if (i >= n) return;
+  const int e = (int)(i % dk2);
+  const int t = (int)((i / dk2) % L);
+  const int h = (int)(i / ((size_t)dk2 * L));
+  T* r = kv + ((size_t)t * H + h) * dk2 + e;
+  if (IN) *r = from_f32<T>(cache[i]);
+  else cache[i] = to_f32(*r);
+}
+template <typename T>
+int att_cache_in_hl(const float* cache, int H, int L, int dk, T* kv, hipStream_t st) {
+  const size_t n = (size_t)H * L * 2 * dk;
+  if (!n) return 0;
+  hipLaunchKernelGGL((att_cache_hl_kernel<T, true>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,
+                     const_cast<float*>(cache), H, L, 2 * dk, kv);
+  CFM_CHECK_LAUNCH();
+  return 0;
+}
+template <typename T>
+int att_cache_out_hl(const T* kv, int start_row, int H, int L, int dk, float* cache, hipStream_t st) {
+  const size_t n = (size_t)H * L * 2 * dk;
+  if (!n) return 0;
+  hipLaunchKernelGGL((att_cache_hl_kernel<T, false>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, cache,
+                     H, L, 2 * dk, const_cast<T*>(kv) + (size_t)start_row * H * 2 * dk);
+  CFM_CHECK_LAUNCH();
+  return 0;
+}
+
 // conv cache [d][lorder] (channel-major, convolution.py:216-231) <-> GLU stream rows [t][d]
 template <typename T, bool IN>
 __global__ void cnn_cache_kernel(float* cache, int d, int lorder, T* glu) {
@@ -131,6 +164,10 @@ template int att_cache_in<float>(const float*, int, int, float*, hipStream_t);
 template int att_cache_in<bf16>(const float*, int, int, bf16*, hipStream_t);
 template int att_cache_out<float>(const float*, int, int, int, float*, hipStream_t);
 template int att_cache_out<bf16>(const bf16*, int, int, int, float*, hipStream_t);
+template int att_cache_in_hl<float>(const float*, int, int, int, float*, hipStream_t);
+template int att_cache_in_hl<bf16>(const float*, int, int, int, bf16*, hipStream_t);
+template int att_cache_out_hl<float>(const float*, int, int, int, int, float*, hipStream_t);
+template int att_cache_out_hl<bf16>(const bf16*, int, int, int, int, float*, hipStream_t);
 template int cnn_cache_in<float>(const float*, int, int, float*, hipStream_t);
 template int cnn_cache_in<bf16>(const float*, int, int, bf16*, hipStream_t);
 template int cnn_cache_out<float>(const float*, int, int, int, float*, hipStream_t);

@@ -66,7 +66,6 @@ struct Carver {
 
 struct LayerW {
   void *ff1m, *ff2m, *ff1, *ff2, *qkv, *pos, *wo, *pw1, *pw2;   // T matrices [N][K]
-  void *ffs_m = nullptr, *ffs = nullptr;   // bf16 fused-FFN slab streams (ffn.hip), macaron / final
   float *b_ff1m, *b_ff2m, *b_ff1, *b_ff2, *b_qkv, *b_o, *b_pw1, *b_pw2;
   float *pu, *pv, *dw_t, *b_dw, *cn_w, *cn_b;
   float *ln_ffm_w, *ln_ffm_b, *ln_mha_w, *ln_mha_b, *ln_conv_w, *ln_conv_b, *ln_ff_w, *ln_ff_b, *ln_fin_w, *ln_fin_b;
@@ -86,12 +85,12 @@ struct FrontW {
 // Kernel classes timed by the optional in-stream profiler (HIP events around launches)
 enum {
   PC_FE_CONV = 0, PC_FE_GEMM, PC_FE_DW2, PC_POS, PC_LN, PC_FFN1, PC_FFN2, PC_QKV, PC_ATTN, PC_OPROJ, PC_PW1,
-  PC_CONV, PC_PW2, PC_CACHE, PC_CTC, PC_FFNF, PC_N
+  PC_CONV, PC_PW2, PC_CACHE, PC_CTC, PC_N
 };
 static const char* const PC_NAMES[PC_N] = {
     "frontend_conv0_dw", "frontend_pw_gemm", "frontend_dw2", "pos_gemm", "layernorm", "ffn_w1_gemm", "ffn_w2_gemm",
     "qkv_gemm", "chunk_attention", "out_proj_gemm", "pw1_glu_gemm", "conv_dw_ln_silu", "pw2_gemm", "cache_copy",
-    "ctc", "ffn_fused"};
+    "ctc"};
 
 struct cfm_model {
   cfm_config cfg;
@@ -103,8 +102,8 @@ struct cfm_model {
   int fe_group_windows = 0;         // "fe_group_windows": cap on front-end windows per group (0 = by memory)
   bool use_ring_attention = true;
   bool use_fused_ctc = true;        // "ctc_fused": bf16 ids-only CTC head as one argmax kernel (ctc.hip), no [rows, V] logits
-  bool use_fused_ffn = false;       // "fused_ffn": bf16 d=512 FFN as one kernel (ffn.hip) instead of two GEMMs (A/B: 16% slower)
-  int attn_diag = 0;                // "attn_diag": 1 = ring kernel without compute (staging only)   // "ring_attention" option (A/B against the generic kernel)
+  int attn_diag = 0;                // "attn_diag": 1 = ring kernel without compute (staging only)
+  cfm::Tuning tune;                 // per-model kernel selection / diagnostics (cfm_model_set_option)
   // profiler: bitmask of PC_* classes to bracket with events on the launch stream
   uint32_t prof_mask = 0;
   mutable std::vector<hipEvent_t> ev_pool;
@@ -152,9 +151,11 @@ struct cfm_model {
     for (auto& it : ev_live) { (void)hipEventDestroy(it.second.first); (void)hipEventDestroy(it.second.second); }
     for (auto e : ev_pool) (void)hipEventDestroy(e);
   }
+  // cache_b: batch size of a streaming-chunk call (plan kind 3): its caches are [nb, cache_b, H, L, 2dk] /
+  // [nb, cache_b, d, 7] (forward_chunk layout) and `aci` etc. point at this element's [H, L, 2dk] slice
   virtual cfm_status encode(const float* feats, const int32_t* plan_dev, const int32_t* plan_hdr, const float* aci,
                             const float* cci, int trunc, float* aco, float* cco, float* out, void* ws, size_t wsb,
-                            hipStream_t st) const = 0;
+                            hipStream_t st, int cache_b = 1) const = 0;
   virtual cfm_status ctc(const float* enc, int rows, float* logp, int32_t* ids, void* ws, size_t wsb,
                          hipStream_t st) const = 0;
   virtual size_t ws_bytes(const int32_t* hdr) const = 0;
@@ -176,6 +177,13 @@ struct ModelT : public cfm_model {
     int g = (int)std::max<size_t>(1, ((size_t)768 << 20) / per);
     if (fe_group_windows > 0) g = std::min(g, fe_group_windows);
     return std::min(g, h[PH_NWIN]);
+  }
+
+  // epilogue args carrying this model's kernel tuning
+  EpiArgs E() const {
+    EpiArgs e;
+    tune.apply(e);
+    return e;
   }
 
   struct WS {
@@ -227,7 +235,7 @@ struct ModelT : public cfm_model {
 
   cfm_status encode(const float* feats, const int32_t* plan_dev, const int32_t* hh, const float* aci, const float* cci,
                     int trunc, float* aco, float* cco, float* out, void* ws, size_t wsb,
-                    hipStream_t st) const override {
+                    hipStream_t st, int cache_b) const override {
     const int d = cfg.d_model, ff = cfg.ffn_dim, H = cfg.n_heads, dk = d / H;
     const float eps = cfg.norm_eps;
     const int rows = hh[PH_ROWS], C = hh[PH_C], L = hh[PH_L];
@@ -235,9 +243,13 @@ struct ModelT : public cfm_model {
     const int p_rows = hh[PH_PROWS], kv_rows = hh[PH_KVROWS], glu_rows = hh[PH_GLUROWS];
     const int kvoff = hh[PH_KVOFF], gluoff = hh[PH_GLUOFF];
     const bool masked = hh[PH_KIND] == 1;
+    const bool stream = hh[PH_KIND] == 3;   // forward_chunk: head-major caches, no row mask
+    const size_t att_ls = (size_t)L * 2 * d * (stream ? cache_b : 1);   // cache stride per layer
+    const size_t cnn_ls = (size_t)d * 7 * (stream ? cache_b : 1);
     const size_t prow_pad = (p_rows + 127) / 128 * 128;
     if (wsb < ws_bytes(hh)) return set_error(CFM_ERR_VALUE, "workspace too small");
-    if (!masked && (aci || cci)) return set_error(CFM_ERR_VALUE, "caches are only defined for the masked batch path");
+    if (!masked && !stream && (aci || cci))
+      return set_error(CFM_ERR_VALUE, "caches are only defined for the masked batch and streaming paths");
     WS w = carve(ws, hh, nullptr);
     const int32_t* meta = plan_dev + plan_meta_off(hh);
     const int32_t* attd = plan_dev + plan_att_off(hh);
@@ -252,20 +264,20 @@ struct ModelT : public cfm_model {
       const int ng = std::min(G, nwin - g0);
       PROF(PC_FE_CONV, frontend_conv0_dw<T>(feats, meta + (size_t)g0 * PLAN_REC, PLAN_REC, ng, Wn, fe.cm, fe.ci, fe.w0, fe.b0,
                                 fe.w1, fe.b1, fe.wpack, d, w.feA, st));
-      EpiArgs e1; e1.bias = fe.b_pw1; e1.out = w.feB; e1.ldo = d;
+      EpiArgs e1 = E(); e1.bias = fe.b_pw1; e1.out = w.feB; e1.ldo = d;
       PROF(PC_FE_GEMM, gemm<T>(EPI_STORE, ACT_RELU, w.feA, d, (const T*)fe.pw1, d, ng * T2 * 19, d, d, e1, st));
-      PROF(PC_FE_DW2, frontend_dw2<T>(w.feB, ng, T2, d, fe.w2, fe.b2, w.feA, st));
-      EpiArgs e2; e2.bias = fe.b_pw2; e2.out = w.feC + (size_t)g0 * T3 * 9 * d; e2.ldo = d;
+      PROF(PC_FE_DW2, frontend_dw2<T>(w.feB, ng, T2, d, fe.w2, fe.b2, w.feA, st, tune.dw2_seg));
+      EpiArgs e2 = E(); e2.bias = fe.b_pw2; e2.out = w.feC + (size_t)g0 * T3 * 9 * d; e2.ldo = d;
       PROF(PC_FE_GEMM, gemm<T>(EPI_STORE, ACT_RELU, w.feA, d, (const T*)fe.pw2, d, ng * T3 * 9, d, d, e2, st));
     }
-    { EpiArgs e3; e3.bias = fe.b_out; e3.out = w.x; e3.ldo = d; e3.row_off = 0; e3.alpha = std::sqrt((float)d);
+    { EpiArgs e3 = E(); e3.bias = fe.b_out; e3.out = w.x; e3.ldo = d; e3.row_off = 0; e3.alpha = std::sqrt((float)d);
       PROF(PC_FE_GEMM, gemm<T>(EPI_STORE_F32, ACT_NONE, w.feC, 9 * d, (const T*)fe.wout, 9 * d, nwin * T3, d, 9 * d, e3, st)); }
     // ---------------- relative positions: P_l = pos . W_pos_l^T for every layer in ONE GEMM against
     // the stacked weights: P is [p_rows, nb * d], layer l at column l * d (row stride nb * d)
     const int nl = (max_layers >= 0 && max_layers < cfg.num_blocks) ? max_layers : cfg.num_blocks;
     const int p_ld = cfg.num_blocks * d;
     PROF(PC_POS, pos_table<T>(d, p_rows, hh[PH_PANCHOR], w.pos, st));
-    { EpiArgs e; e.out = w.P; e.ldo = p_ld;
+    { EpiArgs e = E(); e.out = w.P; e.ldo = p_ld;
       PROF(PC_POS, gemm<T>(EPI_STORE, ACT_NONE, w.pos, d, (const T*)fe.pos_all, d, p_rows, p_ld, d, e, st)); }
     // ---------------- stream padding rows (cache slots and right zero padding)
     if (kvoff > 0) HIPC(hipMemsetAsync(w.kv, 0, (size_t)kvoff * 2 * d * sizeof(T), st));
@@ -294,32 +306,31 @@ struct ModelT : public cfm_model {
     auto resid2 = [&](const T* y, float alpha, const uint8_t* ym, const T* y2, float alpha2, const uint8_t* ym2) {
       ResidAdd<T> r = resid(y, alpha, ym); r.y2 = y2; r.alpha2 = alpha2; r.ymask2 = ym2; return r;
     };
-    // y = w2 . SiLU(w1 . h + b1) + b2: one fused kernel (bf16, d = 512) or two GEMMs through w.hid
-    auto ffn = [&](const void* w1, const float* b1, const void* w2, const float* b2, const void* stream_w,
-                   T* yout) -> cfm_status {
-      if constexpr (sizeof(T) == 2) {
-        if (use_fused_ffn && stream_w) {
-          PROF(PC_FFNF, ffn_fused((const bf16*)w.h, rows, (const bf16*)stream_w, b1, b2, (bf16*)yout, d, ff, st));
-          return CFM_OK;
-        }
-      }
-      { EpiArgs e; e.bias = b1; e.out = w.hid; e.ldo = ff;
+    // y = w2 . SiLU(w1 . h + b1) + b2: two GEMMs through w.hid
+    auto ffn = [&](const void* w1, const float* b1, const void* w2, const float* b2, T* yout) -> cfm_status {
+      { EpiArgs e = E(); e.bias = b1; e.out = w.hid; e.ldo = ff;
         PROF(PC_FFN1, gemm<T>(EPI_STORE, ACT_SILU, w.h, d, (const T*)w1, d, rows, ff, d, e, st)); }
-      { EpiArgs e; e.bias = b2; e.out = yout; e.ldo = d;
+      { EpiArgs e = E(); e.bias = b2; e.out = yout; e.ldo = d;
         PROF(PC_FFN2, gemm<T>(EPI_STORE, ACT_NONE, w.hid, ff, (const T*)w2, ff, rows, d, ff, e, st)); }
       return CFM_OK;
     };
     for (int l = 0; l < nl; ++l) {
       const LayerW& Lw = layers[l];
       // macaron FFN (x 0.5)
-      { const cfm_status fs = ffn(Lw.ff1m, Lw.b_ff1m, Lw.ff2m, Lw.b_ff2m, Lw.ffs_m, w.y); if (fs != CFM_OK) return fs; }
+      { const cfm_status fs = ffn(Lw.ff1m, Lw.b_ff1m, Lw.ff2m, Lw.b_ff2m, w.y); if (fs != CFM_OK) return fs; }
       // MHSA (x + 0.5 y_ffm is not stored: the conv LayerNorm re-applies it)
       { ResidAdd<T> r = resid(w.y, 0.5f, nullptr); r.defer = true;
         PROF(PC_LN, layernorm<T>(w.x, r, rows, d, Lw.ln_mha_w, Lw.ln_mha_b, eps, w.h, nullptr, st)); }
-      if (aci) PROF(PC_CACHE, att_cache_in<T>(aci + (size_t)l * L * 2 * d, L, 2 * d, w.kv, st));
-      { EpiArgs e; e.bias = Lw.b_qkv; e.out = w.q; e.out2 = w.kv; e.row_off = kvoff; e.d = d; e.dk = dk;
+      if (aci) {
+        if (stream) PROF(PC_CACHE, att_cache_in_hl<T>(aci + l * att_ls, H, L, dk, w.kv, st));
+        else PROF(PC_CACHE, att_cache_in<T>(aci + l * att_ls, L, 2 * d, w.kv, st));
+      }
+      { EpiArgs e = E(); e.bias = Lw.b_qkv; e.out = w.q; e.out2 = w.kv; e.row_off = kvoff; e.d = d; e.dk = dk;
         PROF(PC_QKV, gemm<T>(EPI_QKV, ACT_NONE, w.h, d, (const T*)Lw.qkv, d, rows, 3 * d, d, e, st)); }
-      if (aci && aco) PROF(PC_CACHE, att_cache_out<T>(w.kv, cache_start, L, 2 * d, aco + (size_t)l * L * 2 * d, st));
+      if (aci && aco) {
+        if (stream) PROF(PC_CACHE, att_cache_out_hl<T>(w.kv, cache_start, H, L, dk, aco + l * att_ls, st));
+        else PROF(PC_CACHE, att_cache_out<T>(w.kv, cache_start, L, 2 * d, aco + l * att_ls, st));
+      }
       {
         int r = -1;
         hipEvent_t pb_;
@@ -327,7 +338,8 @@ struct ModelT : public cfm_model {
         if constexpr (sizeof(T) == 2) {
           if (masked && use_ring_attention && dk == 64)
             r = chunk_attention_masked_bf16(w.q, w.kv, kv_rows, w.P + (size_t)l * d, p_rows, Lw.pu, Lw.pv,
-                                            attd, natt, H, C, hh[PH_L] + C + hh[PH_R], w.ao, st, attn_diag, p_ld);
+                                            attd, natt, H, C, hh[PH_L] + C + hh[PH_R], w.ao, st, attn_diag, p_ld,
+                                            tune.attn_reuse);
         }
         if (r == -1)
           r = chunk_attention<T>(w.q, w.kv, kv_rows, w.P + (size_t)l * d, p_rows, Lw.pu, Lw.pv, attd, natt,
@@ -335,22 +347,23 @@ struct ModelT : public cfm_model {
         KCHK(r);
         prof_end(PC_ATTN, st, pb_);
       }
-      { EpiArgs e; e.bias = Lw.b_o; e.out = w.y2; e.ldo = d;
+      { EpiArgs e = E(); e.bias = Lw.b_o; e.out = w.y2; e.ldo = d;
         PROF(PC_OPROJ, gemm<T>(EPI_STORE, ACT_NONE, w.ao, d, (const T*)Lw.wo, d, rows, d, d, e, st)); }
       // convolution module: x += 0.5 y_ffm + y_attn, stored
       PROF(PC_LN, layernorm<T>(w.x, resid2(w.y, 0.5f, nullptr, w.y2, 1.f, nullptr), rows, d, Lw.ln_conv_w, Lw.ln_conv_b,
-                               eps, w.h, masked ? nullptr : rmask, st));
-      if (cci) PROF(PC_CACHE, cnn_cache_in<T>(cci + (size_t)l * d * 7, d, 7, w.glu, st));
-      { EpiArgs e; e.bias = Lw.b_pw1; e.out = w.glu; e.ldo = d; e.row_off = gluoff;
+                               eps, w.h, (masked || stream) ? nullptr : rmask, st));
+      if (cci) PROF(PC_CACHE, cnn_cache_in<T>(cci + l * cnn_ls, d, 7, w.glu, st));
+      { EpiArgs e = E(); e.bias = Lw.b_pw1; e.out = w.glu; e.ldo = d; e.row_off = gluoff;
         PROF(PC_PW1, gemm<T>(EPI_GLU, ACT_NONE, w.h, d, (const T*)Lw.pw1, d, rows, 2 * d, d, e, st)); }
-      if (cci && cco) PROF(PC_CACHE, cnn_cache_out<T>(w.glu, cache_start, d, 7, cco + (size_t)l * d * 7, st));
-      PROF(PC_CONV, conv_dw_ln_silu<T>(w.glu, convd, nconv, d, Lw.dw_t, Lw.b_dw, Lw.cn_w, Lw.cn_b, eps, w.cv, st));
-      { EpiArgs e; e.bias = Lw.b_pw2; e.out = w.y; e.ldo = d;
+      if (cci && cco) PROF(PC_CACHE, cnn_cache_out<T>(w.glu, cache_start, d, 7, cco + l * cnn_ls, st));
+      PROF(PC_CONV, conv_dw_ln_silu<T>(w.glu, convd, nconv, d, Lw.dw_t, Lw.b_dw, Lw.cn_w, Lw.cn_b, eps, w.cv, st,
+                                        tune.conv_dot2, tune.conv_dma));
+      { EpiArgs e = E(); e.bias = Lw.b_pw2; e.out = w.y; e.ldo = d;
         PROF(PC_PW2, gemm<T>(EPI_STORE, ACT_NONE, w.cv, d, (const T*)Lw.pw2, d, rows, d, d, e, st)); }
       // FFN (x 0.5); x + y_conv is not stored: norm_final re-applies it
       { ResidAdd<T> r = resid(w.y, 1.f, rmask); r.defer = true;
         PROF(PC_LN, layernorm<T>(w.x, r, rows, d, Lw.ln_ff_w, Lw.ln_ff_b, eps, w.h, nullptr, st)); }
-      { const cfm_status fs = ffn(Lw.ff1, Lw.b_ff1, Lw.ff2, Lw.b_ff2, Lw.ffs, w.y2); if (fs != CFM_OK) return fs; }
+      { const cfm_status fs = ffn(Lw.ff1, Lw.b_ff1, Lw.ff2, Lw.b_ff2, w.y2); if (fs != CFM_OK) return fs; }
       // norm_final over x + y_conv + 0.5 y_ffn (+ next layer's macaron LN, or after_norm)
       const ResidAdd<T> rf = resid2(w.y, 1.f, rmask, w.y2, 0.5f, nullptr);
       if (l + 1 < nl)
@@ -390,11 +403,11 @@ struct ModelT : public cfm_model {
     // tiles); f32x4 epilogue stores need the row pitch V % 4 == 0
     const int V1 = (sizeof(T) == 2 && V % 4 == 0) ? V / 256 * 256 : 0;
     if (V1 > 0) {
-      EpiArgs e; e.bias = fe.ctc_b; e.out = dst; e.ldo = V;
+      EpiArgs e = E(); e.bias = fe.ctc_b; e.out = dst; e.ldo = V;
       PROF(PC_CTC, gemm<T>(EPI_STORE_F32, ACT_NONE, A, d, (const T*)fe.ctc_w, d, rows, V1, d, e, st));
     }
     if (V1 < V) {
-      EpiArgs e; e.bias = fe.ctc_b + V1; e.out = dst + V1; e.ldo = V;
+      EpiArgs e = E(); e.bias = fe.ctc_b + V1; e.out = dst + V1; e.ldo = V;
       PROF(PC_CTC, gemm<T>(EPI_STORE_F32, ACT_NONE, A, d, (const T*)fe.ctc_w + (size_t)V1 * d, d, rows, V - V1, d, e, st));
     }
     PROF(PC_CTC, log_softmax_rows(dst, rows, V, logp ? 1 : 0, ids, st));
@@ -457,12 +470,6 @@ static cfm_status build_model(const cfm_config& cfg, const HostW& hw, int device
         std::memcpy(&p[i], &r, 2);
       }
     }
-    fix.push_back({off, slot});
-  };
-  auto put_ffn_stream = [&](const float* w1, const float* w2, void** slot) {
-    const size_t n = (size_t)2 * d * ff;
-    size_t off = reserve(n * 2);
-    ffn_pack_stream(w1, w2, d, ff, reinterpret_cast<uint16_t*>(img.data() + off), &bf16_bits_rne);
     fix.push_back({off, slot});
   };
   auto vec = [&](const std::string& k, int64_t n) { const float* s = hw.get(k, n); return std::vector<float>(s, s + n); };
@@ -533,12 +540,6 @@ static cfm_status build_model(const cfm_config& cfg, const HostW& hw, int device
       put_f32(hw.get(p + "feed_forward.w_1.bias", ff), ff, &Lw.b_ff1);
       put_T(vec(p + "feed_forward.w_2.weight", (int64_t)d * ff), &Lw.ff2);
       put_f32(hw.get(p + "feed_forward.w_2.bias", d), d, &Lw.b_ff2);
-      if (sizeof(T) == 2 && d == 512 && ff % 64 == 0) {   // fused-FFN slab streams (ffn.hip)
-        put_ffn_stream(hw.get(p + "feed_forward_macaron.w_1.weight", (int64_t)ff * d),
-                       hw.get(p + "feed_forward_macaron.w_2.weight", (int64_t)d * ff), &Lw.ffs_m);
-        put_ffn_stream(hw.get(p + "feed_forward.w_1.weight", (int64_t)ff * d),
-                       hw.get(p + "feed_forward.w_2.weight", (int64_t)d * ff), &Lw.ffs);
-      }
       {
         std::vector<float> w, b;
         for (const char* nm : {"linear_q", "linear_k", "linear_v"}) {
@@ -647,9 +648,14 @@ cfm_status cfm_model_set_option(cfm_model* m, const char* key, int64_t value) {
   if (!std::strcmp(key, "profile")) { m->prof_mask = (uint32_t)value; return CFM_OK; }
   if (!std::strcmp(key, "ring_attention")) { m->use_ring_attention = value != 0; return CFM_OK; }
   if (!std::strcmp(key, "ctc_fused")) { m->use_fused_ctc = value != 0; return CFM_OK; }
-  if (!std::strcmp(key, "fused_ffn")) { m->use_fused_ffn = value != 0; return CFM_OK; }
-  if (!std::strcmp(key, "ffn_variant")) { ffn_set_variant((int)value); return CFM_OK; }
-  if (!std::strcmp(key, "gemm_variant")) { gemm_set_variant((int)value); return CFM_OK; }
+  {   // per-model kernel tuning / diagnostics; defaults are the measured best
+    const std::pair<const char*, int*> knobs[] = {
+        {"gemm_diag", &m->tune.gemm_diag}, {"gemm_wst", &m->tune.gemm_wst},   {"store_mode", &m->tune.store_mode},
+        {"col_group", &m->tune.col_group}, {"attn_reuse", &m->tune.attn_reuse}, {"conv_dot2", &m->tune.conv_dot2},
+        {"conv_dma", &m->tune.conv_dma},   {"dw2_seg", &m->tune.dw2_seg}};
+    for (auto& k : knobs)
+      if (!std::strcmp(key, k.first)) { *k.second = (int)value; return CFM_OK; }
+  }
   if (!std::strcmp(key, "attn_diag")) { m->attn_diag = (int)value; return CFM_OK; }
   if (!std::strcmp(key, "profile_reset")) {
     m->prof_collect();
@@ -699,6 +705,36 @@ cfm_status cfm_encode_padded(const cfm_model* m, const float* xs, const int32_t*
   return m->encode(xs, plan_dev, h, nullptr, nullptr, 0, nullptr, nullptr, out, ws, wsb, (hipStream_t)stream);
 }
 
+size_t cfm_workspace_bytes_stream(const cfm_model* m, int32_t T, int32_t C, int32_t L, int32_t R) {
+  if (!m || C <= 0) return 0;
+  const int Tp = calc_length(T);
+  if (Tp <= 0) return 0;
+  int32_t h[PH_HEADER] = {0};
+  h[PH_KIND] = 3; h[PH_NWIN] = 1; h[PH_ROWS] = Tp; h[PH_C] = C; h[PH_L] = L; h[PH_R] = R;
+  h[PH_W] = T; h[PH_TOUT] = Tp; h[PH_PROWS] = L + 2 * (C + R) - 1; h[PH_KVROWS] = L + Tp; h[PH_GLUROWS] = 7 + Tp;
+  return m->ws_bytes(h);
+}
+
+cfm_status cfm_encode_stream(const cfm_model* m, const float* xs, int32_t B, const int32_t* h, const int32_t* plan_dev,
+                             const float* aci, const float* cci, float* aco, float* cco, float* out, void* ws,
+                             size_t wsb, cfm_stream stream) {
+  if (!m || !xs || !h || !plan_dev || !out) return set_error(CFM_ERR_VALUE, "null argument");
+  if (h[PH_KIND] != 3) return set_error(CFM_ERR_VALUE, "not a streaming-chunk plan");
+  if (B <= 0) return set_error(CFM_ERR_VALUE, "batch must be >= 1");
+  if (!aci || !cci) return set_error(CFM_ERR_ASSERT, "forward_chunk needs att_cache [nb, B, H, L, 2dk] and cnn_cache [nb, B, d, 7]");
+  if ((aco == nullptr) != (cco == nullptr)) return set_error(CFM_ERR_VALUE, "att_cache_out and cnn_cache_out go together");
+  HIPC(hipSetDevice(m->device));
+  const int T = h[PH_W], Tp = h[PH_TOUT], L = h[PH_L], R = h[PH_R], d = m->cfg.d_model;
+  const size_t att_b = (size_t)L * 2 * d, cnn_b = (size_t)d * 7;
+  for (int b = 0; b < B; ++b) {
+    const cfm_status r = m->encode(xs + (size_t)b * T * m->cfg.input_dim, plan_dev, h, aci + b * att_b, cci + b * cnn_b,
+                                   Tp - R, aco ? aco + b * att_b : nullptr, cco ? cco + b * cnn_b : nullptr,
+                                   out + (size_t)b * Tp * d, ws, wsb, (hipStream_t)stream, B);
+    if (r != CFM_OK) return r;
+  }
+  return CFM_OK;
+}
+
 cfm_status cfm_masks_from_plan(const int32_t* h, const int32_t* plan_dev, uint8_t* att, uint8_t* pad,
                                cfm_stream stream) {
   if (!h || !plan_dev || !att || !pad) return set_error(CFM_ERR_VALUE, "null argument");
@@ -722,35 +758,16 @@ int32_t cfm_profile_read(const cfm_model* m, const char** names, double* total_m
 cfm_status cfm_op_gemm(int32_t dtype, int32_t epi, int32_t act, const void* A, int32_t lda, const void* W, int32_t ldw,
                        int32_t M, int32_t N, int32_t K, const float* bias, float alpha, void* out, int32_t ldo,
                        int32_t row_off, void* out2, int32_t d, float* x, int32_t ldx, const uint8_t* rowmask,
-                       int32_t small_tiles, cfm_stream stream) {
+                       int32_t variant, cfm_stream stream) {
   EpiArgs e;
   e.bias = bias; e.alpha = alpha; e.out = out; e.out2 = out2; e.ldo = ldo; e.row_off = row_off; e.x = x; e.ldx = ldx;
-  e.rowmask = rowmask; e.d = d;
-  gemm_force_small_tiles(small_tiles);
+  e.rowmask = rowmask; e.d = d; e.small_tiles = variant & 1; e.diag = (variant >> 8) & 0xff;
   int r;
   if (dtype == CFM_DTYPE_F32)
     r = gemm<float>(epi, act, (const float*)A, lda, (const float*)W, ldw, M, N, K, e, (hipStream_t)stream);
   else
     r = gemm<bf16>(epi, act, (const bf16*)A, lda, (const bf16*)W, ldw, M, N, K, e, (hipStream_t)stream);
-  gemm_force_small_tiles(0);
   if (r) return set_error(CFM_ERR_RUNTIME, std::string("gemm: ") + hipGetErrorString((hipError_t)r));
-  return CFM_OK;
-}
-
-cfm_status cfm_op_ffn(const float* w1, const float* b1, const float* w2, const float* b2, const void* x, void* y,
-                      int32_t M, int32_t d, int32_t ff, cfm_stream stream) {
-  if (!w1 || !w2 || !b1 || !b2 || !x || !y) return set_error(CFM_ERR_VALUE, "null argument");
-  if (d != 512 || ff <= 0 || ff % 64) return set_error(CFM_ERR_VALUE, "fused FFN needs d == 512 and ff % 64 == 0");
-  std::vector<uint16_t> host((size_t)2 * d * ff);
-  ffn_pack_stream(w1, w2, d, ff, host.data(), &bf16_bits_rne);
-  void* dev = nullptr;
-  HIPC(hipMalloc(&dev, host.size() * 2));
-  hipError_t e = hipMemcpyAsync(dev, host.data(), host.size() * 2, hipMemcpyHostToDevice, (hipStream_t)stream);
-  int r = e == hipSuccess ? ffn_fused((const bf16*)x, M, (const bf16*)dev, b1, b2, (bf16*)y, d, ff, (hipStream_t)stream)
-                          : (int)e;
-  if (r == 0) r = (int)hipStreamSynchronize((hipStream_t)stream);
-  (void)hipFree(dev);
-  if (r) return set_error(CFM_ERR_RUNTIME, std::string("ffn: ") + hipGetErrorString((hipError_t)r));
   return CFM_OK;
 }
 

@@ -5,7 +5,7 @@
 namespace cfm {
 
 enum {
-  PH_KIND = 0,      // 1 = masked batch, 2 = padded batch
+  PH_KIND = 0,      // 1 = masked batch, 2 = padded batch, 3 = streaming chunk (forward_chunk)
   PH_NWIN = 1,      // front-end windows (packed chunks / padded utterances)
   PH_NATT = 2,      // attention blocks
   PH_NCONV = 3,     // conv blocks

@@ -9,7 +9,10 @@
 //   conv column j:             g = C*c - 7 + j, valid iff -o <= g < max_len and j-7 <= C+R-1.
 // Both valid sets are contiguous, so masks travel as [lo, hi) ranges.
 // cfm_plan_padded restates forward_encoder's geometry (attention.py:334-386,
-// convolution.py:133-167).
+// convolution.py:133-167).  cfm_plan_stream restates forward_chunk's (encoder.py:310-385): one
+// window of T frames -> T' rows; keys = [L cached | T' current], valid from L - offset
+// (encoder.py:351-357); rel-pos table of a C+R chunk read at row T'-1-i+j (attention.py:256-266);
+// conv chunks of C over [7 cached | T'] with the right edge zero-padded (convolution.py:148-180).
 #include <algorithm>
 #include <cstring>
 #include <vector>
@@ -176,5 +179,55 @@ extern "C" cfm_status cfm_plan_padded(const int32_t* lens, int32_t B, int32_t T,
       }
     }
   }
+  return CFM_OK;
+}
+
+extern "C" cfm_status cfm_plan_stream(int32_t T, int32_t C, int32_t L, int32_t R, int32_t offset, int32_t* t_out,
+                                      int32_t* plan, int64_t* plan_n) {
+  if (C <= 0 || L < 0 || R < 0 || offset < 0)
+    return set_error(CFM_ERR_VALUE, "plan_stream: chunk_size must be > 0, contexts and offset >= 0");
+  const int Tp = calc_length(T);
+  if (Tp <= 0) return set_error(CFM_ERR_VALUE, "plan_stream: input too short for 8x subsampling");
+  if (Tp < R) return set_error(CFM_ERR_VALUE, "plan_stream: the chunk must have at least right_context_size frames");
+  if (Tp > C + R) return set_error(CFM_ERR_VALUE, "plan_stream: more than chunk_size + right_context_size frames");
+  if (C + R + L >= 5000) return set_error(CFM_ERR_ASSERT, "relative PE table: left_context + chunk_size >= 5000 (embedding.py:163)");
+  if (t_out) *t_out = Tp;
+  const int natt = (Tp + 63) / 64;
+  int nconv = 0;
+  for (int j0 = 0; j0 < Tp; j0 += C) nconv += (std::min(C, Tp - j0) + 63) / 64;
+  const int64_t need = plan_ints(1, natt, nconv, Tp);
+  if (plan_n && !plan) { *plan_n = need; return CFM_OK; }
+  if (!plan) return CFM_OK;
+  if (plan_n && *plan_n < need) return set_error(CFM_ERR_VALUE, "plan_stream: plan buffer too small");
+  std::memset(plan, 0, sizeof(int32_t) * need);
+  int32_t* h = plan;
+  h[PH_KIND] = 3; h[PH_NWIN] = 1; h[PH_NATT] = natt; h[PH_NCONV] = nconv; h[PH_ROWS] = Tp;
+  h[PH_C] = C; h[PH_L] = L; h[PH_R] = R; h[PH_W] = T; h[PH_TOUT] = Tp;
+  h[PH_PROWS] = L + 2 * (C + R) - 1; h[PH_PANCHOR] = C + R + L - 1;
+  h[PH_KVROWS] = L + Tp; h[PH_GLUROWS] = 7 + Tp; h[PH_KVOFF] = L; h[PH_GLUOFF] = 7;
+  int32_t* meta = plan + plan_meta_off(h);
+  int32_t* att = plan + plan_att_off(h);
+  int32_t* conv = plan + plan_conv_off(h);
+  uint8_t* rmask = reinterpret_cast<uint8_t*>(plan + plan_mask_off(h));
+  meta[PM_SRC_ROW] = 0; meta[PM_NVALID] = T;
+  const int klo = std::min(std::max(0, L - offset), L + Tp);
+  for (int s = 0; s < natt; ++s) {
+    const int q0 = 64 * s, nq = std::min(64, Tp - q0);
+    int32_t* a = att + (int64_t)s * PLAN_REC;
+    a[AD_Q_ROW0] = q0; a[AD_NQ] = nq; a[AD_KV_ROW0] = 0;
+    a[AD_KEY_LO] = klo; a[AD_KEY_HI] = L + Tp; a[AD_P_BASE] = Tp - 1 - q0; a[AD_Q_VALID] = nq;
+  }
+  int blk = 0;
+  for (int j0 = 0; j0 < Tp; j0 += C) {
+    const int rj = std::min(C, Tp - j0);
+    const int lim = std::min(j0 + C + 7, 7 + Tp);   // chunk end (+ its 7 zero pads) / sequence end
+    for (int q0 = 0; q0 < rj; q0 += 64, ++blk) {
+      const int t0 = j0 + q0;
+      int32_t* cd = conv + (int64_t)blk * PLAN_REC;
+      cd[CD_OUT_ROW0] = t0; cd[CD_NOUT] = std::min(64, rj - q0); cd[CD_SRC_ROW0] = t0;
+      cd[CD_J_LO] = 0; cd[CD_J_HI] = lim - t0;
+    }
+  }
+  for (int t = 0; t < Tp; ++t) rmask[t] = 1;
   return CFM_OK;
 }

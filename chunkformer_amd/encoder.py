@@ -6,6 +6,7 @@ reference; every tensor op of the hot path runs in libcfm.so (HIP, gfx950):
   forward_parallel_chunk  encoder.py:503-681   -> cfm_plan_masked + cfm_encode_masked
   forward_encoder         encoder.py:220-274   -> cfm_plan_padded + cfm_encode_padded
   forward                 encoder.py:461-501   (eval branch: negative sizes -> 0/0/0)
+  forward_chunk           encoder.py:310-385   -> cfm_plan_stream + cfm_encode_stream (realtime path)
   ctc_log_softmax/argmax  ctc.py:73-91          -> cfm_ctc_logprobs / cfm_ctc_ids (fused argmax)
   ctc_collapse            model_utils.py:23-58, 174-221 -> cfm_ctc_collapse
 
@@ -208,6 +209,43 @@ class ChunkFormerEncoder:
         sub = torch.tensor([calc_length(t) for t in lens], device=dev)
         masks = (torch.arange(Tp, device=dev)[None, :] < sub[:, None]).unsqueeze(1)
         return out, masks
+
+    # ------------------------------------------------------------------ streaming
+    @torch.no_grad()
+    def forward_chunk(self, xs: torch.Tensor, att_cache: torch.Tensor = torch.zeros((0, 0, 0, 0, 0)),
+                      cnn_cache: torch.Tensor = torch.zeros((0, 0, 0, 0)), chunk_size: int = 0,
+                      left_context_size: int = 0, right_context_size: int = 0, offset: int = 0):
+        """encoder.py:310-385: one streaming step of the realtime app (stream_asr.py:164-172).
+        xs [B, T, 80]; att_cache [nb, B, H, L, 2dk], cnn_cache [nb, B, d, 7] (required; zeros at the
+        stream start); returns (xs [B, T', d], None, new att_cache, new cnn_cache) like the reference
+        (its second value is an unused placeholder)."""
+        if xs.dim() != 3 or xs.shape[-1] != self.cfg.input_dim:
+            raise RuntimeError(f"expected xs [B, T, {self.cfg.input_dim}], got {tuple(xs.shape)}")
+        B, T, _ = xs.shape
+        C, L, R = int(chunk_size), int(left_context_size), int(right_context_size)
+        nb, H, dk, d = self.num_blocks, self.cfg.n_heads, self.cfg.head_dim, self.cfg.d_model
+        if att_cache.dim() != 5 or att_cache.size(3) == 0:
+            raise AssertionError("forward_chunk needs att_cache [num_blocks, B, H, left_context_size, 2*d_k] "
+                                 "(zeros at the start of a stream)")
+        if tuple(att_cache.shape) != (nb, B, H, L, 2 * dk):
+            raise ValueError(f"att_cache shape {tuple(att_cache.shape)} != {(nb, B, H, L, 2 * dk)}")
+        if tuple(cnn_cache.shape) != (nb, B, d, self.cfg.conv_lorder):
+            raise ValueError(f"cnn_cache shape {tuple(cnn_cache.shape)} != {(nb, B, d, self.cfg.conv_lorder)}")
+        plan, Tp = _lib.plan_stream(T, C, L, R, int(offset))
+        dev = self.device
+        x = xs.to(dev, torch.float32).contiguous()
+        aci = att_cache.to(dev, torch.float32).contiguous()
+        cci = cnn_cache.to(dev, torch.float32).contiguous()
+        aco, cco = torch.empty_like(aci), torch.empty_like(cci)
+        out = torch.empty(B, Tp, d, dtype=torch.float32, device=dev)
+        plan_dev = self._upload(plan)
+        ws_bytes = _lib.cfm_workspace_bytes_stream(self._h, T, C, L, R)
+        ws = self._workspace(ws_bytes)
+        _lib.check(_lib.cfm_encode_stream(self._h, x.data_ptr(), B, plan.data_ptr(), plan_dev.data_ptr(),
+                                          aci.data_ptr(), cci.data_ptr(), aco.data_ptr(), cco.data_ptr(),
+                                          out.data_ptr(), ws.data_ptr(), ws_bytes, self._stream()))
+        self._last_plan = (plan, plan_dev)
+        return out, None, aco, cco
 
     def forward(self, xs, xs_lens, chunk_size: int = 0, left_context_size: int = -1, right_context_size: int = -1,
                 **kwargs):

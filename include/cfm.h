@@ -130,6 +130,25 @@ size_t cfm_workspace_bytes_padded(const cfm_model* m, int32_t B, int32_t T, int3
 cfm_status cfm_encode_padded(const cfm_model* m, const float* xs_dev, const int32_t* plan_host, const int32_t* plan_dev,
                              float* out_dev, void* workspace, size_t workspace_bytes, cfm_stream stream);
 
+/* ------------------------------------------------------------------ streaming
+ * cfm_plan_stream + cfm_encode_stream replace ChunkFormerEncoder.forward_chunk
+ * (encoder.py:310-385), the realtime path (apps/realtime-asr/stream_asr.py:164-172):
+ * xs_dev [B, T, 80] f32 (every frame valid), T' = calc_length(T) with
+ * right_context_size <= T' <= chunk_size + right_context_size; `offset` = frames already
+ * streamed (keys of the first L - offset cache slots are masked, encoder.py:351-357).
+ * att_cache_in [nb, B, H, L, 2*dk] and cnn_cache_in [nb, B, d, 7] f32 are required (the
+ * reference's head-major layout); the new caches (encoder.py:374-383) go to
+ * att_cache_out / cnn_cache_out (may alias the inputs; NULL = not wanted).  out_dev: [B, T', d]
+ * f32 after after_norm.  One plan serves every batch element (they share T and offset). */
+cfm_status cfm_plan_stream(int32_t T, int32_t chunk_size, int32_t left_context, int32_t right_context, int32_t offset,
+                           int32_t* t_out, int32_t* plan_host, int64_t* plan_ints);
+size_t cfm_workspace_bytes_stream(const cfm_model* m, int32_t T, int32_t chunk_size, int32_t left_context,
+                                  int32_t right_context);
+cfm_status cfm_encode_stream(const cfm_model* m, const float* xs_dev, int32_t B, const int32_t* plan_host,
+                             const int32_t* plan_dev, const float* att_cache_in, const float* cnn_cache_in,
+                             float* att_cache_out, float* cnn_cache_out, float* out_dev, void* workspace,
+                             size_t workspace_bytes, cfm_stream stream);
+
 /* Materialise att_mask [N, L+C+R] and mask_pad [N, C+14] (0/1 bytes) of a masked
  * plan: the exact tensors encoder.py:627-645 builds. */
 cfm_status cfm_masks_from_plan(const int32_t* plan_host, const int32_t* plan_dev, uint8_t* att_mask_dev,

@@ -24,18 +24,12 @@ typedef enum { CFM_ACT_NONE = 0, CFM_ACT_RELU = 1, CFM_ACT_SILU = 2 } cfm_act;
  *   RESID:     x[m*ldx + n] += alpha*(acc + bias)*rowmask[m]
  *   QKV:       n < d -> out_T[m*d + n]; else out2_T[(m+row_off)*2d + head*128 + {0,64} + dim]
  *   GLU:       W rows interleaved [a16 | gate16]: out_T[(m+row_off)*ldo + ch] = a*sigmoid(gate)
- * small_tiles=1 forces the 128x128 kernel (A/B testing). */
+ * variant (A/B testing): bit 0 forces the 128x128 kernel; bits 8-15 select a timing diagnostic of
+ * the bf16 kernels (1 no MFMA, 2 no DMA in the loop, 3 no epilogue, 5 no stores; 0 = normal). */
 cfm_status cfm_op_gemm(int32_t dtype, int32_t epi, int32_t act, const void* A, int32_t lda, const void* W, int32_t ldw,
                        int32_t M, int32_t N, int32_t K, const float* bias, float alpha, void* out, int32_t ldo,
                        int32_t row_off, void* out2, int32_t d, float* x, int32_t ldx, const uint8_t* rowmask,
-                       int32_t small_tiles, cfm_stream stream);
-
-/* fused position-wise FFN (bf16): y[M,d] = w2 . SiLU(w1 . x + b1) + b2, x / y bf16 device rows,
- * w1 [ff,d] / w2 [d,ff] f32 HOST arrays in the reference layout (repacked into the slab stream
- * here: this test entry point allocates and synchronises), b1 / b2 f32 device.  d must be 512.
- * Replaces PositionwiseFeedForward.forward (positionwise_feed_forward.py:51-60) with SiLU. */
-cfm_status cfm_op_ffn(const float* w1, const float* b1, const float* w2, const float* b2, const void* x, void* y,
-                      int32_t M, int32_t d, int32_t ff, cfm_stream stream);
+                       int32_t variant, cfm_stream stream);
 
 #ifdef __cplusplus
 }

@@ -20,6 +20,8 @@ Functions and the reference code they restate:
   forward_parallel_chunk              encoder.py:503-681
   forward_encoder (padded/full)       encoder.py:220-308, encoder_layer.py:62-153,
                                       attention.py:268-418, convolution.py:101-192
+  forward_chunk (streaming)           encoder.py:310-385, attention.py:326-333 + 390-418 (cached
+                                      branch, rel_shift 242-266), convolution.py:101-192
   ctc_log_softmax                     ctc.py:73-81
 """
 from __future__ import annotations
@@ -135,15 +137,16 @@ def cmvn(x, sd):
     return x
 
 
-def _attention_core(q, kw, vw, P, u, v, key_mask, dk):
+def _attention_core(q, kw, vw, P, u, v, key_mask, dk, A=None):
     """q [B,Cq,H,dk]; kw/vw [B,W,H,dk]; P [PL,H,dk]; key_mask [B,Cq or 1,W] bool.
-    score(i,j) = ((q_i+u).k_j + (q_i+v).P[A-i+j]) / sqrt(dk), A = PL - W (= C-1 for the
-    chunk window, T'-1 for full attention).  Masked -> -inf, softmax fp32, masked -> 0."""
+    score(i,j) = ((q_i+u).k_j + (q_i+v).P[A-i+j]) / sqrt(dk), A = PL - W by default (= C-1 for
+    the chunk window, T'-1 for full attention).  Masked -> -inf, softmax fp32, masked -> 0."""
     B, Cq, H, _ = q.shape
     W = kw.shape[1]
     ac = torch.einsum("bihd,bjhd->bhij", q + u, kw)
     bdf = torch.einsum("bihd,khd->bhik", q + v, P)
-    A = P.shape[0] - W
+    if A is None:
+        A = P.shape[0] - W
     idx = A - torch.arange(Cq)[:, None] + torch.arange(W)[None, :]
     bd = torch.gather(bdf, 3, idx.expand(B, H, Cq, W))
     s = (ac + bd) / math.sqrt(dk)
@@ -318,6 +321,66 @@ def forward_encoder(sd, cfg, xs, xs_lens, C=0, L=0, R=0):
     x = _ln(x, sd, "encoder.after_norm")
     masks = (torch.arange(Tp)[None, :] < lens_sub[:, None]).unsqueeze(1)
     return x, masks
+
+
+@torch.no_grad()
+def forward_chunk(sd, cfg, xs, att_cache, cnn_cache, C, L, R, offset):
+    """Restatement of ChunkFormerEncoder.forward_chunk (encoder.py:310-385), the realtime path:
+    xs [B, T, 80] (no padding), att_cache [nb, B, H, L, 2dk], cnn_cache [nb, B, d, 7], integer
+    offset.  Returns (xs [B, T', d], new att_cache [nb, B, H, L, 2dk], new cnn_cache [nb, B, d, 7]).
+
+    Per layer (chunk_size C, right context 0): every one of the T' queries attends to the L cached
+    keys + the T' current keys; key j is valid iff j >= L - offset (the flipped att_masks of
+    encoder.py:351-357, cut to L + T' keys, attention.py:132); the rel-pos table is the one of a
+    chunk of C + R frames (embed called with chunk_size = C + R, encoder.py:343-349) read by
+    rel_shift with time1 = T' (row T'-1-i+j, attention.py:256-266).  The conv module concatenates
+    the 7-frame cache and runs the dynamic chunk conv at chunk size C (convolution.py:133-180).
+    New caches: the L keys/values and the 7 GLU frames ending R frames before the chunk end
+    (encoder.py:374-383)."""
+    B, T, _ = xs.shape
+    d, H, dk = cfg.d_model, cfg.n_heads, cfg.head_dim
+    x = frontend(cmvn(xs.float(), sd), sd, d)                       # [B, T', d]
+    Tp = x.shape[1]
+    assert Tp >= R, "forward_chunk needs T' >= right_context_size (cache slicing)"
+    pos = pos_slice(d, C + R, L, 0)
+    key_valid = (torch.arange(L + Tp) >= L - int(offset))[None, None, :].expand(B, 1, L + Tp)
+    new_att, new_cnn = [], []
+    for li in range(cfg.num_blocks):
+        p = f"encoder.encoders.{li}."
+        x = x + 0.5 * _ffn(_ln(x, sd, p + "norm_ff_macaron"), sd, p + "feed_forward_macaron")
+        h = _ln(x, sd, p + "norm_mha")
+        a = p + "self_attn."
+        q = _lin(h, sd, a + "linear_q").view(B, Tp, H, dk)
+        k = _lin(h, sd, a + "linear_k").view(B, Tp, H, dk)
+        v = _lin(h, sd, a + "linear_v").view(B, Tp, H, dk)
+        cache = att_cache[li].permute(0, 2, 1, 3).float()           # [B, L, H, 2dk]
+        kv = torch.cat([cache, torch.cat([k, v], -1)], 1)             # [B, L + T', H, 2dk]
+        new_att.append(kv[:, Tp - R: Tp - R + L].permute(0, 2, 1, 3).clone())
+        P = F.linear(pos, sd[a + "linear_pos.weight"]).view(-1, H, dk)
+        o = _attention_core(q, kv[..., :dk], kv[..., dk:], P, sd[a + "pos_bias_u"], sd[a + "pos_bias_v"],
+                            key_valid, dk, A=Tp - 1)
+        x = x + _lin(o, sd, a + "linear_out")
+        h = _ln(x, sd, p + "norm_conv")
+        c = p + "conv_module."
+        g = F.linear(h, sd[c + "pointwise_conv1.weight"][:, :, 0], sd[c + "pointwise_conv1.bias"])
+        glu = g[..., :d] * torch.sigmoid(g[..., d:])
+        xc = torch.cat([cnn_cache[li].transpose(1, 2).float(), glu], 1)   # [B, 7 + T', d]
+        new_cnn.append(xc[:, Tp - R: Tp - R + LORDER].transpose(1, 2).clone())
+        wdw = sd[c + "depthwise_conv.weight"][:, 0, :]
+        y = sd[c + "depthwise_conv.bias"].expand(B, Tp, d).clone()
+        t = torch.arange(Tp)
+        lim = torch.clamp((t // C) * C + C + LORDER, max=LORDER + Tp)      # chunk end / sequence end
+        for tap in range(2 * LORDER + 1):
+            src = t + tap                                                  # index into xc
+            ok = (src < lim).float()[None, :, None]
+            y = y + xc[:, src.clamp(max=LORDER + Tp - 1)] * ok * wdw[:, tap]
+        y = F.silu(_ln(y, sd, c + "norm"))
+        y = F.linear(y, sd[c + "pointwise_conv2.weight"][:, :, 0], sd[c + "pointwise_conv2.bias"])
+        x = x + y
+        x = x + 0.5 * _ffn(_ln(x, sd, p + "norm_ff"), sd, p + "feed_forward")
+        x = _ln(x, sd, p + "norm_final")
+    x = _ln(x, sd, "encoder.after_norm")
+    return x, torch.stack(new_att), torch.stack(new_cnn)
 
 
 @torch.no_grad()

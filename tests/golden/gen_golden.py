@@ -309,8 +309,54 @@ def gen_text(path):
         json.dump(out, f, ensure_ascii=False)
 
 
+STREAM_LAYERS = [0, 11]   # att_cache layers stored for the 12-layer run
+
+
+def stream_reference(enc, xs_steps, C, L, R, B):
+    """The realtime loop (apps/realtime-asr/stream_asr.py:105-180): zero caches [nb, B, H, L, 2dk] /
+    [nb, B, d, 7], encoder.forward_chunk per step with the caches carried and offset += C."""
+    nb, d, H = enc.num_blocks, enc._output_size, enc.attention_heads
+    att = torch.zeros(nb, B, H, L, 2 * d // H)
+    cnn = torch.zeros(nb, B, d, enc.cnn_module_kernel // 2)
+    offset, outs = 0, []
+    for x in xs_steps:
+        y, _, att, cnn = enc.forward_chunk(x, att_cache=att, cnn_cache=cnn, chunk_size=C, left_context_size=L,
+                                           right_context_size=R, offset=offset)
+        outs.append(y)
+        offset += C
+    return outs, att, cnn
+
+
+def gen_stream(path):
+    """forward_chunk (encoder.py:310-385) streaming steps: (a) the small model, batch of 2, C=16
+    L=32 R=16: four full steps (T' = C + R) and a short last step (T' = 27); (b) the 4-head d=512
+    12-layer model (head_dim 128), C=64 L=R=128, three full steps (T' = 192)."""
+    out = {}
+    with torch.no_grad():
+        enc, _, sd = build_reference(SMALL, 1)
+        C, L, R = 16, 32, 16
+        Tps = [C + R] * 4 + [27]
+        steps = [torch.stack(feats([8 * (tp - 1) + 15] * 2, 300 + i)) for i, tp in enumerate(Tps)]
+        outs, att, cnn = stream_reference(enc, steps, C, L, R, 2)
+        out.update(a_clr=np.array([C, L, R], np.int32), a_tp=np.array(Tps, np.int32), a_B=np.array(2),
+                   a_seed0=np.array(300), a_att=att.numpy(), a_cnn=cnn.numpy())
+        for i, y in enumerate(outs):
+            out[f"a_out{i}"] = y.numpy()
+        enc, _, sd = build_reference(LARGE_4H, 0)
+        C, L, R = 64, 128, 128
+        Tps = [C + R] * 3
+        steps = [torch.stack(feats([8 * (tp - 1) + 15], 400 + i)) for i, tp in enumerate(Tps)]
+        outs, att, cnn = stream_reference(enc, steps, C, L, R, 1)
+        out.update(b_clr=np.array([C, L, R], np.int32), b_tp=np.array(Tps, np.int32), b_B=np.array(1),
+                   b_seed0=np.array(400), b_att_layers=np.array(STREAM_LAYERS, np.int32),
+                   b_att=att[STREAM_LAYERS].numpy(), b_cnn=cnn.numpy())
+        for i, y in enumerate(outs):
+            out[f"b_out{i}"] = y.numpy()
+    np.savez_compressed(path, **out)
+
+
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["masks", "small", "large", "large_4h", "large_endless", "large_full", "text"]
+    which = sys.argv[1:] or ["masks", "small", "large", "large_4h", "large_endless", "large_full", "text", "stream"]
     if "masks" in which:
         gen_masks(os.path.join(HERE, "masks.npz"))
     if "small" in which:
@@ -325,4 +371,6 @@ if __name__ == "__main__":
         gen_text(os.path.join(HERE, "text.json"))
     if "large_full" in which:
         gen_large_full(os.path.join(HERE, "large_full.npz"))
+    if "stream" in which:
+        gen_stream(os.path.join(HERE, "stream.npz"))
     print("ok", which)

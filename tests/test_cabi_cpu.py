@@ -76,3 +76,22 @@ def test_plan_padded_geometry(lib):
     assert p[0] == 2 and p[1] == 3 and p[4] == 3 * tp
     plan, tp = lib.plan_padded([300, 123, 17], 300, 0, 0, 0)
     assert p[9] == tp
+
+
+def test_plan_stream_geometry():
+    """cfm_plan_stream (host C++, forward_chunk geometry): key window, rel-pos base, conv chunk edges."""
+    from chunkformer_amd import _lib
+    C, L, R, off = 16, 32, 16, 5
+    T = 8 * (C + R - 1) + 15
+    plan, tp = _lib.plan_stream(T, C, L, R, off)
+    h = plan[:16].tolist()
+    assert tp == C + R and h[0] == 3 and h[4] == tp and h[12] == L + tp and h[13] == 7 + tp
+    att = plan[16 + 8: 16 + 8 + 8].tolist()          # the one attention block (T' <= 64)
+    assert att[:8] == [0, tp, 0, L - off, L + tp, tp - 1, tp, 0]
+    conv = plan[16 + 16: 16 + 16 + 16].view(2, 8).tolist()
+    assert conv[0][:5] == [0, C, 0, 0, C + 7] and conv[1][:5] == [C, C, C, 0, C + 7]
+    import pytest
+    with pytest.raises(ValueError):
+        _lib.plan_stream(8 * (C + R) + 15 + 8, C, L, R, 0)   # more than C + R frames
+    with pytest.raises(ValueError):
+        _lib.plan_stream(8 * 3 + 15, C, L, R, 0)             # fewer than R frames

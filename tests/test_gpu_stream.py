@@ -1,0 +1,96 @@
+"""GPU parity of the streaming path: ChunkFormerEncoder.forward_chunk
+(encoder.py:310-385) through cfm_plan_stream + cfm_encode_stream, driven like the realtime app
+(apps/realtime-asr/stream_asr.py:105-180: zero caches, offset += chunk_size), against the
+reference's own run of the same steps (tests/golden/stream.npz, gen_golden.py:gen_stream).
+
+Tolerances: fp32 max-abs 1e-4 on every step's output and on the carried caches;
+bf16 rel-L2 <= 2e-2."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+BF16_RELL2 = 2e-2
+
+
+def _rel(a, b):
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))
+
+
+def _run(tag, cfg, seed, dtype):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from chunkformer_amd.encoder import ChunkFormerEncoder
+    from chunkformer_amd.weights import synthetic_features, synthetic_state_dict
+    from conftest import GOLDEN
+    g = np.load(os.path.join(GOLDEN, "stream.npz"))
+    enc = ChunkFormerEncoder(cfg, synthetic_state_dict(cfg, seed), dtype=dtype)
+    C, L, R = (int(v) for v in g[f"{tag}_clr"])
+    B = int(g[f"{tag}_B"])
+    nb, H, dk, d = cfg.num_blocks, cfg.n_heads, cfg.head_dim, cfg.d_model
+    att = torch.zeros(nb, B, H, L, 2 * dk, device="cuda")
+    cnn = torch.zeros(nb, B, d, 7, device="cuda")
+    offset = 0
+    for i, tp in enumerate(g[f"{tag}_tp"].tolist()):
+        x = torch.stack(synthetic_features([8 * (tp - 1) + 15] * B, int(g[f"{tag}_seed0"]) + i))
+        y, _, att, cnn = enc.forward_chunk(x, att_cache=att, cnn_cache=cnn, chunk_size=C, left_context_size=L,
+                                           right_context_size=R, offset=offset)
+        offset += C
+        exp = g[f"{tag}_out{i}"]
+        assert y.shape == exp.shape
+        if dtype == "fp32":
+            np.testing.assert_allclose(y.cpu().numpy(), exp, atol=1e-4, rtol=0, err_msg=f"step {i}")
+        else:
+            assert _rel(y.cpu().numpy(), exp) <= BF16_RELL2, (i, _rel(y.cpu().numpy(), exp))
+    return g, att.cpu().numpy(), cnn.cpu().numpy()
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_forward_chunk_small_batch2(dtype):
+    """d=128 2-layer model, batch 2, C=16 L=32 R=16: four full steps and a short last step."""
+    from chunkformer_amd.config import SMALL
+    g, att, cnn = _run("a", SMALL, 1, dtype)
+    if dtype == "fp32":
+        np.testing.assert_allclose(att, g["a_att"], atol=1e-4, rtol=0)
+        np.testing.assert_allclose(cnn, g["a_cnn"], atol=1e-4, rtol=0)
+    else:
+        assert _rel(att, g["a_att"]) <= BF16_RELL2 and _rel(cnn, g["a_cnn"]) <= BF16_RELL2
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_forward_chunk_large_4h(dtype):
+    """d=512, 4 heads (head_dim 128), 12 layers, C=64 L=R=128: three steps, carried caches."""
+    from chunkformer_amd.config import LARGE_4H
+    g, att, cnn = _run("b", LARGE_4H, 0, dtype)
+    att = att[g["b_att_layers"]]
+    if dtype == "fp32":
+        np.testing.assert_allclose(att, g["b_att"], atol=1e-4, rtol=0)
+        np.testing.assert_allclose(cnn, g["b_cnn"], atol=1e-4, rtol=0)
+    else:
+        assert _rel(att, g["b_att"]) <= BF16_RELL2 and _rel(cnn, g["b_cnn"]) <= BF16_RELL2
+
+
+def test_forward_chunk_matches_oracle_offsets():
+    """Offsets inside the cache (0 < offset < L) and past it, a 4-frame chunk, random caches: the
+    device path against the CPU oracle (oracle/encoder_ref.py:forward_chunk) at fp32."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from chunkformer_amd.config import SMALL
+    from chunkformer_amd.encoder import ChunkFormerEncoder
+    from chunkformer_amd.weights import synthetic_features, synthetic_state_dict
+    from oracle import encoder_ref as ref
+    sd = synthetic_state_dict(SMALL, 1)
+    enc = ChunkFormerEncoder(SMALL, sd, dtype="fp32")
+    gen = torch.Generator().manual_seed(5)
+    for C, L, R, off, tp in [(16, 32, 16, 7, 32), (16, 32, 16, 40, 20), (4, 16, 8, 3, 12), (64, 40, 0, 0, 64)]:
+        att = torch.randn(2, 1, 2, L, 128, generator=gen) * 0.5
+        cnn = torch.randn(2, 1, 128, 7, generator=gen) * 0.5
+        x = torch.stack(synthetic_features([8 * (tp - 1) + 15], 77 + off))
+        y, _, a2, c2 = enc.forward_chunk(x, att.cuda(), cnn.cuda(), C, L, R, off)
+        ry, ra, rc = ref.forward_chunk(sd, SMALL, x, att, cnn, C, L, R, off)
+        np.testing.assert_allclose(y.cpu().numpy(), ry.numpy(), atol=1e-4, rtol=0, err_msg=str((C, L, R, off)))
+        np.testing.assert_allclose(a2.cpu().numpy(), ra.numpy(), atol=1e-4, rtol=0)
+        np.testing.assert_allclose(c2.cpu().numpy(), rc.numpy(), atol=1e-4, rtol=0)

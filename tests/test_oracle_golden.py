@@ -164,3 +164,46 @@ def test_large_full_attention_matches_reference(golden_dir):
     y, masks = ref.forward_encoder(sd, LARGE, xp, lens, 0, 0, 0)
     np.testing.assert_array_equal(masks.numpy(), g["mask"])
     np.testing.assert_allclose(y.numpy(), g["out"], atol=1e-4, rtol=0)
+
+
+def _stream_steps(g, tag, cfg, seed0, sd):
+    from chunkformer_amd.weights import synthetic_features
+    from oracle import encoder_ref as ref
+    C, L, R = (int(v) for v in g[f"{tag}_clr"])
+    B = int(g[f"{tag}_B"])
+    nb, H, dk, d = cfg.num_blocks, cfg.n_heads, cfg.head_dim, cfg.d_model
+    att = torch.zeros(nb, B, H, L, 2 * dk)
+    cnn = torch.zeros(nb, B, d, 7)
+    outs = []
+    for i, tp in enumerate(g[f"{tag}_tp"].tolist()):
+        x = torch.stack(synthetic_features([8 * (tp - 1) + 15] * B, seed0 + i))
+        y, att, cnn = ref.forward_chunk(sd, cfg, x, att, cnn, C, L, R, offset=i * C)
+        outs.append(y)
+    return outs, att, cnn
+
+
+def test_oracle_forward_chunk_small(golden_dir):
+    """forward_chunk streaming steps (encoder.py:310-385) of the small model, batch 2, carried
+    caches, short last step: the oracle against the reference's own run (stream.npz)."""
+    from chunkformer_amd.config import SMALL
+    from chunkformer_amd.weights import synthetic_state_dict
+    g = np.load(os.path.join(golden_dir, "stream.npz"))
+    sd = synthetic_state_dict(SMALL, 1)
+    outs, att, cnn = _stream_steps(g, "a", SMALL, int(g["a_seed0"]), sd)
+    for i, y in enumerate(outs):
+        np.testing.assert_allclose(y.numpy(), g[f"a_out{i}"], atol=2e-5, rtol=0, err_msg=f"step {i}")
+    np.testing.assert_allclose(att.numpy(), g["a_att"], atol=2e-5, rtol=0)
+    np.testing.assert_allclose(cnn.numpy(), g["a_cnn"], atol=2e-5, rtol=0)
+
+
+def test_oracle_forward_chunk_large_4h(golden_dir):
+    """Same on the 12-layer d=512 4-head model, C=64 L=R=128 (head_dim 128)."""
+    from chunkformer_amd.config import LARGE_4H
+    from chunkformer_amd.weights import synthetic_state_dict
+    g = np.load(os.path.join(golden_dir, "stream.npz"))
+    sd = synthetic_state_dict(LARGE_4H, 0)
+    outs, att, cnn = _stream_steps(g, "b", LARGE_4H, int(g["b_seed0"]), sd)
+    for i, y in enumerate(outs):
+        np.testing.assert_allclose(y.numpy(), g[f"b_out{i}"], atol=1e-4, rtol=0, err_msg=f"step {i}")
+    np.testing.assert_allclose(att[g["b_att_layers"]].numpy(), g["b_att"], atol=1e-4, rtol=0)
+    np.testing.assert_allclose(cnn.numpy(), g["b_cnn"], atol=1e-4, rtol=0)

@@ -1,7 +1,7 @@
 """In-process A/B timing of model options on the bench workload (one encoder layer or more):
 interleaved rounds, per-class event times from libcfm's profiler (cdna guide §5.4 rule 24).
 
-    python tools/ab_bench.py --layers 1 --rounds 3 --variant fused_ffn=1,ffn_variant=0 --variant fused_ffn=0
+    python tools/ab_bench.py --layers 1 --rounds 3 --variant attn_reuse=0 --variant attn_reuse=1
 """
 import argparse
 import os

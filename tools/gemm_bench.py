@@ -28,6 +28,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--small", action="store_true")
+    ap.add_argument("--diag", type=int, default=0, help="timing diagnostic of the bf16 kernels (cfm_ops.h)")
     ap.add_argument("--only", default="")
     a = ap.parse_args()
     st = torch.cuda.current_stream().cuda_stream
@@ -46,13 +47,13 @@ def main():
         def run():
             if epi == 3:
                 L.check(L.cfm_op_gemm(1, epi, act, A.data_ptr(), K, W.data_ptr(), K, Mr, N, K, bias.data_ptr(), 1.0,
-                                      q.data_ptr(), 512, 128, kv.data_ptr(), 512, None, 0, None, int(a.small), st))
+                                      q.data_ptr(), 512, 128, kv.data_ptr(), 512, None, 0, None, int(a.small) | (a.diag << 8), st))
             elif epi == 2:
                 L.check(L.cfm_op_gemm(1, epi, act, A.data_ptr(), K, W.data_ptr(), K, Mr, N, K, bias.data_ptr(), 0.5,
-                                      None, 0, 0, None, 0, x.data_ptr(), N, None, int(a.small), st))
+                                      None, 0, 0, None, 0, x.data_ptr(), N, None, int(a.small) | (a.diag << 8), st))
             else:
                 L.check(L.cfm_op_gemm(1, epi, act, A.data_ptr(), K, W.data_ptr(), K, Mr, N, K, bias.data_ptr(), 1.0,
-                                      out.data_ptr(), out.shape[1], 0, None, 0, None, 0, None, int(a.small), st))
+                                      out.data_ptr(), out.shape[1], 0, None, 0, None, 0, None, int(a.small) | (a.diag << 8), st))
         for _ in range(3):
             run()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

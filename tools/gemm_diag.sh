@@ -1,10 +1,10 @@
 # GEMM component timing on the encoder shapes: normal / no-MFMA / no-DMA / no-epilogue builds
-# (CFM_GEMM_DIAG, gemm_bf16.hip) + hipBLASLt reference.  Run via gpurun from the repo root.
+# (cfm_op_gemm variant bits 8-15) + hipBLASLt reference.  Run via gpurun from the repo root.
 set -e
 R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/gemm_diag
 mkdir -p $O
 for d in 0 1 2; do
-  CFM_GEMM_DIAG=$d timeout -k 10 120 python3 $R/tools/gemm_bench.py --iters 20 > $O/diag$d.log 2>&1
+  timeout -k 10 120 python3 $R/tools/gemm_bench.py --iters 20 --diag $d > $O/diag$d.log 2>&1
 done
 timeout -k 10 120 python3 $R/tools/torch_gemm_ref.py > $O/hipblaslt.log 2>&1

@@ -27,7 +27,6 @@ CLASSES = [
     ("conv_dw_ln_silu", "conv_dw_ln_silu"),
     ("ln_kernel", "layernorm"),
     ("ln2_kernel", "layernorm2"),
-    ("ffn_fused_kernel", "ffn_fused"),
 ]
 
 
