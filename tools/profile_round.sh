@@ -3,7 +3,7 @@
 #   then the plain bench line.  Summaries land in gpurun_out/prof_<round>/; copy them to
 #   profiles/<round>_* (traffic.json, kernel_stats.csv, bench.json) afterwards.
 set -e
-RND=${1:-r01}
+RND=${1:-r02}
 R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/prof_$RND
 mkdir -p $O
