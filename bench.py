@@ -144,6 +144,12 @@ def committed_traffic(cls: str = "ffn_w1_gemm"):
         return None, None
 
 
+def apply_opts(enc, opts):
+    for kv in opts:
+        k, v = kv.split("=")
+        enc.set_option(k, int(v, 0))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -163,6 +169,8 @@ def main():
     ap.add_argument("--hours", type=float, default=16.0, help="endless: audio hours")
     ap.add_argument("--tbd", type=int, default=1800, help="endless: total_batch_duration (s)")
     ap.add_argument("--batch", type=int, default=256, help="full: utterances of T=3000 frames")
+    ap.add_argument("--opt", action="append", default=[], metavar="KEY=VALUE",
+                    help="per-model kernel option (cfm_model_set_option), A/B runs only")
     args = ap.parse_args()
     if args.config in ("endless", "full"):
         return bench_single(args)
@@ -194,6 +202,7 @@ def main():
                       for p in mine)
 
     enc = ChunkFormerEncoder(LARGE, synthetic_state_dict(LARGE, 0), device=dev, dtype=args.dtype)
+    apply_opts(enc, args.opt)
 
     def step():
         return enc.forward_parallel_chunk(xs, xs_lens, C, L, R)
@@ -336,6 +345,7 @@ def bench_single(args):
     torch.cuda.set_device(dev)
     model = ChunkFormerModel(LARGE, synthetic_state_dict(LARGE, 0), dtype=args.dtype, device=dev)
     enc = model.encoder
+    apply_opts(enc, args.opt)
     g = torch.Generator(device=dev).manual_seed(1234)
     d_, ff_ = LARGE.d_model, LARGE.ffn_dim
     if args.config == "endless":

@@ -32,6 +32,8 @@ struct EpiArgs {
   int small_tiles = 0;           // force the 128 x 128 kernel (cfm_op_gemm A/B)
 };
 
+enum { SITE_QKV = 1, SITE_OPROJ = 2, SITE_PW2 = 4, SITE_FFN2 = 8, SITE_FFN1 = 16, SITE_PW1 = 32, SITE_FE = 64 };
+
 // Per-model kernel tuning (cfm_model_set_option); the defaults are the measured best
 struct Tuning {
   int gemm_diag = 0, gemm_wst = 1, store_mode = 0, col_group = 0;
@@ -39,10 +41,12 @@ struct Tuning {
   int conv_dot2 = 1;             // conv module: bf16 dot2 kernel (0: per-tap f32 kernel)
   int conv_dma = 1;              // conv module: LDS-DMA window staging (0: register staging)
   int dw2_seg = 4;               // front-end dw2: row segments per walk
-  void apply(EpiArgs& e) const {
+  // GEMM sites whose bf16 outputs are stored non-temporally ("nt_sites" bit mask, SITE_* below)
+  int nt_sites = 0;
+  void apply(EpiArgs& e, int site = 0) const {
     e.diag = gemm_diag;
     e.wst = gemm_wst;
-    e.store_mode = store_mode;
+    e.store_mode = (nt_sites & site) ? 2 : store_mode;
     e.col_group = col_group;
   }
 };

@@ -249,6 +249,7 @@ static int launch256(const bf16* A, int lda, const bf16* W, int ldw, int M, int 
   // ep.diag (timing diagnostics, model option "gemm_diag"): 1 no MFMA, 2 no DMA in the loop, 3 no
   // epilogue, 5 / 6 wave-group priorities
 #define G256(D) hipLaunchKernelGGL((gemm_bf16_256_kernel<EPI, ACT, D>), dim3(grid), dim3(512), 0, st, A, lda, W, ldw, M, N, K, ep)
+#ifdef CFM_GEMM_DIAG
   switch (ep.diag) {
     case 1: G256(1); break;
     case 2: G256(2); break;
@@ -257,6 +258,9 @@ static int launch256(const bf16* A, int lda, const bf16* W, int ldw, int M, int 
     case 6: G256(6); break;
     default: G256(0); break;
   }
+#else
+  G256(0);
+#endif
 #undef G256
   CFM_CHECK_LAUNCH();
   return 0;

@@ -39,6 +39,9 @@ constexpr int WST_NSLOT = 16;
 constexpr int WST_DEPTH = WST_NSLOT - 1;         // steps in flight ahead of the one being read
 }  // namespace
 
+#ifndef WSP_LGKM
+#define WSP_LGKM 1   // 0: every K-step closes with lgkmcnt(0) (re-seed reads waited at once)
+#endif
 #define WST_VMCNT(N) asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory")
 
 // acc += W-fragment (AGPR, "a") x A-fragment (VGPR): the 256 weight registers per lane live in the
@@ -94,6 +97,20 @@ constexpr int wsp_nops(int s) {
   return EPI == EPI_GLU ? ((s & 1) ? 27 : 24) : 2 * wsp_half<ACT>() + 5;
 }
 constexpr int wsp_lo(int i, int n) { return (i * n + 31) / 32; }   // first op of gap i
+constexpr int wsp_gap(int o, int n) {                                  // gap that carries op o
+  int i = 0;
+  while (i < 31 && wsp_lo(i + 1, n) <= o) ++i;
+  return i;
+}
+// re-seed reads (LDS) issued after the step's last A-fragment read (gap 14): the step's closing
+// wait leaves exactly these in flight (they land before the next tile's first MFMA on that buffer,
+// which the last step of a tile waits for in full)
+template <int EPI, int ACT>
+constexpr int wsp_late_seeds(int s) {
+  const int n = wsp_nops<EPI, ACT>(s), H = wsp_half<ACT>() + 1;
+  const int o0 = EPI == EPI_GLU ? 22 : H - 1, o1 = EPI == EPI_GLU ? 23 : 2 * H - 1;
+  return (wsp_gap(o0, n) >= 14) + (wsp_gap(o1, n) >= 14);
+}
 }  // namespace
 
 template <int EPI, int ACT, int DIAG = 0>
@@ -186,6 +203,10 @@ __global__ __launch_bounds__(256, 1) void gemm_wsp_kernel(const bf16* __restrict
   unsigned voffS[2];
 #pragma unroll
   for (int p = 0; p < 2; ++p) voffS[p] = (unsigned)(fr * old[p] + lcol) * 2;
+  if constexpr (DIAG == 7) {   // timing only (wrong layout): every store 8 full 128-B rows
+#pragma unroll
+    for (int p = 0; p < 2; ++p) voffS[p] = (unsigned)(((fr & 7) + 8 * p) * old[p] - 32 * p + ((fr >> 3) * 4 + g) * 8) * 2;
+  }
 
   const unsigned lds_base = (unsigned)(size_t)(__attribute__((address_space(3))) char*)smem;
   const int key = (fr >> 1) & 7;
@@ -273,33 +294,36 @@ __global__ __launch_bounds__(256, 1) void gemm_wsp_kernel(const bf16* __restrict
       pin(et[i]);
     };
     if constexpr (EPI == EPI_GLU) {
+      // ops 0-19 gate chain, 20-21 packs, 22-23 re-seeds (both accumulators are dead after op 19),
+      // then on odd S the 2 swaps and the store
       constexpr int jj = S >> 1, h = S & 1;
-      constexpr int nseed = h ? 25 : 22;
       auto gate = [&](int i) -> float { return a[2 * h + 1][jj][i]; };
       auto lin = [&](int i) -> float { return a[2 * h][jj][i]; };
-      if constexpr (O >= nseed) {
-        seed(std::integral_constant<int, 2 * h + (O - nseed)>{}, jj);
+      if constexpr (O == 22 || O == 23) {
+        seed(std::integral_constant<int, 2 * h + (O - 22)>{}, jj);
       } else if constexpr (DIAG == 3) {
       } else if constexpr (O < 20) {
         chain(O, gate, lin);
       } else if constexpr (O < 22) {
         epk[2 * h + O - 20] = pack_bf16x2(et[2 * (O - 20)], et[2 * (O - 20) + 1]);
         pin(epk[2 * h + O - 20]);
-      } else if constexpr (O < 24) {
-        swap(O - 22);
-      } else {   // O == 24
+      } else if constexpr (O < 26) {
+        swap(O - 24);
+      } else {   // O == 26
         store(0, jj);
       }
     } else {
+      // ops: per half q (one 16-column n-block) H - 2 activation ops, 2 packs and the re-seed of
+      // that n-block's accumulator (dead after the packs), then 2 swaps and the store
       constexpr int p = S & 1, jj = S >> 1;   // the two 64-B halves of a 128-B row piece in consecutive steps
-      constexpr int H = wsp_half<ACT>();
-      if constexpr (O >= 2 * H + 3) {
-        seed(std::integral_constant<int, 2 * p + (O - 2 * H - 3)>{}, jj);
+      constexpr int H = wsp_half<ACT>() + 1;
+      if constexpr (O < 2 * H && O % H == H - 1) {
+        seed(std::integral_constant<int, 2 * p + O / H>{}, jj);
       } else if constexpr (DIAG == 3) {
       } else if constexpr (O < 2 * H) {
         constexpr int q = O / H, o = O % H;
         auto val = [&](int i) -> float { return a[2 * p + q][jj][i]; };
-        if constexpr (o < H - 2) {
+        if constexpr (o < H - 3) {
           if constexpr (ACT == ACT_SILU) {
             chain(o, val, val);
           } else {
@@ -307,7 +331,7 @@ __global__ __launch_bounds__(256, 1) void gemm_wsp_kernel(const bf16* __restrict
             pin(et[o]);
           }
         } else {
-          constexpr int k = o - (H - 2);   // pack k of this half: values 2k, 2k+1
+          constexpr int k = o - (H - 3);   // pack k of this half: values 2k, 2k+1
           if constexpr (ACT == ACT_NONE) epk[2 * q + k] = pack_bf16x2(val(2 * k), val(2 * k + 1));
           else epk[2 * q + k] = pack_bf16x2(et[2 * k], et[2 * k + 1]);
           pin(epk[2 * q + k]);
@@ -334,7 +358,7 @@ __global__ __launch_bounds__(256, 1) void gemm_wsp_kernel(const bf16* __restrict
       // land in dead slots -- so exactly 28 loads are younger-or-equal here) and, after the
       // barrier, every wave's pieces of it; every wave is also past its reads of slot y-1, which
       // the DMA below refills
-      if constexpr (DIAG != 2) WST_VMCNT(26);
+      if constexpr (DIAG != 2 && DIAG != 4) WST_VMCNT(26);
       asm volatile("s_barrier" ::: "memory");
       bf16x8(&cur)[4][2] = afr[KS & 1];
       bf16x8(&nxt)[4][2] = afr[(KS + 1) & 1];
@@ -346,14 +370,20 @@ __global__ __launch_bounds__(256, 1) void gemm_wsp_kernel(const bf16* __restrict
           constexpr int rmb = (i >> 1) & 3, rkh = i >> 3;
           lds_read_into<(slot_n & 7) * WST_SLOT + rmb * 2048>(nxt[rmb][rkh], rdb[slot_n >> 3][rkh]);
         }
-        if constexpr (i == 6 || i == 22)
+        if constexpr ((i == 6 || i == 22) && DIAG != 4)
           issue_piece(KS == 0 ? dA1 : dA2, std::integral_constant<int, i == 22 ? 1 : 0>{},
                       std::integral_constant<int, (KS + WST_DEPTH) % WST_NK>{},
                       std::integral_constant<int, slot_d>{});
         sfor<wsp_lo(i, n_ops), wsp_lo(i + 1, n_ops)>([&](auto Oc) { epi_op(KSc, Oc, acc[1 - BUF], sd, std::true_type{}); });
         __builtin_amdgcn_sched_barrier(0);
       });
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      constexpr int late = wsp_late_seeds<EPI, ACT>(KS);
+      if constexpr (KS == WST_NK - 1 || late == 0 || !WSP_LGKM)
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      else if constexpr (late == 1)
+        asm volatile("s_waitcnt lgkmcnt(1)" ::: "memory");
+      else
+        asm volatile("s_waitcnt lgkmcnt(2)" ::: "memory");
     });
   };
   auto drain = [&](f32x4(&a)[4][4], int rt) {
@@ -412,17 +442,27 @@ static int launch_wst(const bf16* A, int lda, const bf16* W, int ldw, int M, int
   const size_t ld = EPI == EPI_QKV ? 2 * (size_t)ep.d : (size_t)ep.ldo;
   if ((size_t)M * ld * 2 >= (1ull << 31)) return -1;
 #define WSP_LAUNCH(D) hipLaunchKernelGGL((gemm_wsp_kernel<EPI, ACT, D>), dim3(n_cu), dim3(256), 0, st, A, lda, W, ldw, M, N, ep)
-  // DIAG (timing experiments only, model option "gemm_diag"): 1 = no MFMAs, 2 = no DMA wait (stale LDS),
-  // 3 = no epilogue (re-seeds only), 5 = no stores, 8 / 9 = nt / sc1 store policy
+#ifdef CFM_GEMM_DIAG
+  // DIAG (timing experiments only, diagnostic builds, model option "gemm_diag"): 1 = no MFMAs,
+  // 2 = no DMA wait (stale LDS), 3 = no epilogue (re-seeds only), 4 = no DMA in the loop (stale LDS),
+  // 5 = no stores, 7 = full-line stores (wrong layout)
   switch (ep.diag) {
     case 1: WSP_LAUNCH(1); break;
     case 2: WSP_LAUNCH(2); break;
     case 3: WSP_LAUNCH(3); break;
+    case 4: WSP_LAUNCH(4); break;
     case 5: WSP_LAUNCH(5); break;
-    case 8: WSP_LAUNCH(8); break;
-    case 9: WSP_LAUNCH(9); break;
-    default: WSP_LAUNCH(0); break;
+    case 7: WSP_LAUNCH(7); break;
+    default: break;
   }
+  if (ep.diag >= 1 && ep.diag <= 7 && ep.diag != 6) {
+    CFM_CHECK_LAUNCH();
+    return 0;
+  }
+#endif
+  // store policy (per GEMM site, EpiArgs::store_mode): 2 = nt
+  if (ep.store_mode == 2) WSP_LAUNCH(8);
+  else WSP_LAUNCH(0);
 #undef WSP_LAUNCH
   CFM_CHECK_LAUNCH();
   return 0;

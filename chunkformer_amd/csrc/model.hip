@@ -180,9 +180,9 @@ struct ModelT : public cfm_model {
   }
 
   // epilogue args carrying this model's kernel tuning
-  EpiArgs E() const {
+  EpiArgs E(int site = 0) const {
     EpiArgs e;
-    tune.apply(e);
+    tune.apply(e, site);
     return e;
   }
 
@@ -264,10 +264,10 @@ struct ModelT : public cfm_model {
       const int ng = std::min(G, nwin - g0);
       PROF(PC_FE_CONV, frontend_conv0_dw<T>(feats, meta + (size_t)g0 * PLAN_REC, PLAN_REC, ng, Wn, fe.cm, fe.ci, fe.w0, fe.b0,
                                 fe.w1, fe.b1, fe.wpack, d, w.feA, st));
-      EpiArgs e1 = E(); e1.bias = fe.b_pw1; e1.out = w.feB; e1.ldo = d;
+      EpiArgs e1 = E(SITE_FE); e1.bias = fe.b_pw1; e1.out = w.feB; e1.ldo = d;
       PROF(PC_FE_GEMM, gemm<T>(EPI_STORE, ACT_RELU, w.feA, d, (const T*)fe.pw1, d, ng * T2 * 19, d, d, e1, st));
       PROF(PC_FE_DW2, frontend_dw2<T>(w.feB, ng, T2, d, fe.w2, fe.b2, w.feA, st, tune.dw2_seg));
-      EpiArgs e2 = E(); e2.bias = fe.b_pw2; e2.out = w.feC + (size_t)g0 * T3 * 9 * d; e2.ldo = d;
+      EpiArgs e2 = E(SITE_FE); e2.bias = fe.b_pw2; e2.out = w.feC + (size_t)g0 * T3 * 9 * d; e2.ldo = d;
       PROF(PC_FE_GEMM, gemm<T>(EPI_STORE, ACT_RELU, w.feA, d, (const T*)fe.pw2, d, ng * T3 * 9, d, d, e2, st));
     }
     { EpiArgs e3 = E(); e3.bias = fe.b_out; e3.out = w.x; e3.ldo = d; e3.row_off = 0; e3.alpha = std::sqrt((float)d);
@@ -308,9 +308,9 @@ struct ModelT : public cfm_model {
     };
     // y = w2 . SiLU(w1 . h + b1) + b2: two GEMMs through w.hid
     auto ffn = [&](const void* w1, const float* b1, const void* w2, const float* b2, T* yout) -> cfm_status {
-      { EpiArgs e = E(); e.bias = b1; e.out = w.hid; e.ldo = ff;
+      { EpiArgs e = E(SITE_FFN1); e.bias = b1; e.out = w.hid; e.ldo = ff;
         PROF(PC_FFN1, gemm<T>(EPI_STORE, ACT_SILU, w.h, d, (const T*)w1, d, rows, ff, d, e, st)); }
-      { EpiArgs e = E(); e.bias = b2; e.out = yout; e.ldo = d;
+      { EpiArgs e = E(SITE_FFN2); e.bias = b2; e.out = yout; e.ldo = d;
         PROF(PC_FFN2, gemm<T>(EPI_STORE, ACT_NONE, w.hid, ff, (const T*)w2, ff, rows, d, ff, e, st)); }
       return CFM_OK;
     };
@@ -325,7 +325,7 @@ struct ModelT : public cfm_model {
         if (stream) PROF(PC_CACHE, att_cache_in_hl<T>(aci + l * att_ls, H, L, dk, w.kv, st));
         else PROF(PC_CACHE, att_cache_in<T>(aci + l * att_ls, L, 2 * d, w.kv, st));
       }
-      { EpiArgs e = E(); e.bias = Lw.b_qkv; e.out = w.q; e.out2 = w.kv; e.row_off = kvoff; e.d = d; e.dk = dk;
+      { EpiArgs e = E(SITE_QKV); e.bias = Lw.b_qkv; e.out = w.q; e.out2 = w.kv; e.row_off = kvoff; e.d = d; e.dk = dk;
         PROF(PC_QKV, gemm<T>(EPI_QKV, ACT_NONE, w.h, d, (const T*)Lw.qkv, d, rows, 3 * d, d, e, st)); }
       if (aci && aco) {
         if (stream) PROF(PC_CACHE, att_cache_out_hl<T>(w.kv, cache_start, H, L, dk, aco + l * att_ls, st));
@@ -347,18 +347,18 @@ struct ModelT : public cfm_model {
         KCHK(r);
         prof_end(PC_ATTN, st, pb_);
       }
-      { EpiArgs e = E(); e.bias = Lw.b_o; e.out = w.y2; e.ldo = d;
+      { EpiArgs e = E(SITE_OPROJ); e.bias = Lw.b_o; e.out = w.y2; e.ldo = d;
         PROF(PC_OPROJ, gemm<T>(EPI_STORE, ACT_NONE, w.ao, d, (const T*)Lw.wo, d, rows, d, d, e, st)); }
       // convolution module: x += 0.5 y_ffm + y_attn, stored
       PROF(PC_LN, layernorm<T>(w.x, resid2(w.y, 0.5f, nullptr, w.y2, 1.f, nullptr), rows, d, Lw.ln_conv_w, Lw.ln_conv_b,
                                eps, w.h, (masked || stream) ? nullptr : rmask, st));
       if (cci) PROF(PC_CACHE, cnn_cache_in<T>(cci + l * cnn_ls, d, 7, w.glu, st));
-      { EpiArgs e = E(); e.bias = Lw.b_pw1; e.out = w.glu; e.ldo = d; e.row_off = gluoff;
+      { EpiArgs e = E(SITE_PW1); e.bias = Lw.b_pw1; e.out = w.glu; e.ldo = d; e.row_off = gluoff;
         PROF(PC_PW1, gemm<T>(EPI_GLU, ACT_NONE, w.h, d, (const T*)Lw.pw1, d, rows, 2 * d, d, e, st)); }
       if (cci && cco) PROF(PC_CACHE, cnn_cache_out<T>(w.glu, cache_start, d, 7, cco + l * cnn_ls, st));
       PROF(PC_CONV, conv_dw_ln_silu<T>(w.glu, convd, nconv, d, Lw.dw_t, Lw.b_dw, Lw.cn_w, Lw.cn_b, eps, w.cv, st,
                                         tune.conv_dot2, tune.conv_dma));
-      { EpiArgs e = E(); e.bias = Lw.b_pw2; e.out = w.y; e.ldo = d;
+      { EpiArgs e = E(SITE_PW2); e.bias = Lw.b_pw2; e.out = w.y; e.ldo = d;
         PROF(PC_PW2, gemm<T>(EPI_STORE, ACT_NONE, w.cv, d, (const T*)Lw.pw2, d, rows, d, d, e, st)); }
       // FFN (x 0.5); x + y_conv is not stored: norm_final re-applies it
       { ResidAdd<T> r = resid(w.y, 1.f, rmask); r.defer = true;
@@ -652,7 +652,7 @@ cfm_status cfm_model_set_option(cfm_model* m, const char* key, int64_t value) {
     const std::pair<const char*, int*> knobs[] = {
         {"gemm_diag", &m->tune.gemm_diag}, {"gemm_wst", &m->tune.gemm_wst},   {"store_mode", &m->tune.store_mode},
         {"col_group", &m->tune.col_group}, {"attn_reuse", &m->tune.attn_reuse}, {"conv_dot2", &m->tune.conv_dot2},
-        {"conv_dma", &m->tune.conv_dma},   {"dw2_seg", &m->tune.dw2_seg}};
+        {"conv_dma", &m->tune.conv_dma},   {"dw2_seg", &m->tune.dw2_seg},   {"nt_sites", &m->tune.nt_sites}};
     for (auto& k : knobs)
       if (!std::strcmp(key, k.first)) { *k.second = (int)value; return CFM_OK; }
   }
@@ -762,6 +762,8 @@ cfm_status cfm_op_gemm(int32_t dtype, int32_t epi, int32_t act, const void* A, i
   EpiArgs e;
   e.bias = bias; e.alpha = alpha; e.out = out; e.out2 = out2; e.ldo = ldo; e.row_off = row_off; e.x = x; e.ldx = ldx;
   e.rowmask = rowmask; e.d = d; e.small_tiles = variant & 1; e.diag = (variant >> 8) & 0xff;
+  e.store_mode = (variant >> 16) & 3;
+  if ((variant >> 18) & 3) e.wst = ((variant >> 18) & 3) == 3 ? 0 : 1;
   int r;
   if (dtype == CFM_DTYPE_F32)
     r = gemm<float>(epi, act, (const float*)A, lda, (const float*)W, ldw, M, N, K, e, (hipStream_t)stream);

@@ -30,10 +30,14 @@ def main():
     ap.add_argument("--small", action="store_true")
     ap.add_argument("--diag", type=int, default=0, help="timing diagnostic of the bf16 kernels (cfm_ops.h)")
     ap.add_argument("--only", default="")
+    ap.add_argument("--store", type=int, default=0, help="epilogue store policy (EpiArgs::store_mode: 2 = nt)")
+    ap.add_argument("--wst", type=int, default=0, help="K = 512 weight-stationary kernel: 1 on, 3 off")
     a = ap.parse_args()
     st = torch.cuda.current_stream().cuda_stream
     for name, N, K, epi, act in SHAPES:
-        if a.only and a.only != name:
+        if a.only and name not in a.only.split(","):
+            continue
+        if a.diag in (3, 4, 5, 7) and K != 512:   # those diagnostics exist only in the K = 512 kernel
             continue
         Mr = M if name != "fe_pw1" else 2845 * 2451 // 4
         A = torch.randn(Mr, K, device="cuda").to(torch.bfloat16)
@@ -47,13 +51,13 @@ def main():
         def run():
             if epi == 3:
                 L.check(L.cfm_op_gemm(1, epi, act, A.data_ptr(), K, W.data_ptr(), K, Mr, N, K, bias.data_ptr(), 1.0,
-                                      q.data_ptr(), 512, 128, kv.data_ptr(), 512, None, 0, None, int(a.small) | (a.diag << 8), st))
+                                      q.data_ptr(), 512, 128, kv.data_ptr(), 512, None, 0, None, int(a.small) | (a.diag << 8) | (a.store << 16) | (a.wst << 18), st))
             elif epi == 2:
                 L.check(L.cfm_op_gemm(1, epi, act, A.data_ptr(), K, W.data_ptr(), K, Mr, N, K, bias.data_ptr(), 0.5,
-                                      None, 0, 0, None, 0, x.data_ptr(), N, None, int(a.small) | (a.diag << 8), st))
+                                      None, 0, 0, None, 0, x.data_ptr(), N, None, int(a.small) | (a.diag << 8) | (a.store << 16) | (a.wst << 18), st))
             else:
                 L.check(L.cfm_op_gemm(1, epi, act, A.data_ptr(), K, W.data_ptr(), K, Mr, N, K, bias.data_ptr(), 1.0,
-                                      out.data_ptr(), out.shape[1], 0, None, 0, None, 0, None, int(a.small) | (a.diag << 8), st))
+                                      out.data_ptr(), out.shape[1], 0, None, 0, None, 0, None, int(a.small) | (a.diag << 8) | (a.store << 16) | (a.wst << 18), st))
         for _ in range(3):
             run()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
