@@ -161,7 +161,7 @@ def main():
     ap.add_argument("--no-gather-logp", action="store_true", help="sharded: skip the bf16 log-prob all-gather")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-breakdown", action="store_true")
-    ap.add_argument("--config", default="auto", choices=["auto", "masked", "sharded", "endless", "full"],
+    ap.add_argument("--config", default="auto", choices=["auto", "masked", "sharded", "endless", "full", "fbank"],
                     help="auto = masked at 1 GPU, sharded at N > 1; masked = configs[1] (240 min per GPU, the "
                          "headline line); sharded = configs[2] (one 980-min batch over all ranks); endless = "
                          "configs[3] (16 h endless_decode, graph-replayed segments); full = configs[4] (full "
@@ -174,6 +174,8 @@ def main():
     args = ap.parse_args()
     if args.config in ("endless", "full"):
         return bench_single(args)
+    if args.config == "fbank":
+        return bench_fbank(args)
 
     rank, world, local = init_from_env()
     local = local % torch.cuda.device_count()   # (rehearsal of several ranks on one GPU: gloo backend)
@@ -420,6 +422,62 @@ def bench_single(args):
                      "peak": peak, "unit": "TFLOP/s", "frac": round(achieved / peak, 4) if achieved else None,
                      "traffic": None, "flops_per_launch": fl_launch, "avg_launch_ms": round(avg_s * 1e3, 4),
                      "launches": n1},
+    }
+    print(json.dumps(res), flush=True)
+
+
+def bench_fbank(args):
+    """GPU Kaldi fbank (§8(f) row 2, chunkformer_model.py:306-314 parameters) over `--hours` of
+    16 kHz int16-scale synthetic audio resident in HBM: frames/s, HBM roofline of the kernel
+    (samples in + features out per launch), the CPU oracle (oracle/fbank_ref.py, torch float32,
+    all cores) on 60 s of the same audio beside it."""
+    from chunkformer_amd.fbank import KaldiFbank
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    n = int(args.hours * 3600 * 16000)
+    g = torch.Generator(device=dev).manual_seed(7)
+    x = (torch.randn(n, generator=g, device=dev) * 3000).round_()
+    fb = KaldiFbank(dev, num_mel_bins=80, frame_length=25, frame_shift=10, dither=0.0, energy_floor=0.0,
+                    sample_frequency=16000)
+    frames = fb.num_frames(n)
+    for _ in range(args.warmup):
+        fb(x)
+    torch.cuda.synchronize()
+    st = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record(st)
+    for _ in range(args.steps):
+        fb(x)
+    e1.record(st)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    kern_s = e0.elapsed_time(e1) / 1e3 / args.steps
+    nbytes = n * 4 + frames * 80 * 4
+    from oracle import fbank_ref
+    xs = x[: 60 * 16000].cpu()
+    cpu_model, threads = host_cpu()
+    torch.set_num_threads(threads)
+    c0 = time.perf_counter()
+    reps = 0
+    while time.perf_counter() - c0 < 10.0:
+        fbank_ref.fbank(xs, num_mel_bins=80, frame_length=25, frame_shift=10, dither=0.0, energy_floor=0.0)
+        reps += 1
+    cpu_fps = reps * fbank_ref.num_frames(xs.numel(), 400, 160) / (time.perf_counter() - c0)
+    res = {
+        "metric": "fbank frames/sec (80-dim Kaldi log-mel, 25/10 ms, povey) from 16 kHz audio resident in HBM",
+        "value": round(frames * args.steps / dt, 1), "unit": "fbank-frames/s", "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic (N(0, 3000^2) int16-scale samples)",
+        "config": {"workload": f"kaldi.fbank over one {args.hours:g} h waveform ({n} samples, {frames} frames)",
+                   "parallelism": "single GPU"},
+        "roofline": {"bound": "hbm", "kernel": "fbank_kernel<8> (LDS radix-2 FFT, 16 frames per block)",
+                     "achieved": round(nbytes / kern_s / 1e9, 1), "peak": 8000.0, "unit": "GB/s",
+                     "frac": round(nbytes / kern_s / 1e9 / 8000.0, 4), "traffic": None,
+                     "algorithmic_bytes_per_launch": nbytes, "avg_launch_ms": round(kern_s * 1e3, 3)},
+        "cpu_baseline": {"value": round(cpu_fps, 1), "unit": "fbank-frames/s", "cores": threads, "cpu": cpu_model,
+                         "kind": "port", "sample": "oracle/fbank_ref.py (torchaudio kaldi.fbank restated, torch "
+                                                   "float32 CPU) on the first 60 s of the same audio, repeated ~10 s"},
     }
     print(json.dumps(res), flush=True)
 

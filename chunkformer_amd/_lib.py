@@ -74,6 +74,19 @@ cfm_ctc_logprobs = _sig("cfm_ctc_logprobs", I32, P, P, I32, P, P, P, SZ, P)
 cfm_ctc_ids_workspace_bytes = _sig("cfm_ctc_ids_workspace_bytes", SZ, P, I32)
 cfm_ctc_ids = _sig("cfm_ctc_ids", I32, P, P, I32, P, P, SZ, P)
 cfm_ctc_collapse = _sig("cfm_ctc_collapse", I32, P, P, P, I32, I32, I32, P, P, P, P, P, P)
+# Kaldi fbank (include/cfm.h)
+class CfmFbankConfig(ctypes.Structure):
+    _fields_ = [("sample_frequency", ctypes.c_float), ("frame_length_ms", ctypes.c_float),
+                ("frame_shift_ms", ctypes.c_float), ("num_mel_bins", I32), ("low_freq", ctypes.c_float),
+                ("high_freq", ctypes.c_float), ("preemphasis_coefficient", ctypes.c_float), ("dither", ctypes.c_float),
+                ("remove_dc_offset", I32), ("round_to_power_of_two", I32), ("snip_edges", I32), ("use_energy", I32),
+                ("use_log_fbank", I32), ("window_type", I32)]
+
+
+cfm_fbank_create = _sig("cfm_fbank_create", I32, ctypes.POINTER(CfmFbankConfig), I32, ctypes.POINTER(P))
+cfm_fbank_destroy = _sig("cfm_fbank_destroy", None, P)
+cfm_fbank_num_frames = _sig("cfm_fbank_num_frames", I64, P, I64)
+cfm_fbank_compute = _sig("cfm_fbank_compute", I32, P, P, I64, P, P)
 # include/cfm_ops.h
 cfm_op_gemm = _sig("cfm_op_gemm", I32, I32, I32, I32, P, I32, P, I32, I32, I32, I32, P, ctypes.c_float, P, I32, I32, P,
                    I32, P, I32, P, I32, P)
@@ -83,7 +96,8 @@ EXPORTED = ["cfm_version", "cfm_last_error", "cfm_model_create", "cfm_model_dest
             "cfm_plan_masked", "cfm_plan_padded", "cfm_workspace_bytes_masked", "cfm_workspace_bytes_padded",
             "cfm_encode_masked", "cfm_encode_padded", "cfm_masks_from_plan", "cfm_profile_read", "cfm_ctc_workspace_bytes",
             "cfm_ctc_logprobs", "cfm_ctc_ids_workspace_bytes", "cfm_ctc_ids", "cfm_ctc_collapse",
-            "cfm_plan_stream", "cfm_workspace_bytes_stream", "cfm_encode_stream"]
+            "cfm_plan_stream", "cfm_workspace_bytes_stream", "cfm_encode_stream",
+            "cfm_fbank_create", "cfm_fbank_destroy", "cfm_fbank_num_frames", "cfm_fbank_compute"]
 
 
 def profile_read(h):

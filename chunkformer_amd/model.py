@@ -6,10 +6,11 @@
   batch_decode     chunkformer_model.py:462-552   duration-budget grouping -> masked batch -> CTC
   from_pretrained  chunkformer_model.py:107-200   LOCAL directory only (no hub access)
 
-Audio loading + fbank (`_load_audio_and_extract_features`, 276-319) is outside the hot
-path and its dependencies (pydub, torchaudio) are absent: wherever the reference takes an
-`audio_path`, this mirror takes 80-dim fbank features -- a `[T, 80]` tensor, or a path to
-a `.npy` (loaded with allow_pickle=False) / `.pt` (torch.load weights_only=True) file.
+Audio (`_load_audio_and_extract_features`, 276-318): wherever the reference takes an
+`audio_path`, this mirror takes a 16-bit PCM `.wav` path (decoded with the standard library,
+features by the GPU Kaldi fbank of fbank.py with the reference's parameters, config
+`fbank_conf` / `resample_conf`), or 80-dim fbank features directly -- a `[T, 80]` tensor, or a
+path to a `.npy` (loaded with allow_pickle=False) / `.pt` (torch.load weights_only=True) file.
 
 CTC post-processing (remove_duplicates_and_blank and get_output_with_timestamps' sentence
 split, chunkformer/utils/model_utils.py:23-221) runs on the device (cfm_ctc_collapse); only
@@ -121,7 +122,11 @@ def budget_groups(lens: Sequence[int], total_batch_duration: float) -> List[List
     return groups
 
 
-def _load_features(x: Features) -> torch.Tensor:
+def _load_features(x: Features, featurize=None) -> torch.Tensor:
+    if isinstance(x, str) and x.lower().endswith(".wav"):
+        from .fbank import load_wav
+        samples, sr = load_wav(x)
+        return featurize(samples, sr)
     if isinstance(x, torch.Tensor):
         t = x
     elif isinstance(x, np.ndarray):
@@ -132,8 +137,8 @@ def _load_features(x: Features) -> torch.Tensor:
         elif x.endswith(".pt"):
             t = torch.load(x, map_location="cpu", weights_only=True)
         else:
-            raise ValueError(f"{x}: audio decoding/fbank is not part of this build; pass 80-dim fbank "
-                             "features ([T, 80] tensor, .npy or .pt)")
+            raise ValueError(f"{x}: only 16-bit PCM .wav audio is decoded here (no pydub/ffmpeg); or pass "
+                             "80-dim fbank features ([T, 80] tensor, .npy or .pt)")
     else:
         raise TypeError(f"unsupported feature input {type(x)}")
     if t.dim() == 3 and t.shape[0] == 1:
@@ -148,12 +153,31 @@ class ChunkFormerModel:
     """encoder + CTC head; the inference API of chunkformer_model.py on libcfm."""
 
     def __init__(self, cfg: EncoderConfig, state_dict: Dict[str, torch.Tensor], dtype: str = "bf16", device=None,
-                 char_dict: Optional[Dict[int, str]] = None):
+                 char_dict: Optional[Dict[int, str]] = None, fbank_conf: Optional[dict] = None,
+                 resample_conf: Optional[dict] = None):
         self.config = cfg
         self.encoder = ChunkFormerEncoder(cfg, state_dict, device=device, dtype=dtype)
         self.device = self.encoder.device
         self.char_dict = char_dict
+        self.fbank_conf = dict(fbank_conf or {})
+        self.resample_conf = dict(resample_conf or {})
+        self._fbank = None
         self._endless_runners: Dict[tuple, EndlessGraphRunner] = {}
+
+    def extract_features(self, samples, sample_rate: Optional[int] = None) -> torch.Tensor:
+        """_load_audio_and_extract_features (chunkformer_model.py:276-318) after decoding:
+        kaldi.fbank with the config's num_mel_bins / frame_length / frame_shift, dither 0,
+        energy_floor 0, at resample_conf.resample_rate (16 kHz), on int16-scale samples; on the GPU."""
+        rate = int(self.resample_conf.get("resample_rate", 16000))
+        if sample_rate is not None and int(sample_rate) != rate:
+            raise ValueError(f"audio at {sample_rate} Hz: resampling is not part of this build, expected {rate} Hz")
+        if self._fbank is None:
+            from .fbank import KaldiFbank
+            self._fbank = KaldiFbank(self.device, num_mel_bins=int(self.fbank_conf.get("num_mel_bins", 80)),
+                                     frame_length=float(self.fbank_conf.get("frame_length", 25)),
+                                     frame_shift=float(self.fbank_conf.get("frame_shift", 10)), dither=0.0,
+                                     energy_floor=0.0, sample_frequency=float(rate))
+        return self._fbank(torch.as_tensor(samples, dtype=torch.float32))
 
     # ---------------------------------------------------------------- loading
     @classmethod
@@ -216,7 +240,8 @@ class ChunkFormerModel:
                     if len(arr) != 2:
                         raise AssertionError(f"bad vocab line {line!r}")
                     char_dict[int(arr[1])] = arr[0]
-        return cls(cfg, sd, dtype=dtype, device=device, char_dict=char_dict)
+        return cls(cfg, sd, dtype=dtype, device=device, char_dict=char_dict, fbank_conf=conf.get("fbank_conf"),
+                   resample_conf=conf.get("resample_conf"))
 
     # ---------------------------------------------------------------- API
     def encode(self, xs: torch.Tensor, xs_lens: torch.Tensor, chunk_size: Optional[int] = None,
@@ -245,7 +270,7 @@ class ChunkFormerModel:
         L = left_context_size if left_context_size is not None else 128
         R = right_context_size if right_context_size is not None else 128
         cfg, enc, dev = self.config, self.encoder, self.device
-        xs = _load_features(audio_path)
+        xs = _load_features(audio_path, self.extract_features)
         trunc, segs = endless_segments(xs.shape[0], C, L, R, total_batch_duration, cfg.num_blocks, cfg.kernel_size)
         xs_dev = xs.to(dev, torch.float32)
         ids, outs = [], []
@@ -292,7 +317,7 @@ class ChunkFormerModel:
         C = chunk_size if chunk_size is not None else 64
         L = left_context_size if left_context_size is not None else 128
         R = right_context_size if right_context_size is not None else 128
-        feats = [_load_features(a) for a in audio_paths]
+        feats = [_load_features(a, self.extract_features) for a in audio_paths]
         decodes = []
         for grp in budget_groups([f.shape[0] for f in feats], total_batch_duration):
             xs = [feats[i] for i in grp]

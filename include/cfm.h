@@ -184,6 +184,42 @@ cfm_status cfm_ctc_collapse(const int32_t* ids_dev, const int32_t* row_start_dev
                             int32_t* n_tokens_dev, int32_t* segments_dev /* [rows, 3] or NULL */,
                             int32_t* n_segments_dev /* [B] or NULL */, cfm_stream stream);
 
+/* ---- Kaldi log-mel filterbank (the reference's feature front: chunkformer_model.py:276-318 and
+ * dataset/processor.py:210-239 call torchaudio.compliance.kaldi.fbank).  Fields and defaults follow
+ * torchaudio's fbank() signature; the reference decodes with dither 0, energy_floor 0, 80 bins,
+ * 25 / 10 ms, povey window, int16-scale samples.  Supported: dither 0, snip_edges, use_energy 0,
+ * padded frames of 128 .. 1024 samples. */
+typedef enum { CFM_WINDOW_POVEY = 0, CFM_WINDOW_HAMMING = 1, CFM_WINDOW_HANNING = 2, CFM_WINDOW_RECTANGULAR = 3,
+               CFM_WINDOW_BLACKMAN = 4 } cfm_window_type;
+typedef struct {
+  float sample_frequency;        /* 16000 */
+  float frame_length_ms;         /* 25 */
+  float frame_shift_ms;          /* 10 */
+  int32_t num_mel_bins;          /* 80 in the reference (torchaudio default 23) */
+  float low_freq;                /* 20 */
+  float high_freq;               /* 0: Nyquist; < 0: offset from Nyquist */
+  float preemphasis_coefficient; /* 0.97 */
+  float dither;                  /* must be 0 */
+  int32_t remove_dc_offset;      /* 1 */
+  int32_t round_to_power_of_two; /* 1 */
+  int32_t snip_edges;            /* must be 1 */
+  int32_t use_energy;            /* must be 0 */
+  int32_t use_log_fbank;         /* 1 */
+  int32_t window_type;           /* cfm_window_type, POVEY (blackman uses coefficient 0.42) */
+} cfm_fbank_config;
+typedef struct cfm_fbank cfm_fbank;
+
+/* window, FFT twiddles and mel filters on `device` (replaces the per-call get_mel_banks /
+ * _feature_window_function of compliance/kaldi.py) */
+cfm_status cfm_fbank_create(const cfm_fbank_config* cfg, int32_t device, cfm_fbank** out);
+void cfm_fbank_destroy(cfm_fbank* h);
+/* frames of a waveform of num_samples samples: 1 + (n - win) / shift, 0 when n < win */
+int64_t cfm_fbank_num_frames(const cfm_fbank* h, int64_t num_samples);
+/* out_dev[frames, num_mel_bins] (f32) = kaldi.fbank(wave_dev[num_samples]) (f32 device samples,
+ * int16 scale); stream-ordered, no allocation, no host synchronisation */
+cfm_status cfm_fbank_compute(const cfm_fbank* h, const float* wave_dev, int64_t num_samples, float* out_dev,
+                             cfm_stream stream);
+
 #ifdef __cplusplus
 }
 #endif
