@@ -438,9 +438,8 @@ static int launch_wst(const bf16* A, int lda, const bf16* W, int ldw, int M, int
     if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0) n_cu = 256;
     n_cu = n_cu / 8 * 8;
   }
-  // 32-bit buffer-store offsets: every output row offset must stay below 2^31 bytes
-  const size_t ld = EPI == EPI_QKV ? 2 * (size_t)ep.d : (size_t)ep.ldo;
-  if ((size_t)M * ld * 2 >= (1ull << 31)) return -1;
+  // buffer descriptors are built per 64-row tile on 64-bit bases (offsets inside one tile stay
+  // below 64 rows x ld), so outputs past 2 GiB (a 980-minute batch's FFN hidden: 3 GB) stay here
 #define WSP_LAUNCH(D) hipLaunchKernelGGL((gemm_wsp_kernel<EPI, ACT, D>), dim3(n_cu), dim3(256), 0, st, A, lda, W, ldw, M, N, ep)
 #ifdef CFM_GEMM_DIAG
   // DIAG (timing experiments only, diagnostic builds, model option "gemm_diag"): 1 = no MFMAs,

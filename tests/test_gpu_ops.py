@@ -127,3 +127,20 @@ def test_gemm_qkv_and_glu(L, mode, M):
     r = _ref(A, W1, b1)
     _close(out[7:], r[:, :d] * torch.sigmoid(r[:, d:]), tol)
 
+
+
+def test_gemm_output_past_2gib(L):
+    """K = 512 weight-stationary kernel with a > 2 GiB output (a 980-minute batch's FFN hidden):
+    sampled rows against torch, including the last tile."""
+    M, N, K = 540_037, 2048, 512
+    g = torch.Generator(device="cuda").manual_seed(11)
+    A = (torch.randn(M, K, device="cuda", generator=g) * 0.5).to(torch.bfloat16)
+    W = (torch.randn(N, K, device="cuda", generator=g) / K ** 0.5).to(torch.bfloat16)
+    bias = torch.randn(N, device="cuda", generator=g)
+    out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    assert out.numel() * 2 > 2 ** 31
+    _run(L, L.DTYPE_BF16, 0, 2, A, W, bias, out=out, ldo=N)
+    rows = torch.cat([torch.arange(0, 64), torch.randint(0, M, (2000,), generator=torch.Generator().manual_seed(1)),
+                      torch.arange(M - 100, M)]).cuda()
+    r = torch.nn.functional.silu(_ref(A[rows], W, bias))
+    _close(out[rows], r, 1e-2)
