@@ -167,7 +167,10 @@ def main():
                          "configs[3] (16 h endless_decode, graph-replayed segments); full = configs[4] (full "
                          "attention, B=256)")
     ap.add_argument("--hours", type=float, default=16.0, help="endless: audio hours")
-    ap.add_argument("--tbd", type=int, default=1800, help="endless: total_batch_duration (s)")
+    ap.add_argument("--tbd", type=int, default=7200,
+                    help="endless: total_batch_duration (s); a memory budget that does not change results "
+                         "(tests/test_gpu_model.py): 7200 s segments fill one MI355X better than the "
+                         "reference's 1800 s default (DESIGN.md §8)")
     ap.add_argument("--batch", type=int, default=256, help="full: utterances of T=3000 frames")
     ap.add_argument("--opt", action="append", default=[], metavar="KEY=VALUE",
                     help="per-model kernel option (cfm_model_set_option), A/B runs only")
@@ -403,6 +406,13 @@ def bench_single(args):
     enc.set_option("profile", 0)
     ms1, n1 = _lib.profile_read(enc._h)[roof_cls]
     avg_s = ms1 / max(n1, 1) / 1e3
+    # per-class breakdown of one eager call (endless: one full segment)
+    enc.set_option("profile_reset", 1)
+    enc.set_option("profile", (1 << len(_lib.PROFILE_CLASSES)) - 1)
+    prof_call()
+    torch.cuda.synchronize()
+    enc.set_option("profile", 0)
+    breakdown = {k: round(v[0], 3) for k, v in _lib.profile_read(enc._h).items() if v[1]}
     peak = PEAK_TFLOPS[args.dtype]
     if roof_cls == "ffn_w1_gemm":
         fl_launch = 2.0 * rows * ff_ * d_
@@ -422,6 +432,7 @@ def bench_single(args):
                      "peak": peak, "unit": "TFLOP/s", "frac": round(achieved / peak, 4) if achieved else None,
                      "traffic": None, "flops_per_launch": fl_launch, "avg_launch_ms": round(avg_s * 1e3, 4),
                      "launches": n1},
+        "breakdown_ms_one_call": breakdown,
     }
     print(json.dumps(res), flush=True)
 

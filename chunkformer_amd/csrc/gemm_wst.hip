@@ -472,7 +472,11 @@ int gemm_bf16_wst(int epi, int act, const bf16* A, int lda, const bf16* W, int l
                   const EpiArgs& ep, hipStream_t st) {
   if (K != WST_K || N % 256 || lda % 8 || ldw % 8 || M <= 0) return -1;
   // enough rows for every CU of an XCD's column tiles to own several tiles
-  if ((M + WST_MT - 1) / WST_MT < 8 * 32 * 2) return -1;
+  // enough row tiles for every CU of an XCD's column tiles to own some: 512 for the GLU epilogue,
+  // 128 otherwise (measured at endless_decode's 12.7k-row segments: FFN w1 45 -> 41 us, QKV 36 ->
+  // 30 us; GLU 20 -> 24 us, so it keeps the 256 x 256 kernel there); ep.wst == 2: any M (A/B)
+  const int min_tiles = epi == EPI_GLU ? 512 : 128;
+  if (ep.wst < 2 && (M + WST_MT - 1) / WST_MT < min_tiles) return -1;
   if (N / 256 > 32) return -1;
   switch (epi) {
     case EPI_STORE:

@@ -355,8 +355,22 @@ def gen_stream(path):
     np.savez_compressed(path, **out)
 
 
+def gen_endless_tbd(path, cfg=SMALL, seed=1):
+    """The small endless input of small.npz decoded again with total_batch_duration 80 (2 segments
+    instead of 7): the reference's output depends (slightly) on the segmentation, so the bench's
+    larger segments are pinned at their own tbd."""
+    enc, ctc, sd = build_reference(cfg, seed)
+    x = feats([6000], 11)[0]
+    with torch.no_grad():
+        eo, ids, ac, cc, nseg = endless_reference(enc, ctc, x, 16, 32, 32, tbd=80)
+    np.savez_compressed(path, sd_digest=sd_digest(sd), seed=np.array(seed), feat_seed=np.array(11),
+                        clrt=np.array([16, 32, 32, 80], np.int32), nseg=np.array(nseg), out=eo.numpy(),
+                        ids=ids.numpy().astype(np.int32), att=ac.numpy(), cnn=cc.numpy())
+
+
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["masks", "small", "large", "large_4h", "large_endless", "large_full", "text", "stream"]
+    which = sys.argv[1:] or ["masks", "small", "large", "large_4h", "large_endless", "large_full", "text", "stream",
+                             "endless_tbd"]
     if "masks" in which:
         gen_masks(os.path.join(HERE, "masks.npz"))
     if "small" in which:
@@ -373,4 +387,6 @@ if __name__ == "__main__":
         gen_large_full(os.path.join(HERE, "large_full.npz"))
     if "stream" in which:
         gen_stream(os.path.join(HERE, "stream.npz"))
+    if "endless_tbd" in which:
+        gen_endless_tbd(os.path.join(HERE, "endless_tbd80.npz"))
     print("ok", which)

@@ -31,7 +31,8 @@ def main():
     ap.add_argument("--diag", type=int, default=0, help="timing diagnostic of the bf16 kernels (cfm_ops.h)")
     ap.add_argument("--only", default="")
     ap.add_argument("--store", type=int, default=0, help="epilogue store policy (EpiArgs::store_mode: 2 = nt)")
-    ap.add_argument("--wst", type=int, default=0, help="K = 512 weight-stationary kernel: 1 on, 3 off")
+    ap.add_argument("--m", type=int, default=0, help="rows (default: the 240-min batch)")
+    ap.add_argument("--wst", type=int, default=0, help="K = 512 weight-stationary kernel: 1 on, 2 on at any M, 3 off")
     a = ap.parse_args()
     st = torch.cuda.current_stream().cuda_stream
     for name, N, K, epi, act in SHAPES:
@@ -39,7 +40,7 @@ def main():
             continue
         if a.diag in (3, 4, 5, 7) and K != 512:   # those diagnostics exist only in the K = 512 kernel
             continue
-        Mr = M if name != "fe_pw1" else 2845 * 2451 // 4
+        Mr = a.m if a.m else (M if name != "fe_pw1" else 2845 * 2451 // 4)
         A = torch.randn(Mr, K, device="cuda").to(torch.bfloat16)
         W = (torch.randn(N, K, device="cuda") / K ** 0.5).to(torch.bfloat16)
         bias = torch.randn(N, device="cuda")
