@@ -419,7 +419,7 @@ def bench_single(args):
         kname = "ffn_w1_gemm (gemm_wsp_kernel<EPI_STORE,SiLU>: K=512 weight-stationary bf16 MFMA)"
     else:
         fl_launch = attn_fl
-        kname = "chunk_attention (chunk_attention_kernel<bf16>, full-attention descriptors)"
+        kname = "chunk_attention (full_attention_bf16_kernel: every key of the utterance staged once per block)"
     achieved = fl_launch / avg_s / 1e12 if n1 else None
     res = {
         "metric": METRIC, "value": round(value, 1), "unit": "audio-frames/s", "n_gpus": 1, "steps": args.steps,

@@ -602,4 +602,277 @@ int chunk_attention_masked_bf16(const bf16* q, const bf16* kv, int kv_rows, cons
   return 0;
 }
 
+
+// =====================================================================================
+// Dense path (bf16, dk 64, full attention: forward_encoder with chunk_size -1, BASELINE configs[4];
+// any padded plan without left context): one 512-thread block = two consecutive 64-query
+// descriptors of one utterance x one head (8 waves, two per SIMD), with every key of the
+// utterance (T' <= 384) staged ONCE in LDS for all 8 waves instead of each wave reloading K and P
+// fragments from global memory per 64-key tile (chunk_attention_kernel):
+//   phase 1: K rows (swizzled) and the 64 NT + 127 relative-position rows the block's queries reach;
+//            V rows are loaded into registers at the same time;
+//   scores:  the ring kernel's compute -- S^T = K.(q+u)^T, band^T = P.(q+v)^T skewed through a bf16
+//            scratch (pitch 49 write, 48 read), exact softmax with all <= 384 scores of a query in
+//            registers;
+//   phase 2: V^T is written over the dead K region, then O^T = V^T.P^T with the score registers as
+//            the B operand.
+// LDS: max(K 48 KiB, V^T 49 KiB) + P 64 KiB + 8 skew scratches = 126 KiB.
+// =====================================================================================
+namespace {
+constexpr int FA_KEYS = 384;                        // keys staged (T' <= 384: utterances <= 30.8 s)
+constexpr int FA_NT = FA_KEYS / 64;                 // key tiles
+constexpr int FA_PROWS = 64 * FA_NT + 128;          // P rows staged (64 NT + 127, rounded)
+constexpr int FA_K_BYTES = FA_KEYS * 128;
+constexpr int FA_VT_PITCH = (FA_KEYS + 8) * 2;
+constexpr int FA_VT_BYTES = 64 * FA_VT_PITCH;
+constexpr int FA_KV_BYTES = FA_VT_BYTES > FA_K_BYTES ? FA_VT_BYTES : FA_K_BYTES;
+constexpr int FA_P_BYTES = FA_PROWS * 128;
+constexpr int FA_LDS = FA_KV_BYTES + FA_P_BYTES + 8 * SCR_BYTES + 512;
+static_assert(FA_LDS <= 163840, "full-attention LDS");
+}  // namespace
+
+__global__ __launch_bounds__(512, 1) void full_attention_bf16_kernel(
+    const bf16* __restrict__ Q, const bf16* __restrict__ KV, int kv_rows, const bf16* __restrict__ P, int p_rows,
+    const float* __restrict__ pos_u, const float* __restrict__ pos_v, const int32_t* __restrict__ desc, int H,
+    int nd, bf16* __restrict__ out, int p_ld) {
+  __shared__ __attribute__((aligned(16))) char smem[FA_LDS];
+  char* kr = smem;   // K in phase 1, V^T in phase 2
+  char* vt = smem;
+  char* pl = smem + FA_KV_BYTES;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int fr = lane & 15, g = lane >> 4;
+  const int half = __builtin_amdgcn_readfirstlane(w) >> 2, wq = w & 3;
+  bf16* scr = reinterpret_cast<bf16*>(pl + FA_P_BYTES + w * SCR_BYTES);
+  const unsigned scr_base = (unsigned)(size_t)(__attribute__((address_space(3))) char*)scr;
+  float* uv = reinterpret_cast<float*>(pl + FA_P_BYTES + 8 * SCR_BYTES);
+  const int h = blockIdx.y, d = H * 64;
+  const int npair = (nd + 1) >> 1, u = blockIdx.x / npair, pr2 = blockIdx.x % npair;
+  const int dix = u * nd + 2 * pr2 + half;
+  const bool has = 2 * pr2 + half < nd;
+  const int32_t* D0 = desc + (size_t)(u * nd + 2 * pr2) * AD_INTS;
+  const int32_t* D = desc + (size_t)(has ? dix : u * nd + 2 * pr2) * AD_INTS;
+  const int kv_row0 = D0[AD_KV_ROW0], key_hi = D0[AD_KEY_HI];   // shared by the pair (one utterance)
+  const int q_row0 = D[AD_Q_ROW0], nq = D[AD_NQ], p_base = D[AD_P_BASE], q_valid = D[AD_Q_VALID];
+  const int pb0 = D0[AD_P_BASE] - 127;   // P row of LDS row 0
+
+  if (tid < 128) uv[tid] = (tid < 64 ? pos_u : pos_v)[h * 64 + (tid & 63)];
+  // ---- phase 1: issue every global load of the thread (K, P, and V for phase 2), then the stores
+  constexpr int KIT = FA_KEYS * 8 / 512, PIT = FA_PROWS * 8 / 512, VIT = (FA_KEYS / 2) * 8 / 512;
+  static_assert(FA_KEYS * 8 % 512 == 0 && FA_PROWS * 8 % 512 == 0 && (FA_KEYS / 2) * 8 % 512 == 0, "staging");
+  u32x4 sk[KIT], sp[PIT], sv0[VIT], sv1[VIT];
+  const u32x4 z4 = (u32x4){0u, 0u, 0u, 0u};
+#pragma unroll
+  for (int it = 0; it < VIT; ++it) {   // V rows: two keys x one 16-B chunk (zero past key_hi: p = 0 x finite)
+    const int idx = tid + 512 * it, pr = idx % (FA_KEYS / 2), ch = idx / (FA_KEYS / 2), j = 2 * pr;
+    sv0[it] = j < key_hi ? *reinterpret_cast<const u32x4*>(KV + (size_t)min(kv_row0 + j, kv_rows - 1) * (2 * d) +
+                                                            h * 128 + 64 + ch * 8)
+                         : z4;
+    sv1[it] = j + 1 < key_hi ? *reinterpret_cast<const u32x4*>(KV + (size_t)min(kv_row0 + j + 1, kv_rows - 1) * (2 * d) +
+                                                                h * 128 + 64 + ch * 8)
+                             : z4;
+  }
+#pragma unroll
+  for (int it = 0; it < KIT; ++it) {   // K rows: one 16-B chunk (8 lanes per row: conflict-free stores)
+    const int idx = tid + 512 * it, j = idx >> 3, ch = idx & 7;
+    sk[it] = j < key_hi ? *reinterpret_cast<const u32x4*>(KV + (size_t)min(kv_row0 + j, kv_rows - 1) * (2 * d) +
+                                                           h * 128 + ch * 8)
+                        : z4;
+  }
+#pragma unroll
+  for (int it = 0; it < PIT; ++it) {   // P rows pb0 .. (zero outside [0, p_rows): they reach masked scores only)
+    const int idx = tid + 512 * it, r = idx >> 3, ch = idx & 7, prow = pb0 + r;
+    sp[it] = prow >= 0 && prow < p_rows ? *reinterpret_cast<const u32x4*>(P + (size_t)prow * p_ld + h * 64 + ch * 8)
+                                        : z4;
+  }
+#pragma unroll
+  for (int it = 0; it < KIT; ++it) {
+    const int idx = tid + 512 * it;
+    *reinterpret_cast<u32x4*>(kr + sw128(idx >> 3, idx & 7)) = sk[it];
+  }
+#pragma unroll
+  for (int it = 0; it < PIT; ++it) {
+    const int idx = tid + 512 * it;
+    *reinterpret_cast<u32x4*>(pl + sw128(idx >> 3, idx & 7)) = sp[it];
+  }
+  __syncthreads();
+
+  const int i0 = wq * 16;
+  const bool active = has && i0 < nq;
+  f32x4 S[FA_NT][4];
+  float l = 0.f;
+  const int key8 = (fr >> 1) & 7;
+  const int frag_lane[2] = {fr * 128 + ((g ^ key8) << 4), fr * 128 + (((4 + g) ^ key8) << 4)};
+  if (active) {
+    bf16x8 qraw[2];
+    {
+      const bf16* qp = Q + ((size_t)q_row0 + min(i0 + fr, nq - 1)) * d + h * 64;
+      qraw[0] = *reinterpret_cast<const bf16x8*>(qp + 8 * g);
+      qraw[1] = *reinterpret_cast<const bf16x8*>(qp + 32 + 8 * g);
+    }
+    bf16x8 qu[2], qv[2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const f32x4 u0 = *reinterpret_cast<const f32x4*>(uv + s * 32 + 8 * g);
+      const f32x4 u1 = *reinterpret_cast<const f32x4*>(uv + s * 32 + 8 * g + 4);
+      const f32x4 v0_ = *reinterpret_cast<const f32x4*>(uv + 64 + s * 32 + 8 * g);
+      const f32x4 v1_ = *reinterpret_cast<const f32x4*>(uv + 64 + s * 32 + 8 * g + 4);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float qf = (float)qraw[s][e];   // 1/sqrt(64) = 2^-3 folded in: exact in bf16 and f32
+        qu[s][e] = (bf16)((qf + (e < 4 ? u0[e] : u1[e - 4])) * 0.125f);
+        qv[s][e] = (bf16)((qf + (e < 4 ? v0_[e] : v1_[e - 4])) * 0.125f);
+      }
+    }
+    f32x4 band_next = (f32x4){0.f, 0.f, 0.f, 0.f};
+    float mx = -INFINITY;
+    // band rows kb0 = p_base - i0 - 15 + j0 .. +79 -> LDS row kb0 - pb0
+    const int lbase = p_base - i0 - 15 - pb0;
+#pragma unroll
+    for (int t = 0; t < FA_NT; ++t) {
+      const int j0 = 64 * t;
+      if (j0 >= key_hi) {
+#pragma unroll
+        for (int st = 0; st < 4; ++st) S[t][st] = (f32x4){-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+        continue;
+      }
+#pragma unroll
+      for (int st = 0; st < 4; ++st) {
+        f32x4 a = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+          a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+              *reinterpret_cast<const bf16x8*>(kr + (j0 + 16 * st) * 128 + frag_lane[s]), qu[s], a, 0, 0, 0);
+        S[t][st] = a;
+      }
+      f32x4 band[5];
+#pragma unroll
+      for (int pt = 0; pt < 5; ++pt) {
+        if (pt == 0 && t > 0) {   // subtile 0 of this tile is subtile 4 of the previous one
+          band[0] = band_next;
+          continue;
+        }
+        f32x4 a = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+          a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+              *reinterpret_cast<const bf16x8*>(pl + (lbase + j0 + 16 * pt) * 128 + frag_lane[s]), qv[s], a, 0, 0, 0);
+        band[pt] = a;
+      }
+      band_next = band[4];
+      const bool tmask = j0 + 64 > key_hi;   // the last tile of a short utterance
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+#pragma unroll
+        for (int pt = 0; pt < 3; ++pt) {
+          const f32x4 a = band[2 * hh + pt];
+          const unsigned waddr = scr_base + 2u * (unsigned)(fr * SCR_PITCH + 1 + 16 * pt + 4 * g);
+          const unsigned lo = pack_bf16x2_a(a[0], a[1]), hi = pack_bf16x2_a(a[2], a[3]);
+          asm volatile("ds_write_b64 %0, %1" ::"v"(waddr), "v"((u32x2_a){lo, hi}) : "memory");
+        }
+        typedef bf16 bf16x4 __attribute__((ext_vector_type(4)));
+        bf16x4 bdv4[2];
+#pragma unroll
+        for (int st2 = 0; st2 < 2; ++st2)
+          asm volatile("ds_read_b64 %0, %1"
+                       : "=v"(bdv4[st2])
+                       : "v"(scr_base + 2u * (unsigned)(fr * (SCR_PITCH - 1) + 16 + 16 * st2 + 4 * g))
+                       : "memory");
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(bdv4[0]), "+v"(bdv4[1])::"memory");
+#pragma unroll
+        for (int st2 = 0; st2 < 2; ++st2) {
+          const int st = 2 * hh + st2;
+#pragma unroll
+          for (int rr = 0; rr < 4; ++rr) {
+            float sv = S[t][st][rr] + (float)bdv4[st2][rr];
+            if (tmask && j0 + 32 * hh + 16 * st2 + 4 * g + rr >= key_hi) sv = -INFINITY;
+            S[t][st][rr] = sv;
+            mx = fmaxf(mx, sv);
+          }
+        }
+      }
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    if (mx == -INFINITY) mx = 0.f;   // no valid key: every p = 0, output 0
+    const float mxl = mx * 1.4426950408889634f;
+#pragma unroll
+    for (int t = 0; t < FA_NT; ++t)
+#pragma unroll
+      for (int st = 0; st < 4; ++st)
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+          const float p = __builtin_amdgcn_exp2f(fmaf(S[t][st][rr], 1.4426950408889634f, -mxl));
+          S[t][st][rr] = p;
+          l += p;
+        }
+    l += __shfl_xor(l, 16, 64);
+    l += __shfl_xor(l, 32, 64);
+  }
+  // ---- phase 2: V^T over the K region (every wave is past its K reads)
+  __syncthreads();
+  typedef bf16 bf16x2_ __attribute__((ext_vector_type(2)));
+#pragma unroll
+  for (int it = 0; it < VIT; ++it) {
+    const int idx = tid + 512 * it, pr = idx % (FA_KEYS / 2), ch = idx / (FA_KEYS / 2), j = 2 * pr;
+    const bf16x8 a = __builtin_bit_cast(bf16x8, sv0[it]), b = __builtin_bit_cast(bf16x8, sv1[it]);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) *reinterpret_cast<bf16x2_*>(vt + (ch * 8 + e) * FA_VT_PITCH + j * 2) = (bf16x2_){a[e], b[e]};
+  }
+  __syncthreads();
+  if (!active) return;
+  const int vt_lane = fr * FA_VT_PITCH + 8 * g;
+  f32x4 O[4];
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt) O[nt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int t = 0; t < FA_NT; ++t) {
+    const int j0 = 64 * t;
+    if (j0 >= key_hi) continue;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      bf16x8 pb;
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        pb[rr] = (bf16)S[t][2 * s][rr];
+        pb[4 + rr] = (bf16)S[t][2 * s + 1][rr];
+      }
+      const char* va_ = vt + vt_lane + (j0 + 32 * s) * 2;
+      const char* vb_ = vt + vt_lane + (j0 + 32 * s + 16) * 2;
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        typedef bf16 bf16x4 __attribute__((ext_vector_type(4)));
+        const bf16x4 lo = *reinterpret_cast<const bf16x4*>(va_ + 16 * nt * FA_VT_PITCH);
+        const bf16x4 hi = *reinterpret_cast<const bf16x4*>(vb_ + 16 * nt * FA_VT_PITCH);
+        const bf16x8 va = (bf16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        O[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va, pb, O[nt], 0, 0, 0);
+      }
+    }
+  }
+  const int qi = i0 + fr;
+  if (qi >= nq) return;
+  const bool live = qi < q_valid && l > 0.f;
+  const float inv = live ? 1.f / l : 0.f;
+  bf16* op = out + ((size_t)q_row0 + qi) * d + h * 64;
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt) {
+    typedef bf16 bf16x4 __attribute__((ext_vector_type(4)));
+    *reinterpret_cast<bf16x4*>(op + 16 * nt + 4 * g) =
+        (bf16x4){(bf16)(O[nt][0] * inv), (bf16)(O[nt][1] * inv), (bf16)(O[nt][2] * inv), (bf16)(O[nt][3] * inv)};
+  }
+}
+
+// -1 when not eligible (T' > 384, dk != 64): the caller uses chunk_attention_kernel.  `nd` = the
+// plan's 64-query descriptors per utterance (consecutive), `nutt` utterances.
+int full_attention_bf16(const bf16* q, const bf16* kv, int kv_rows, const bf16* P, int p_rows, const float* pos_u,
+                        const float* pos_v, const int32_t* desc, int nutt, int nd, int H, int dk, int t_keys,
+                        bf16* out, hipStream_t st, int p_ld) {
+  if (nutt <= 0 || nd <= 0) return 0;
+  if (dk != 64 || t_keys > FA_KEYS || t_keys <= 0) return -1;
+  if (p_ld <= 0) p_ld = H * 64;
+  hipLaunchKernelGGL(full_attention_bf16_kernel, dim3(nutt * ((nd + 1) / 2), H), dim3(512), 0, st, q, kv, kv_rows, P,
+                     p_rows, pos_u, pos_v, desc, H, nd, out, p_ld);
+  CFM_CHECK_LAUNCH();
+  return 0;
+}
+
 }  // namespace cfm

@@ -90,6 +90,11 @@ int chunk_attention(const T* q, const T* kv, int kv_rows, const T* P, int p_rows
 CFM_HD_INLINE int qkv_kv_col(int cc, int which, int dk) { return (cc / dk) * 2 * dk + which * dk + (cc & (dk - 1)); }
 
 // masked-batch ring kernel (bf16, head dim 64); -1 = shape not eligible
+// full attention (padded plan with chunk_size <= 0), bf16, dk 64, T' <= 384: every key of the utterance
+// staged once per block; -1 when not eligible (attention.hip)
+int full_attention_bf16(const bf16* q, const bf16* kv, int kv_rows, const bf16* P, int p_rows, const float* pos_u,
+                        const float* pos_v, const int32_t* desc, int nutt, int nd, int H, int dk, int t_keys,
+                        bf16* out, hipStream_t st, int p_ld);
 int chunk_attention_masked_bf16(const bf16* q, const bf16* kv, int kv_rows, const bf16* P, int p_rows,
                                 const float* pos_u, const float* pos_v, const int32_t* desc, int n_chunks, int H,
                                 int C, int W, bf16* out, hipStream_t st, int diag = 0, int p_ld = 0, int reuse = 1);

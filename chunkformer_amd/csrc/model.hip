@@ -340,6 +340,11 @@ struct ModelT : public cfm_model {
             r = chunk_attention_masked_bf16(w.q, w.kv, kv_rows, w.P + (size_t)l * d, p_rows, Lw.pu, Lw.pv,
                                             attd, natt, H, C, hh[PH_L] + C + hh[PH_R], w.ao, st, attn_diag, p_ld,
                                             tune.attn_reuse);
+          // full attention (padded plan, one chunk of T' per utterance: key window [0, T')) -> dense kernel
+          else if (!masked && !stream && hh[PH_L] == 0 && hh[PH_R] == 0 && hh[PH_C] == hh[PH_TOUT] &&
+                   use_ring_attention && natt == hh[PH_NWIN] * ((hh[PH_TOUT] + 63) / 64))
+            r = full_attention_bf16(w.q, w.kv, kv_rows, w.P + (size_t)l * d, p_rows, Lw.pu, Lw.pv, attd, hh[PH_NWIN],
+                                    (hh[PH_TOUT] + 63) / 64, H, dk, hh[PH_TOUT], w.ao, st, p_ld);
         }
         if (r == -1)
           r = chunk_attention<T>(w.q, w.kv, kv_rows, w.P + (size_t)l * d, p_rows, Lw.pu, Lw.pv, attd, natt,

@@ -177,3 +177,27 @@ def test_ring_attention_matches_generic(cfm, small_models, small_g, case):
     enc.set_option("ring_attention", 1)
     assert _rel_l2(outs[0], outs[1]) <= 1e-2
     assert _rel_l2(outs[0], g[f"{case}_out"]) <= BF16_RELL2
+
+
+@pytest.mark.parametrize("clr", [(-1, -1, -1), (16, 0, 16), (64, 0, 0), (0, 0, 0)])
+def test_dense_attention_matches_generic(cfm, small_models, clr):
+    """bf16 padded plans without left context (full attention, or chunks with right context only):
+    the dense kernel (every key staged once per block) against the generic per-block kernel, on
+    utterances padded to different lengths (key padding masks, a masked partial last tile)."""
+    from chunkformer_amd.weights import synthetic_features
+    enc = small_models["bf16"]
+    lens = [3000, 1790, 523, 40]
+    xs = synthetic_features(lens, 77)
+    T = max(lens)
+    xp = torch.zeros(len(lens), T, 80)
+    for i, t in enumerate(xs):
+        xp[i, : t.shape[0]] = t
+    outs = []
+    for ring in (1, 0):
+        enc.set_option("ring_attention", ring)
+        y, _ = enc.forward_encoder(xp, torch.tensor(lens, dtype=torch.int32), *clr)
+        outs.append(y.float().cpu().numpy())
+    enc.set_option("ring_attention", 1)
+    for b, t in enumerate(lens):
+        n = (t - 15) // 8 + 1
+        assert _rel_l2(outs[0][b, :n], outs[1][b, :n]) <= 1e-2, b
