@@ -768,7 +768,7 @@ cfm_status cfm_op_gemm(int32_t dtype, int32_t epi, int32_t act, const void* A, i
   e.bias = bias; e.alpha = alpha; e.out = out; e.out2 = out2; e.ldo = ldo; e.row_off = row_off; e.x = x; e.ldx = ldx;
   e.rowmask = rowmask; e.d = d; e.small_tiles = variant & 1; e.diag = (variant >> 8) & 0xff;
   e.store_mode = (variant >> 16) & 3;
-  if ((variant >> 18) & 3) e.wst = ((variant >> 18) & 3) == 3 ? 0 : (variant >> 18) & 3;
+  if ((variant >> 18) & 7) e.wst = ((variant >> 18) & 7) == 7 ? 0 : (variant >> 18) & 7;
   int r;
   if (dtype == CFM_DTYPE_F32)
     r = gemm<float>(epi, act, (const float*)A, lda, (const float*)W, ldw, M, N, K, e, (hipStream_t)stream);

@@ -26,8 +26,8 @@ typedef enum { CFM_ACT_NONE = 0, CFM_ACT_RELU = 1, CFM_ACT_SILU = 2 } cfm_act;
  *   GLU:       W rows interleaved [a16 | gate16]: out_T[(m+row_off)*ldo + ch] = a*sigmoid(gate)
  * variant (A/B testing): bit 0 forces the 128x128 kernel; bits 8-15 select a timing diagnostic of
  * the bf16 kernels (1 no MFMA, 2 no DMA in the loop, 3 no epilogue, 5 no stores; 0 = normal; only
- * in a library built with -DCFM_GEMM_DIAG); bits 16-17 the bf16 store policy (2 = nt); bits 18-19 the
- * K = 512 weight-stationary kernel (0 = model default, 1 = on, 2 = on at any M, 3 = off). */
+ * in a library built with -DCFM_GEMM_DIAG); bits 16-17 the bf16 store policy (2 = nt); bits 18-20 the
+ * K = 512 weight-stationary kernel (0 = model default, 1 = on, 2 = on at any M, 7 = off). */
 cfm_status cfm_op_gemm(int32_t dtype, int32_t epi, int32_t act, const void* A, int32_t lda, const void* W, int32_t ldw,
                        int32_t M, int32_t N, int32_t K, const float* bias, float alpha, void* out, int32_t ldo,
                        int32_t row_off, void* out2, int32_t d, float* x, int32_t ldx, const uint8_t* rowmask,

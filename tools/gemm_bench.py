@@ -32,7 +32,7 @@ def main():
     ap.add_argument("--only", default="")
     ap.add_argument("--store", type=int, default=0, help="epilogue store policy (EpiArgs::store_mode: 2 = nt)")
     ap.add_argument("--m", type=int, default=0, help="rows (default: the 240-min batch)")
-    ap.add_argument("--wst", type=int, default=0, help="K = 512 weight-stationary kernel: 1 on, 2 on at any M, 3 off")
+    ap.add_argument("--wst", type=int, default=0, help="K = 512 weight-stationary kernel: 1 on, 2 on at any M, 7 off")
     a = ap.parse_args()
     st = torch.cuda.current_stream().cuda_stream
     for name, N, K, epi, act in SHAPES:
