@@ -52,6 +52,8 @@ from chunkformer_amd.weights import synthetic_state_dict  # noqa: E402
 
 METRIC = "audio-frames/sec (80-dim fbank) through encoder, chunkformer-large chunk=64, 1/2/4/8 GPU"
 PEAK_TFLOPS = {"bf16": 2500.0, "fp32": 157.3}   # MI355X dense MFMA peaks (MI355X_MICROARCH.md)
+MEASURED_BF16_CEILING = 1833.8   # TFLOP/s, tools/mfma_peak.hip on this pool
+HIPBLASLT_W1 = 706.8             # TFLOP/s, hipBLASLt M=182080 N=2048 K=512 bf16
 C, L, R = 64, 128, 128
 
 
@@ -325,7 +327,14 @@ def main():
                          "traffic_unit": "HBM bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)",
                          "traffic_source": traffic_src,
                          "algorithmic_bytes_per_launch": alg_bytes,
-                         "flops_per_launch": fl_launch, "avg_launch_ms": round(avg_s * 1e3, 4), "launches": n1},
+                         "flops_per_launch": fl_launch, "avg_launch_ms": round(avg_s * 1e3, 4), "launches": n1,
+                         # context, not the contract's peak: the bf16 MFMA rate this chip sustains on random
+                         # operands (tools/mfma_peak.hip, 2 waves/SIMD, in-kernel clock 1.83 GHz) and the
+                         # vendor GEMM on the same shape without bias/activation (tools/torch_gemm_ref.py)
+                         "measured_mfma_ceiling": MEASURED_BF16_CEILING if args.dtype == "bf16" else None,
+                         "frac_of_measured_ceiling": (round(achieved / MEASURED_BF16_CEILING, 4)
+                                                      if achieved and args.dtype == "bf16" else None),
+                         "hipblaslt_same_shape_tflops": HIPBLASLT_W1 if args.dtype == "bf16" else None},
             "step_tflops_algorithmic": round(step_flops / (dt_max / args.steps) / 1e12, 1),
             "ctc_ms": round(ctc_ms, 3),
             "allgather_ids_ms": round(gather_ms, 3) if gather_ms is not None else None,
