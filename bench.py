@@ -255,7 +255,10 @@ def main():
     avg_s = (ms1 / max(n1, 1)) / 1e3
     achieved = fl_launch / avg_s / 1e12 if n1 else None
     peak = PEAK_TFLOPS[args.dtype]
-    traffic, traffic_src = committed_traffic(roof_cls) if args.dtype == "bf16" else (None, None)
+    # the committed PMC traffic was collected on the default workload (configs[1], 2,845 chunks on one
+    # GPU); other row counts report null rather than a number measured on a different launch size
+    profiled = args.dtype == "bf16" and not sharded and world == 1 and n_chunks == 2845
+    traffic, traffic_src = committed_traffic(roof_cls) if profiled else (None, None)
     step_flops = n_chunks * flops_per_chunk(LARGE) + LARGE.num_blocks * 2 * (L + 2 * C + R - 1) * LARGE.d_model ** 2
 
     # ---- CTC head + the collectives (timed separately; not part of `value`)
