@@ -494,7 +494,7 @@ def bench_fbank(args):
         "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic (N(0, 3000^2) int16-scale samples)",
         "config": {"workload": f"kaldi.fbank over one {args.hours:g} h waveform ({n} samples, {frames} frames)",
                    "parallelism": "single GPU"},
-        "roofline": {"bound": "hbm", "kernel": "fbank_kernel<8> (LDS radix-2 FFT, 16 frames per block)",
+        "roofline": {"bound": "hbm", "kernel": "fbank_kernel<8> (persistent blocks, 16 frames per group, four-step 16x16 FFT in registers)",
                      "achieved": round(nbytes / kern_s / 1e9, 1), "peak": 8000.0, "unit": "GB/s",
                      "frac": round(nbytes / kern_s / 1e9 / 8000.0, 4), "traffic": None,
                      "algorithmic_bytes_per_launch": nbytes, "avg_launch_ms": round(kern_s * 1e3, 3)},

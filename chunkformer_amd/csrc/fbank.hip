@@ -12,10 +12,12 @@
 // Layout and kernel: the waveform is a flat f32 device array (int16 scale, as the reference feeds
 // pydub samples); one 256-thread block takes FB = 16 consecutive frames, stages their samples once
 // in LDS (frames overlap: 15 * shift + win samples), 16 threads per frame.  The N-point real FFT
-// runs as an N/2-point complex radix-2 FFT of z[n] = y[2n] + i y[2n+1] in LDS (input written in
-// bit-reversed order) plus the real-split post-pass; mel filters are sparse ranges (each FFT bin
-// feeds at most two filters).  Bytes per frame: 4 * shift in (the overlap is re-read from LDS, not
+// runs as an N/2-point complex FFT of z[n] = y[2n] + i y[2n+1] plus the real-split post-pass: for
+// N = 512 (the reference's 25 ms at 16 kHz) a four-step 16 x 16 FFT, two 16-point DFTs in
+// registers around one LDS transpose; other sizes a radix-2 FFT in LDS (input written in
+// bit-reversed order).  Mel filters are sparse ranges (each FFT bin feeds at most two filters).  Bytes per frame: 4 * shift in (the overlap is re-read from LDS, not
 // HBM) + 4 * bins out = 960 B at 16 kHz / 80 bins: the kernel is LDS-bound, far below HBM.
+#include <algorithm>
 #include <cmath>
 #include <cstring>
 #include <string>
@@ -29,8 +31,37 @@ namespace cfm {
 namespace {
 constexpr int FB = 16;    // frames per block
 constexpr int TPF = 16;   // threads per frame
+constexpr int FBK_SAMPLES = 8192;   // samples of one group staged per block (15 shift + win)
 
 CFM_DEV int brev(int v, int bits) { return (int)(__builtin_bitreverse32((unsigned)v) >> (32 - bits)); }
+CFM_DEV float2 cmul(float2 a, float2 w) { return make_float2(a.x * w.x - a.y * w.y, a.x * w.y + a.y * w.x); }
+
+// in-register 16-point DFT, a[k] = sum_m a[m] e^{-2 pi i m k / 16} (radix-2 DIT, natural-order output)
+CFM_DEV void fft16(float2 (&a)[16]) {
+  constexpr int br[16] = {0, 8, 4, 12, 2, 10, 6, 14, 1, 9, 5, 13, 3, 11, 7, 15};
+  constexpr float C[8] = {1.f, 0.92387953251128674f, 0.70710678118654752f, 0.38268343236508977f,
+                          0.f, -0.38268343236508977f, -0.70710678118654752f, -0.92387953251128674f};
+  constexpr float S[8] = {0.f, 0.38268343236508977f, 0.70710678118654752f, 0.92387953251128674f,
+                          1.f, 0.92387953251128674f, 0.70710678118654752f, 0.38268343236508977f};
+  float2 b[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) b[i] = a[br[i]];
+#pragma unroll
+  for (int st = 1; st <= 4; ++st) {
+    const int half = 1 << (st - 1);
+#pragma unroll
+    for (int i0 = 0; i0 < 16; ++i0) {
+      const int k = i0 & (2 * half - 1);
+      if (k >= half) continue;
+      const int i1 = i0 + half, e = k << (4 - st);   // W_{2 half}^k = W16^(k 16 / 2 half)
+      const float2 t = cmul(b[i1], make_float2(C[e], -S[e]));
+      b[i1] = make_float2(b[i0].x - t.x, b[i0].y - t.y);
+      b[i0] = make_float2(b[i0].x + t.x, b[i0].y + t.y);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 16; ++i) a[i] = b[i];
+}
 }  // namespace
 
 template <int LOGM>
@@ -54,89 +85,136 @@ __global__ __launch_bounds__(256) void fbank_kernel(const float* __restrict__ wa
   int* lmi = reinterpret_cast<int*>(lmw + nw);                // [nbins] lo, [nbins + 1] offsets
   float* sx = reinterpret_cast<float*>(lmi + 2 * nbins + 1);  // block's samples
   const int tid = threadIdx.x, f = tid / TPF, j = tid % TPF;
-  const long long F0 = (long long)blockIdx.x * FB;
-  const long long base = F0 * shift;
-  const int nload = (int)min((long long)(FB - 1) * shift + win, n_samples - base);
-  for (int i = tid; i < nload; i += 256) sx[i] = wave[base + i];
-  // constants in LDS: every stage and filter reads them at LDS latency, not L2's
+  // constants in LDS once per (persistent) block: every stage and filter reads them at LDS latency
   for (int i = tid; i < M / 2; i += 256) ltw[i] = tw[i];
   for (int i = tid; i <= M / 2; i += 256) ltw2[i] = tw2[i];
   for (int i = tid; i < win; i += 256) lwin[i] = window[i];
   for (int i = tid; i < nw; i += 256) lmw[i] = mel_w[i];
   for (int i = tid; i < 2 * nbins + 1; i += 256) lmi[i] = i < nbins ? mel_lo[i] : mel_off[i - nbins];
-  __syncthreads();
-
-  const long long F = F0 + f;
-  const bool live = F < n_frames;
-  const float* x = sx + f * shift;
-  float2* z = cz + f * ZS;
-  // ---- frame mean over the 16 threads of the frame (lanes 16f .. 16f+15 of one wave)
-  float s = 0.f;
-  if (live)
-    for (int n = j; n < win; n += TPF) s += x[n];
+  // samples of a 16-frame group (<= FBK_SAMPLES), prefetched into registers one group ahead
+  const int span = (FB - 1) * shift + win;
+  float pre[FBK_SAMPLES / 256];
+  const long long ngroups = (n_frames + FB - 1) / FB;
+  auto fetch = [&](long long grp) {
+    const long long base = grp * FB * shift;
 #pragma unroll
-  for (int o = TPF / 2; o > 0; o >>= 1) s += __shfl_xor(s, o, TPF);
-  const float mean = remove_dc ? s / (float)win : 0.f;
-  // ---- DC removal, pre-emphasis, window, zero pad; z[n] = y[2n] + i y[2n+1] at bit-reversed n
-  for (int n = j; n < 2 * M; n += TPF) {
-    float y = 0.f;
-    if (live && n < win) {
-      const float cur = x[n] - mean, prev = x[n > 0 ? n - 1 : 0] - mean;
-      y = (cur - preemph * prev) * lwin[n];
+    for (int q = 0; q < FBK_SAMPLES / 256; ++q) {
+      const int i = tid + 256 * q;
+      pre[q] = (grp < ngroups && i < span && base + i < n_samples) ? wave[base + i] : 0.f;
     }
-    float* zp = reinterpret_cast<float*>(&z[brev(n >> 1, LOGM)]);
-    zp[n & 1] = y;
-  }
-  __syncthreads();
-  // ---- radix-2 DIT, M/2 butterflies per stage, 16 threads per frame
+  };
+  fetch(blockIdx.x);
+  for (long long grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {
+    __syncthreads();   // the previous group's reads of sx / cz / pw are done
+#pragma unroll
+    for (int q = 0; q < FBK_SAMPLES / 256; ++q)
+      if (tid + 256 * q < span) sx[tid + 256 * q] = pre[q];
+    __syncthreads();
+    fetch(grp + gridDim.x);
+
+    const long long F = grp * FB + f;
+    const bool live = F < n_frames;
+    const float* x = sx + f * shift;
+    float2* z = cz + f * ZS;
+    // ---- frame mean over the 16 threads of the frame (lanes 16f .. 16f+15 of one wave)
+    float s = 0.f;
+    if (live)
+      for (int n = j; n < win; n += TPF) s += x[n];
+#pragma unroll
+    for (int o = TPF / 2; o > 0; o >>= 1) s += __shfl_xor(s, o, TPF);
+    const float mean = remove_dc ? s / (float)win : 0.f;
+    if constexpr (LOGM == 8) {
+      // ---- four-step 256 = 16 x 16 FFT: thread j takes z[j + 16 m] (m = 0..15), a 16-point DFT in
+      // registers, the W256^(j k1) twiddle, one transpose through LDS, a second 16-point DFT
+      float2 a[16];
+#pragma unroll
+      for (int m = 0; m < 16; ++m) {
+        const int n0 = 2 * (j + 16 * m);
+        float y0 = 0.f, y1 = 0.f;   // DC removal, pre-emphasis (x[-1] = x[0]), window, zero pad
+        if (live && n0 < win) {
+          const float c0 = x[n0] - mean, p0 = x[n0 > 0 ? n0 - 1 : 0] - mean;
+          y0 = (c0 - preemph * p0) * lwin[n0];
+          if (n0 + 1 < win) y1 = ((x[n0 + 1] - mean) - preemph * c0) * lwin[n0 + 1];
+        }
+        a[m] = make_float2(y0, y1);
+      }
+      fft16(a);
+#pragma unroll
+      for (int k1 = 0; k1 < 16; ++k1) {
+        const int e = j * k1;   // < 256: W256^e = -W256^(e - 128) past 128
+        const float2 w = ltw[e & 127];
+        z[16 * k1 + j] = cmul(a[k1], (e & 128) ? make_float2(-w.x, -w.y) : w);
+      }
+      __syncthreads();
+#pragma unroll
+      for (int t = 0; t < 16; ++t) a[t] = z[16 * j + t];
+      fft16(a);   // a[k2] = Z[j + 16 k2]
+      __syncthreads();
+#pragma unroll
+      for (int k2 = 0; k2 < 16; ++k2) z[j + 16 * k2] = a[k2];
+      __syncthreads();
+    } else {
+      // ---- DC removal, pre-emphasis, window, zero pad; z[n] = y[2n] + i y[2n+1] at bit-reversed n
+      for (int n = j; n < 2 * M; n += TPF) {
+        float y = 0.f;
+        if (live && n < win) {
+          const float cur = x[n] - mean, prev = x[n > 0 ? n - 1 : 0] - mean;
+          y = (cur - preemph * prev) * lwin[n];
+        }
+        float* zp = reinterpret_cast<float*>(&z[brev(n >> 1, LOGM)]);
+        zp[n & 1] = y;
+      }
+      __syncthreads();
+      // ---- radix-2 DIT, M/2 butterflies per stage, 16 threads per frame
 #pragma unroll 1
-  for (int st = 1; st <= LOGM; ++st) {
-    const int half = 1 << (st - 1);
-    for (int b = j; b < M / 2; b += TPF) {
-      const int k = b & (half - 1), i0 = ((b >> (st - 1)) << st) + k, i1 = i0 + half;
-      const float2 w = ltw[k << (LOGM - st)];
-      const float2 a = z[i0], c = z[i1];
-      const float2 t = make_float2(w.x * c.x - w.y * c.y, w.x * c.y + w.y * c.x);
-      z[i0] = make_float2(a.x + t.x, a.y + t.y);
-      z[i1] = make_float2(a.x - t.x, a.y - t.y);
+      for (int st = 1; st <= LOGM; ++st) {
+        const int half = 1 << (st - 1);
+        for (int b = j; b < M / 2; b += TPF) {
+          const int k = b & (half - 1), i0 = ((b >> (st - 1)) << st) + k, i1 = i0 + half;
+          const float2 w = ltw[k << (LOGM - st)];
+          const float2 av = z[i0], c = z[i1];
+          const float2 t = make_float2(w.x * c.x - w.y * c.y, w.x * c.y + w.y * c.x);
+          z[i0] = make_float2(av.x + t.x, av.y + t.y);
+          z[i1] = make_float2(av.x - t.x, av.y - t.y);
+        }
+        __syncthreads();
+      }
+    }
+    // ---- real split: X[k] = (Z[k] + conj Z[M-k]) / 2 - i W^k (Z[k] - conj Z[M-k]) / 2, W = e^{-2 pi i / N};
+    // power = |X|^2
+    float* p = pw + f * PS;
+    for (int k = j; k <= M / 2; k += TPF) {
+      const float2 zk = z[k & (M - 1)], zm = z[(M - k) & (M - 1)];
+#pragma unroll
+      for (int side = 0; side < 2; ++side) {
+        if (side == 1 && (k == 0 || 2 * k == M)) {   // k = 0 also yields bin M; k = M/2 is its own mirror
+          if (k == 0) {
+            const float a = zk.x - zk.y;
+            p[M] = a * a;
+          }
+          continue;
+        }
+        const int kk = side ? M - k : k;
+        const float2 A = side ? zm : zk, B = side ? zk : zm;   // Z[kk], Z[M - kk]
+        const float er = 0.5f * (A.x + B.x), ei = 0.5f * (A.y - B.y);     // (Z[kk] + conj Z[M-kk]) / 2
+        const float orr = 0.5f * (A.y + B.y), oi = -0.5f * (A.x - B.x);   // (Z[kk] - conj Z[M-kk]) / (2i)
+        // W^kk; past M/2 (side 1): W^(M-k) = -conj(W^k)
+        const float2 w = side ? make_float2(-ltw2[k].x, ltw2[k].y) : ltw2[k];
+        const float xr = er + (w.x * orr - w.y * oi), xi = ei + (w.x * oi + w.y * orr);
+        p[kk] = fmaf(xr, xr, xi * xi);   // |X|^2 (torch: abs, then squared; equal to an ulp)
+      }
     }
     __syncthreads();
-  }
-  // ---- real split: X[k] = (Z[k] + conj Z[M-k]) / 2 - i W^k (Z[k] - conj Z[M-k]) / 2, W = e^{-2 pi i / N};
-  // power = |X|^2 as torch computes it (abs, then squared)
-  float* p = pw + f * PS;
-  for (int k = j; k <= M / 2; k += TPF) {
-    const float2 zk = z[k & (M - 1)], zm = z[(M - k) & (M - 1)];
-#pragma unroll
-    for (int side = 0; side < 2; ++side) {
-      if (side == 1 && (k == 0 || 2 * k == M)) {   // k = 0 also yields bin M; k = M/2 is its own mirror
-        if (k == 0) {
-          const float a = hypotf(zk.x - zk.y, 0.f);
-          p[M] = a * a;
-        }
-        continue;
+    // ---- mel filters (sparse ranges) and log
+    if (live)
+      for (int m = j; m < nbins; m += TPF) {
+        const int lo = lmi[m], o0 = lmi[nbins + m], o1 = lmi[nbins + m + 1];
+        float e = 0.f;
+        for (int q = o0; q < o1; ++q) e = fmaf(lmw[q], p[lo + q - o0], e);
+        if (use_log) e = __logf(fmaxf(e, 1.1920928955078125e-07f));   // v_log_f32 x ln 2
+        out[F * nbins + m] = e;
       }
-      const int kk = side ? M - k : k;
-      const float2 A = side ? zm : zk, B = side ? zk : zm;   // Z[kk], Z[M - kk]
-      const float er = 0.5f * (A.x + B.x), ei = 0.5f * (A.y - B.y);     // (Z[kk] + conj Z[M-kk]) / 2
-      const float orr = 0.5f * (A.y + B.y), oi = -0.5f * (A.x - B.x);   // (Z[kk] - conj Z[M-kk]) / (2i)
-      // W^kk; past M/2 (side 1): W^(M-k) = -conj(W^k)
-      const float2 w = side ? make_float2(-ltw2[k].x, ltw2[k].y) : ltw2[k];
-      const float xr = er + (w.x * orr - w.y * oi), xi = ei + (w.x * oi + w.y * orr);
-      const float a = hypotf(xr, xi);
-      p[kk] = a * a;
-    }
-  }
-  __syncthreads();
-  if (!live) return;
-  // ---- mel filters (sparse ranges) and log
-  for (int m = j; m < nbins; m += TPF) {
-    const int lo = lmi[m], o0 = lmi[nbins + m], o1 = lmi[nbins + m + 1];
-    float e = 0.f;
-    for (int q = o0; q < o1; ++q) e = fmaf(lmw[q], p[lo + q - o0], e);
-    if (use_log) e = logf(fmaxf(e, 1.1920928955078125e-07f));
-    out[F * nbins + m] = e;
-  }
+  }   // group loop
 }
 
 }  // namespace cfm
@@ -237,7 +315,8 @@ cfm_status cfm_fbank_create(const cfm_fbank_config* cfg, int32_t device, cfm_fba
   const int logm = __builtin_ctz(N) - 1;
   if (logm < 6 || logm > 9) return set_error(CFM_ERR_ASSERT, "fbank: padded frame must be 128 .. 1024 samples");
   if (cfg->num_mel_bins < 1 || cfg->num_mel_bins > 512) return set_error(CFM_ERR_VALUE, "fbank: num_mel_bins");
-  if ((size_t)(cfm::FB - 1) * shift + win > 8192) return set_error(CFM_ERR_ASSERT, "fbank: frame shift too large");
+  if ((size_t)(cfm::FB - 1) * shift + win > (size_t)cfm::FBK_SAMPLES)
+    return set_error(CFM_ERR_ASSERT, "fbank: frame shift too large");
   if (hipSetDevice(device) != hipSuccess) return set_error(CFM_ERR_RUNTIME, "fbank: hipSetDevice");
   auto* h = new cfm_fbank();
   h->cfg = *cfg;
@@ -316,7 +395,15 @@ cfm_status cfm_fbank_compute(const cfm_fbank* h, const float* wave_dev, int64_t 
   if (!wave_dev || !out_dev) return set_error(CFM_ERR_VALUE, "fbank: null buffer");
   const int M = 1 << h->logm;
   const size_t lds = fbank_lds(M, h->shift, h->win, h->nbins, h->n_mel_w);
-  const dim3 grid((unsigned)((nf + cfm::FB - 1) / cfm::FB));
+  // persistent blocks (constants staged once each): two resident per CU
+  static int n_cu = 0;
+  if (!n_cu) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0) n_cu = 256;
+  }
+  const long long groups = (nf + cfm::FB - 1) / cfm::FB;
+  const dim3 grid((unsigned)std::min<long long>(groups, 2LL * n_cu));
   const hipStream_t st = (hipStream_t)stream;
 #define FBK(L)                                                                                                      \
   hipLaunchKernelGGL(cfm::fbank_kernel<L>, grid, dim3(256), lds, st, wave_dev, (long long)num_samples, (long long)nf, \
