@@ -201,3 +201,12 @@ def test_dense_attention_matches_generic(cfm, small_models, clr):
     for b, t in enumerate(lens):
         n = (t - 15) // 8 + 1
         assert _rel_l2(outs[0][b, :n], outs[1][b, :n]) <= 1e-2, b
+
+
+def test_masked_batch_rejects_length_mismatch(cfm, small_models):
+    """xs[i] must be passed at xs_origin_lens[i] frames (encoder.py:556-580 plans from x.size(0) and
+    bounds from xs_origin_lens; they only agree when equal)."""
+    enc = small_models["fp32"]
+    xs = [torch.randn(300, 80), torch.randn(200, 80)]
+    with pytest.raises(ValueError):
+        enc.forward_parallel_chunk(xs, torch.tensor([300, 150], dtype=torch.int32), 16, 32, 32)
