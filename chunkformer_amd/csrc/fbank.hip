@@ -10,8 +10,9 @@
 //   filters (mel = 1127 ln(1 + f/700), low 20 Hz, high = Nyquist); log(max(e, FLT_EPSILON)).
 //
 // Layout and kernel: the waveform is a flat f32 device array (int16 scale, as the reference feeds
-// pydub samples); one 256-thread block takes FB = 16 consecutive frames, stages their samples once
-// in LDS (frames overlap: 15 * shift + win samples), 16 threads per frame.  The N-point real FFT
+// pydub samples); one 256-thread block takes FB = 16 consecutive frames, 16 threads per frame; each
+// wave stages the samples of its 4 frames once in LDS (3 * shift + win: frames overlap) and works
+// without block barriers (every exchange is among the 16 lanes of one frame).  The N-point real FFT
 // runs as an N/2-point complex FFT of z[n] = y[2n] + i y[2n+1] plus the real-split post-pass: for
 // N = 512 (the reference's 25 ms at 16 kHz) a four-step 16 x 16 FFT, two 16-point DFTs in
 // registers around one LDS transpose; other sizes a radix-2 FFT in LDS (input written in
@@ -26,12 +27,22 @@
 #include "cfm_common.h"
 #include "status.h"
 
+#ifndef CFM_FBANK_DIAG
+#define CFM_FBANK_DIAG 0   // timing-only builds (tools/build_variant.py): 1 no mel sums, 2 no DFTs
+#endif
+
 namespace cfm {
 
 namespace {
-constexpr int FB = 16;    // frames per block
+constexpr int FB = 16;    // frames per block (one group)
 constexpr int TPF = 16;   // threads per frame
-constexpr int FBK_SAMPLES = 8192;   // samples of one group staged per block (15 shift + win)
+constexpr int FBW = 4;    // frames per wave (64 / TPF)
+constexpr int FBK_WSAMPLES = 2048;   // samples staged per wave and group (3 shift + win)
+
+// Every LDS exchange after the constants is between the 16 lanes of one frame, i.e. inside one
+// wave: LDS operations of a wave complete in order, so waiting for them (and fencing the
+// compiler) replaces the block barriers.
+CFM_DEV void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
 CFM_DEV int brev(int v, int bits) { return (int)(__builtin_bitreverse32((unsigned)v) >> (32 - bits)); }
 CFM_DEV float2 cmul(float2 a, float2 w) { return make_float2(a.x * w.x - a.y * w.y, a.x * w.y + a.y * w.x); }
@@ -83,38 +94,40 @@ __global__ __launch_bounds__(256) void fbank_kernel(const float* __restrict__ wa
   const int nw = mel_off[nbins];
   float* lmw = lwin + win;                                    // [nw] mel weights
   int* lmi = reinterpret_cast<int*>(lmw + nw);                // [nbins] lo, [nbins + 1] offsets
-  float* sx = reinterpret_cast<float*>(lmi + 2 * nbins + 1);  // block's samples
-  const int tid = threadIdx.x, f = tid / TPF, j = tid % TPF;
+  const int wspan = (FBW - 1) * shift + win;
+  const int tid = threadIdx.x, f = tid / TPF, j = tid % TPF, wv = tid >> 6, lane = tid & 63;
+  float* sx = reinterpret_cast<float*>(lmi + 2 * nbins + 1) + wv * wspan;   // this wave's samples
   // constants in LDS once per (persistent) block: every stage and filter reads them at LDS latency
   for (int i = tid; i < M / 2; i += 256) ltw[i] = tw[i];
   for (int i = tid; i <= M / 2; i += 256) ltw2[i] = tw2[i];
   for (int i = tid; i < win; i += 256) lwin[i] = window[i];
   for (int i = tid; i < nw; i += 256) lmw[i] = mel_w[i];
   for (int i = tid; i < 2 * nbins + 1; i += 256) lmi[i] = i < nbins ? mel_lo[i] : mel_off[i - nbins];
-  // samples of a 16-frame group (<= FBK_SAMPLES), prefetched into registers one group ahead
-  const int span = (FB - 1) * shift + win;
-  float pre[FBK_SAMPLES / 256];
+  __syncthreads();   // constants staged; from here on the waves run independently
+  // samples of the wave's 4 frames (3 shift + win <= FBK_WSAMPLES), prefetched into registers one
+  // group ahead
+  float pre[FBK_WSAMPLES / 64];
   const long long ngroups = (n_frames + FB - 1) / FB;
   auto fetch = [&](long long grp) {
-    const long long base = grp * FB * shift;
+    const long long base = (grp * FB + wv * FBW) * shift;
 #pragma unroll
-    for (int q = 0; q < FBK_SAMPLES / 256; ++q) {
-      const int i = tid + 256 * q;
-      pre[q] = (grp < ngroups && i < span && base + i < n_samples) ? wave[base + i] : 0.f;
+    for (int q = 0; q < FBK_WSAMPLES / 64; ++q) {
+      const int i = lane + 64 * q;
+      pre[q] = (grp < ngroups && i < wspan && base + i < n_samples) ? wave[base + i] : 0.f;
     }
   };
   fetch(blockIdx.x);
   for (long long grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {
-    __syncthreads();   // the previous group's reads of sx / cz / pw are done
+    wave_lds_sync();   // the previous group's reads of sx / cz / pw are done
 #pragma unroll
-    for (int q = 0; q < FBK_SAMPLES / 256; ++q)
-      if (tid + 256 * q < span) sx[tid + 256 * q] = pre[q];
-    __syncthreads();
+    for (int q = 0; q < FBK_WSAMPLES / 64; ++q)
+      if (lane + 64 * q < wspan) sx[lane + 64 * q] = pre[q];
+    wave_lds_sync();
     fetch(grp + gridDim.x);
 
     const long long F = grp * FB + f;
     const bool live = F < n_frames;
-    const float* x = sx + f * shift;
+    const float* x = sx + (f - wv * FBW) * shift;
     float2* z = cz + f * ZS;
     // ---- frame mean over the 16 threads of the frame (lanes 16f .. 16f+15 of one wave)
     float s = 0.f;
@@ -123,62 +136,30 @@ __global__ __launch_bounds__(256) void fbank_kernel(const float* __restrict__ wa
 #pragma unroll
     for (int o = TPF / 2; o > 0; o >>= 1) s += __shfl_xor(s, o, TPF);
     const float mean = remove_dc ? s / (float)win : 0.f;
-    if constexpr (LOGM == 8) {
-      // ---- four-step 256 = 16 x 16 FFT: thread j takes z[j + 16 m] (m = 0..15), a 16-point DFT in
-      // registers, the W256^(j k1) twiddle, one transpose through LDS, a second 16-point DFT
-      float2 a[16];
-#pragma unroll
-      for (int m = 0; m < 16; ++m) {
-        const int n0 = 2 * (j + 16 * m);
-        float y0 = 0.f, y1 = 0.f;   // DC removal, pre-emphasis (x[-1] = x[0]), window, zero pad
-        if (live && n0 < win) {
-          const float c0 = x[n0] - mean, p0 = x[n0 > 0 ? n0 - 1 : 0] - mean;
-          y0 = (c0 - preemph * p0) * lwin[n0];
-          if (n0 + 1 < win) y1 = ((x[n0 + 1] - mean) - preemph * c0) * lwin[n0 + 1];
-        }
-        a[m] = make_float2(y0, y1);
+    // ---- DC removal, pre-emphasis, window, zero pad; z[n] = y[2n] + i y[2n+1] at bit-reversed n
+    for (int n = j; n < 2 * M; n += TPF) {
+      float y = 0.f;
+      if (live && n < win) {
+        const float cur = x[n] - mean, prev = x[n > 0 ? n - 1 : 0] - mean;
+        y = (cur - preemph * prev) * lwin[n];
       }
-      fft16(a);
-#pragma unroll
-      for (int k1 = 0; k1 < 16; ++k1) {
-        const int e = j * k1;   // < 256: W256^e = -W256^(e - 128) past 128
-        const float2 w = ltw[e & 127];
-        z[16 * k1 + j] = cmul(a[k1], (e & 128) ? make_float2(-w.x, -w.y) : w);
-      }
-      __syncthreads();
-#pragma unroll
-      for (int t = 0; t < 16; ++t) a[t] = z[16 * j + t];
-      fft16(a);   // a[k2] = Z[j + 16 k2]
-      __syncthreads();
-#pragma unroll
-      for (int k2 = 0; k2 < 16; ++k2) z[j + 16 * k2] = a[k2];
-      __syncthreads();
-    } else {
-      // ---- DC removal, pre-emphasis, window, zero pad; z[n] = y[2n] + i y[2n+1] at bit-reversed n
-      for (int n = j; n < 2 * M; n += TPF) {
-        float y = 0.f;
-        if (live && n < win) {
-          const float cur = x[n] - mean, prev = x[n > 0 ? n - 1 : 0] - mean;
-          y = (cur - preemph * prev) * lwin[n];
-        }
-        float* zp = reinterpret_cast<float*>(&z[brev(n >> 1, LOGM)]);
-        zp[n & 1] = y;
-      }
-      __syncthreads();
-      // ---- radix-2 DIT, M/2 butterflies per stage, 16 threads per frame
+      float* zp = reinterpret_cast<float*>(&z[brev(n >> 1, LOGM)]);
+      zp[n & 1] = y;
+    }
+    wave_lds_sync();
+    // ---- radix-2 DIT, M/2 butterflies per stage, 16 threads per frame
 #pragma unroll 1
-      for (int st = 1; st <= LOGM; ++st) {
-        const int half = 1 << (st - 1);
-        for (int b = j; b < M / 2; b += TPF) {
-          const int k = b & (half - 1), i0 = ((b >> (st - 1)) << st) + k, i1 = i0 + half;
-          const float2 w = ltw[k << (LOGM - st)];
-          const float2 av = z[i0], c = z[i1];
-          const float2 t = make_float2(w.x * c.x - w.y * c.y, w.x * c.y + w.y * c.x);
-          z[i0] = make_float2(av.x + t.x, av.y + t.y);
-          z[i1] = make_float2(av.x - t.x, av.y - t.y);
-        }
-        __syncthreads();
+    for (int st = 1; st <= LOGM; ++st) {
+      const int half = 1 << (st - 1);
+      for (int b = j; b < M / 2; b += TPF) {
+        const int k = b & (half - 1), i0 = ((b >> (st - 1)) << st) + k, i1 = i0 + half;
+        const float2 w = ltw[k << (LOGM - st)];
+        const float2 av = z[i0], c = z[i1];
+        const float2 t = make_float2(w.x * c.x - w.y * c.y, w.x * c.y + w.y * c.x);
+        z[i0] = make_float2(av.x + t.x, av.y + t.y);
+        z[i1] = make_float2(av.x - t.x, av.y - t.y);
       }
+      wave_lds_sync();
     }
     // ---- real split: X[k] = (Z[k] + conj Z[M-k]) / 2 - i W^k (Z[k] - conj Z[M-k]) / 2, W = e^{-2 pi i / N};
     // power = |X|^2
@@ -204,7 +185,7 @@ __global__ __launch_bounds__(256) void fbank_kernel(const float* __restrict__ wa
         p[kk] = fmaf(xr, xr, xi * xi);   // |X|^2 (torch: abs, then squared; equal to an ulp)
       }
     }
-    __syncthreads();
+    wave_lds_sync();
     // ---- mel filters (sparse ranges) and log
     if (live)
       for (int m = j; m < nbins; m += TPF) {
@@ -212,6 +193,158 @@ __global__ __launch_bounds__(256) void fbank_kernel(const float* __restrict__ wa
         float e = 0.f;
         for (int q = o0; q < o1; ++q) e = fmaf(lmw[q], p[lo + q - o0], e);
         if (use_log) e = __logf(fmaxf(e, 1.1920928955078125e-07f));   // v_log_f32 x ln 2
+        out[F * nbins + m] = e;
+      }
+  }   // group loop
+}
+
+
+// N = 512 (the reference's 25 ms / 10 ms at 16 kHz; win <= 512): the samples go straight from
+// global memory into registers -- lane j of a frame holds samples 2(j + 16m), 2(j + 16m) + 1,
+// m = 0..15, which are exactly its inputs of the four-step FFT -- the pre-emphasis neighbour of
+// an even sample comes from lane j - 1 by a DPP row rotate, and the power spectrum is written over
+// the frame's own FFT buffer.  LDS: 34 KiB of FFT buffers + 8 KiB of constants per 16 frames ->
+// 3 blocks per CU (143 VGPRs), and no sample staging.  Persistent blocks, samples of the next
+// group in flight while the current one is transformed.
+__global__ __launch_bounds__(256, 3) void fbank512_kernel(const float* __restrict__ wave, long long n_samples,
+                                                          long long n_frames, int shift, int win,
+                                                          const float* __restrict__ window,
+                                                          const float2* __restrict__ tw, const float2* __restrict__ tw2,
+                                                          const int* __restrict__ mel_lo, const int* __restrict__ mel_off,
+                                                          const float* __restrict__ mel_w, int nbins, float preemph,
+                                                          int remove_dc, int use_log, float* __restrict__ out,
+                                                          int vec2) {
+  // (transpose rows of pitch 17 or 18 against bank conflicts measured equal or slower: the row
+  // reads are ds_read_b128 at pitch 16)
+  constexpr int M = 256, ZP = 16, ZS = M + 2;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float2* cz = reinterpret_cast<float2*>(smem);               // [FB][ZS]: FFT buffer, then |X|^2
+  float2* ltw = cz + FB * ZS;                                 // [16 k1][16 j] W256^(j k1)
+  float2* ltw2 = ltw + M;                                     // [M/2 + 1] real-split twiddles
+  float* lwin = reinterpret_cast<float*>(ltw2 + M / 2 + 1);   // [2M] window, zero past win
+  const int nw = mel_off[nbins];
+  float* lmw = lwin + 2 * M;                                  // [nw] mel weights
+  int* lmi = reinterpret_cast<int*>(lmw + nw);                // [nbins] lo, [nbins + 1] offsets
+  const int tid = threadIdx.x, f = tid / TPF, j = tid % TPF;
+  for (int i = tid; i < M; i += 256) {   // lane j reads row k1 at column j: conflict-free
+    const int e = (i >> 4) * (i & 15);     // < 256: W256^e = -W256^(e - 128) past 128
+    const float2 w = tw[e & 127];
+    ltw[i] = (e & 128) ? make_float2(-w.x, -w.y) : w;
+  }
+  for (int i = tid; i <= M / 2; i += 256) ltw2[i] = tw2[i];
+  for (int i = tid; i < 2 * M; i += 256) lwin[i] = i < win ? window[i] : 0.f;
+  for (int i = tid; i < nw; i += 256) lmw[i] = mel_w[i];
+  for (int i = tid; i < 2 * nbins + 1; i += 256) lmi[i] = i < nbins ? mel_lo[i] : mel_off[i - nbins];
+  __syncthreads();   // constants staged; from here on the waves run independently
+  const long long ngroups = (n_frames + FB - 1) / FB;
+  float2 pre[16];
+  auto fetch = [&](long long grp) {
+    const long long F = grp * FB + f;
+    const bool ok = grp < ngroups && F < n_frames;   // a live frame's samples are all in range
+    const float* xs = wave + (ok ? F * shift : 0);
+    if (vec2) {   // frames start 8-B aligned: one dwordx2 per sample pair
+#pragma unroll
+      for (int m = 0; m < 16; ++m) {
+        const int n0 = 2 * (j + 16 * m);
+        pre[m] = ok && n0 + 1 < win ? *reinterpret_cast<const float2*>(xs + n0)
+                                    : make_float2(ok && n0 < win ? xs[n0] : 0.f, 0.f);
+      }
+    } else {
+#pragma unroll
+      for (int m = 0; m < 16; ++m) {
+        const int n0 = 2 * (j + 16 * m);
+        pre[m].x = ok && n0 < win ? xs[n0] : 0.f;
+        pre[m].y = ok && n0 + 1 < win ? xs[n0 + 1] : 0.f;
+      }
+    }
+  };
+  fetch(blockIdx.x);
+  for (long long grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {
+    const long long F = grp * FB + f;
+    const bool live = F < n_frames;
+    float2* z = cz + f * ZS;
+    // ---- frame mean over the 16 lanes of the frame (samples past win are zero)
+    float s = 0.f;
+#pragma unroll
+    for (int m = 0; m < 16; ++m) s += pre[m].x + pre[m].y;
+#pragma unroll
+    for (int o = TPF / 2; o > 0; o >>= 1) s += __shfl_xor(s, o, TPF);
+    const float mean = remove_dc ? s / (float)win : 0.f;
+    // ---- DC removal, pre-emphasis (x[-1] = x[0]), window, zero pad: a[m] = (y[n0], y[n0 + 1]).
+    // x[n0 - 1] is lane j-1's odd sample of the same m (row_ror:1 within the 16 lanes), for j = 0
+    // lane 15's odd sample of m - 1 (the previous m's rotate)
+    float2 a[16];
+    float up_prev = 0.f;
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
+      const float up = __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, pre[m].y),
+                                                                          0x121, 0xf, 0xf, false));
+      const float prev = j > 0 ? up : (m > 0 ? up_prev : pre[0].x);
+      up_prev = up;
+      const float c0 = pre[m].x - mean, c1 = pre[m].y - mean;
+      const float2 w = reinterpret_cast<const float2*>(lwin)[j + 16 * m];
+      a[m] = make_float2((c0 - preemph * (prev - mean)) * w.x, (c1 - preemph * c0) * w.y);
+    }
+    // ---- four-step 256 = 16 x 16 FFT: a 16-point DFT in registers, the W256^(j k1) twiddle, one
+    // transpose through LDS, a second 16-point DFT
+#if CFM_FBANK_DIAG != 2
+    fft16(a);
+#endif
+    wave_lds_sync();   // the previous group's mel reads of z are done
+#pragma unroll
+    for (int k1 = 0; k1 < 16; ++k1) z[ZP * k1 + j] = cmul(a[k1], ltw[16 * k1 + j]);
+    wave_lds_sync();
+#pragma unroll
+    for (int t = 0; t < 16; ++t) a[t] = z[ZP * j + t];
+#if CFM_FBANK_DIAG != 2
+    fft16(a);   // a[k2] = Z[j + 16 k2]
+#endif
+    wave_lds_sync();
+#pragma unroll
+    for (int k2 = 0; k2 < 16; ++k2) z[j + 16 * k2] = a[k2];
+    fetch(grp + gridDim.x);   // the next group's samples load under the real split and mel filters
+    wave_lds_sync();
+    // ---- real split and |X|^2 into registers (k = j + 16 i <= M/2, both mirrors), then over z
+    float q0[9], q1[9];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+      const int k = j + 16 * i;
+      q0[i] = q1[i] = 0.f;
+      if (k > M / 2) continue;
+      const float2 zk = z[k & (M - 1)], zm = z[(M - k) & (M - 1)];
+      const float2 w2 = ltw2[k];
+#pragma unroll
+      for (int side = 0; side < 2; ++side) {
+        const float2 A = side ? zm : zk, B = side ? zk : zm;   // Z[kk], Z[M - kk]
+        const float er = 0.5f * (A.x + B.x), ei = 0.5f * (A.y - B.y);
+        const float orr = 0.5f * (A.y + B.y), oi = -0.5f * (A.x - B.x);
+        const float2 w = side ? make_float2(-w2.x, w2.y) : w2;   // W^(M-k) = -conj(W^k)
+        const float xr = er + (w.x * orr - w.y * oi), xi = ei + (w.x * oi + w.y * orr);
+        (side ? q1[i] : q0[i]) = fmaf(xr, xr, xi * xi);
+      }
+      if (k == 0) q1[i] = (zk.x - zk.y) * (zk.x - zk.y);   // bin M
+    }
+    wave_lds_sync();   // every lane's reads of z are done before z is overwritten
+    float* p = reinterpret_cast<float*>(z);
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+      const int k = j + 16 * i;
+      if (k > M / 2) continue;
+      p[k] = q0[i];
+      if (k != M / 2) p[k == 0 ? M : M - k] = q1[i];
+    }
+    wave_lds_sync();
+    // ---- mel filters (sparse ranges) and log
+    if (live)
+      for (int m = j; m < nbins; m += TPF) {
+        const int lo = lmi[m], o0 = lmi[nbins + m], o1 = lmi[nbins + m + 1];
+        float e = 0.f;
+#if CFM_FBANK_DIAG == 1
+        e = p[lo] + (float)(o1 - o0);
+#else
+        for (int q = o0; q < o1; ++q) e = fmaf(lmw[q], p[lo + q - o0], e);
+#endif
+        if (use_log) e = __logf(fmaxf(e, 1.1920928955078125e-07f));
         out[F * nbins + m] = e;
       }
   }   // group loop
@@ -233,9 +366,13 @@ namespace {
 using cfm::set_error;
 
 // dynamic LDS of fbank_kernel: spectra [FB][M + 2] float2, power [FB][M + 5], the block's samples
+size_t fbank512_lds(int nbins, int nw) {
+  return (size_t)cfm::FB * 258 * 8 + (size_t)(256 + 129) * 8 + (size_t)(512 + nw + 2 * nbins + 1) * 4;
+}
+
 size_t fbank_lds(int M, int shift, int win, int nbins, int nw) {
   return (size_t)cfm::FB * (M + 2) * 8 + (size_t)cfm::FB * (M + 5) * 4 + (size_t)(M + 1) * 8 +
-         (size_t)(win + nw + 2 * nbins + 1) * 4 + (size_t)((cfm::FB - 1) * shift + win) * 4;
+         (size_t)(win + nw + 2 * nbins + 1) * 4 + (size_t)(cfm::FB / cfm::FBW) * ((cfm::FBW - 1) * shift + win) * 4;
 }
 
 // torch.hann_window(N, periodic=False) (and the other kaldi window types) as torchaudio builds it in
@@ -315,8 +452,8 @@ cfm_status cfm_fbank_create(const cfm_fbank_config* cfg, int32_t device, cfm_fba
   const int logm = __builtin_ctz(N) - 1;
   if (logm < 6 || logm > 9) return set_error(CFM_ERR_ASSERT, "fbank: padded frame must be 128 .. 1024 samples");
   if (cfg->num_mel_bins < 1 || cfg->num_mel_bins > 512) return set_error(CFM_ERR_VALUE, "fbank: num_mel_bins");
-  if ((size_t)(cfm::FB - 1) * shift + win > (size_t)cfm::FBK_SAMPLES)
-    return set_error(CFM_ERR_ASSERT, "fbank: frame shift too large");
+  if (logm != 8 && (size_t)(cfm::FBW - 1) * shift + win > (size_t)cfm::FBK_WSAMPLES)
+    return set_error(CFM_ERR_ASSERT, "fbank: frame length / shift too large (3 shift + length > 2048 samples)");
   if (hipSetDevice(device) != hipSuccess) return set_error(CFM_ERR_RUNTIME, "fbank: hipSetDevice");
   auto* h = new cfm_fbank();
   h->cfg = *cfg;
@@ -354,11 +491,10 @@ cfm_status cfm_fbank_create(const cfm_fbank_config* cfg, int32_t device, cfm_fba
     cfm_fbank_destroy(h);
     return set_error(CFM_ERR_RUNTIME, "fbank: device allocation / upload failed");
   }
-  // LDS beyond the default 64 KiB (N = 1024 frames)
+  // LDS beyond the default 64 KiB (N = 1024 frames; the N = 512 kernel needs < 40 KiB)
   const size_t lds = fbank_lds(M, shift, win, h->nbins, (int)mw.size());
-  if (lds > 65536) {
+  if (logm != 8 && lds > 65536) {
     const void* fn = logm == 9   ? (const void*)cfm::fbank_kernel<9>
-                     : logm == 8 ? (const void*)cfm::fbank_kernel<8>
                      : logm == 7 ? (const void*)cfm::fbank_kernel<7>
                                  : (const void*)cfm::fbank_kernel<6>;
     if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) {
@@ -394,8 +530,8 @@ cfm_status cfm_fbank_compute(const cfm_fbank* h, const float* wave_dev, int64_t 
   if (nf == 0) return CFM_OK;
   if (!wave_dev || !out_dev) return set_error(CFM_ERR_VALUE, "fbank: null buffer");
   const int M = 1 << h->logm;
-  const size_t lds = fbank_lds(M, h->shift, h->win, h->nbins, h->n_mel_w);
-  // persistent blocks (constants staged once each): two resident per CU
+  const size_t lds = h->logm == 8 ? fbank512_lds(h->nbins, h->n_mel_w) : fbank_lds(M, h->shift, h->win, h->nbins, h->n_mel_w);
+  // persistent blocks (constants staged once each): three resident per CU for N = 512, else two
   static int n_cu = 0;
   if (!n_cu) {
     int dev = 0;
@@ -403,7 +539,7 @@ cfm_status cfm_fbank_compute(const cfm_fbank* h, const float* wave_dev, int64_t 
     if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0) n_cu = 256;
   }
   const long long groups = (nf + cfm::FB - 1) / cfm::FB;
-  const dim3 grid((unsigned)std::min<long long>(groups, 2LL * n_cu));
+  const dim3 grid((unsigned)std::min<long long>(groups, (h->logm == 8 ? 3LL : 2LL) * n_cu));
   const hipStream_t st = (hipStream_t)stream;
 #define FBK(L)                                                                                                      \
   hipLaunchKernelGGL(cfm::fbank_kernel<L>, grid, dim3(256), lds, st, wave_dev, (long long)num_samples, (long long)nf, \
@@ -412,7 +548,12 @@ cfm_status cfm_fbank_compute(const cfm_fbank* h, const float* wave_dev, int64_t 
   switch (h->logm) {
     case 6: FBK(6); break;
     case 7: FBK(7); break;
-    case 8: FBK(8); break;
+    case 8:
+      hipLaunchKernelGGL(cfm::fbank512_kernel, grid, dim3(256), lds, st, wave_dev, (long long)num_samples, (long long)nf,
+                         h->shift, h->win, h->window, h->tw, h->tw2, h->mel_lo, h->mel_off, h->mel_w, h->nbins,
+                         h->cfg.preemphasis_coefficient, h->cfg.remove_dc_offset, h->cfg.use_log_fbank, out_dev,
+                         (int)(h->shift % 2 == 0 && reinterpret_cast<uintptr_t>(wave_dev) % 8 == 0));
+      break;
     default: FBK(9); break;
   }
 #undef FBK

@@ -59,6 +59,33 @@ def test_fbank_options(fb, window_type, bins, sr, length):
     assert (got - exp).abs().max().item() <= TOL
 
 
+@pytest.mark.parametrize("shift_ms,length_ms,offset", [(10.0, 25.0, 1), (10.0625, 25.0, 0), (10.0, 25.0625, 0),
+                                                       (10.0625, 31.9375, 3)])
+def test_fbank_odd_shift_length_and_unaligned_samples(fb, shift_ms, length_ms, offset):
+    """Odd frame shift / odd frame length (161 / 401 / 511 samples) and a waveform that does not
+    start 8-B aligned: the scalar sample loads and the partial last pair of the N = 512 kernel."""
+    x = _speechlike(30000 + offset, 11)
+    kw = dict(num_mel_bins=80, frame_length=length_ms, frame_shift=shift_ms, dither=0.0, sample_frequency=16000)
+    xd = x.cuda()[offset:]
+    got = fb.fbank(xd, **kw).cpu()
+    exp = ref.fbank(x[offset:], **kw)
+    assert got.shape == exp.shape
+    assert (got - exp).abs().max().item() <= TOL
+
+
+@pytest.mark.parametrize("remove_dc,preemph,use_log", [(False, 0.97, True), (True, 0.0, True), (True, 0.97, False)])
+def test_fbank_switches(fb, remove_dc, preemph, use_log):
+    x = _speechlike(24000, 5)
+    kw = dict(REF, remove_dc_offset=remove_dc, preemphasis_coefficient=preemph, use_log_fbank=use_log)
+    got = fb.fbank(x.cuda(), **kw).cpu()
+    exp = ref.fbank(x, **kw)
+    assert got.shape == exp.shape
+    if use_log:
+        assert (got - exp).abs().max().item() <= TOL
+    else:   # linear mel energies: relative to each value (2e-3 in log = 0.2% relative)
+        assert ((got - exp).abs() / exp.abs().clamp_min(1e-3)).max().item() <= TOL
+
+
 def test_fbank_silence_and_dc(fb):
     x = torch.cat([torch.zeros(8000), torch.full((8000,), -77.0)])
     got, exp = fb.fbank(x.cuda(), **REF).cpu(), ref.fbank(x, **REF)
