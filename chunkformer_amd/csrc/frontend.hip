@@ -149,85 +149,86 @@ __global__ __launch_bounds__(256, 3) void fe_conv0_dw_mfma_kernel(const float* _
         for (int j = 0; j < 8; ++j) xa[s][j] = (bf16)xs[(j / 3) * FE_F0 + j % 3];
       } else {
         xa[s][0] = (bf16)xs[2 * FE_F0 + 2];
+        xa[s][1] = (bf16)1.f;   // k = 9: the conv0 bias row (B holds b0 there; bf16 as under autocast)
 #pragma unroll
-        for (int j = 1; j < 8; ++j) xa[s][j] = (bf16)0.f;
+        for (int j = 2; j < 8; ++j) xa[s][j] = (bf16)0.f;
       }
     }
   }
-  // per-channel-tile weights, software-pipelined one tile ahead
-  bf16x8 wb;
-  float wk[9], bc0, bc1;
+  // per-channel-tile weights, software-pipelined one tile ahead: load_w only issues the raw
+  // 16-B loads; they are unpacked when the next tile starts, so their wait lands a whole tile
+  // later.  (The compiler's wait at the top of a pass also covers the previous pass's stores --
+  // loads and stores share vmcnt in issue order; hand-counted waits on inline-asm loads that
+  // leave those stores in flight measured within 2%, not kept.)
+  f32x4 qw[5];
   auto load_w = [&](int c) {
     const f32x4* wp = reinterpret_cast<const f32x4*>(wpack + (size_t)c * FE_WPACK);
-    const f32x4 q0 = wp[0], q1 = wp[1], q2 = wp[2], q3 = wp[3], q4 = wp[4], q5 = wp[5];
-    // lanes of the upper half need only conv0 tap 8 (k = 8); the rest of K is zero
-    const float t[9] = {q0[0], q0[1], q0[2], q0[3], q1[0], q1[1], q1[2], q1[3], q2[0]};
 #pragma unroll
-    for (int j = 0; j < 8; ++j) wb[j] = (bf16)(hh ? (j ? 0.f : t[8]) : t[j]);
-    const float u[9] = {q2[1], q2[2], q2[3], q3[0], q3[1], q3[2], q3[3], q4[0], q4[1]};
-#pragma unroll
-    for (int s = 0; s < 9; ++s) wk[s] = u[s];
-    bc0 = q4[2];
-    bc1 = q4[3];
-    (void)q5;
+    for (int i = 0; i < 5; ++i) qw[i] = wp[i];
   };
   load_w(n);
-  for (int ct = 0; ct < d; ct += 32) {
-    const int c = ct + n;
-    const bf16x8 wbc = wb;
-    float wkc[9];
+  // the window's output range as a wave-uniform buffer descriptor (readfirstlane: SGPRs, so the
+  // stores need no waterfall loop)
+  const unsigned long long obase = (unsigned long long)(out + (size_t)win * P * d);
+  const unsigned long long obu = ((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(obase >> 32)) << 32) |
+                                 (unsigned)__builtin_amdgcn_readfirstlane((unsigned)obase);
+  const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)obu, (short)0, __builtin_amdgcn_readfirstlane(P * d * 2), 0x00020000);
+  unsigned voff[4];   // byte offsets of this lane's 16-B store chunks at channel 0
 #pragma unroll
-    for (int s = 0; s < 9; ++s) wkc[s] = wk[s];
-    f32x16 seed, o;
+  for (int k = 0; k < 4; ++k) voff[k] = (unsigned)(((pw + (lane >> 3) + 8 * k) * d + (lane & 7) * 8) * 2);
+  // two 32-channel tiles per iteration, then one unconditional store pass of the 64 staged
+  // channels
+  for (int ct = 0; ct < d; ct += 64) {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      seed[r] = bc0;
-      o[r] = bc1;
+    for (int half = 0; half < 2; ++half) {
+      // lanes of the upper half need only conv0 tap 8 (k = 8) and the bias b0 (k = 9); the rest
+      // of K is zero, so the conv0 MFMAs start from a zero accumulator
+      const float t[9] = {qw[0][0], qw[0][1], qw[0][2], qw[0][3], qw[1][0], qw[1][1], qw[1][2], qw[1][3], qw[2][0]};
+      bf16x8 wcur;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) wcur[j] = (bf16)(hh ? (j == 0 ? t[8] : j == 1 ? qw[4][2] : 0.f) : t[j]);
+      const float wkc[9] = {qw[2][1], qw[2][2], qw[2][3], qw[3][0], qw[3][1], qw[3][2], qw[3][3], qw[4][0], qw[4][1]};
+      const f32x16 seed = {};
+      f32x16 o;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) o[r] = qw[4][3];
+      load_w(min(ct + 32 * half + 32 + n, d - 1));   // past the last tile: a harmless reload
+      // taps are software-pipelined one deep: MFMA s+1 is issued before tap s's relu/FMA work
+      // (scheduling barriers pin the order: without them the compiler sinks MFMA s+1 below tap
+      // s's VALU and both accumulator sets share registers, serialising MFMA and VALU per wave)
+      f32x16 acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xa[0], wcur, seed, 0, 0, 0);
+#pragma unroll
+      for (int s = 0; s < 9; ++s) {
+        f32x16 nxt;
+        if (s + 1 < 9) nxt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xa[s + 1], wcur, seed, 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        // one v_max_f32 + one v_fma_f32 per value (IEEE mode off in build.py: no canonicalising
+        // max in front; no SLP packing: a v_pk_fma_f32 beside MFMAs issues slower than two v_fma_f32)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[r] = fmaf(fmaxf(acc[r], 0.f), wkc[s], o[r]);
+        __builtin_amdgcn_sched_barrier(0);
+        if (s + 1 < 9) acc = nxt;
+      }
+      char* os = ostage[wv];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = 8 * (r >> 2) + 4 * hh + (r & 3);
+        *reinterpret_cast<bf16*>(os + m * OPITCH + (32 * half + n) * 2) = (bf16)o[r];
+      }
     }
-    if (ct + 32 < d) load_w(c + 32);
-    // taps are software-pipelined one deep: MFMA s+1 is issued before tap s's
-    // relu/FMA work; the asm after each tap's VALU (it consumes the dw1 accumulators and
-    // re-defines the B operand the MFMA two taps ahead reads) keeps at most two
-    // accumulator sets live
-    bf16x8 wcur = wbc;
-    typedef float f32x2 __attribute__((ext_vector_type(2)));
-    f32x16 acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xa[0], wcur, seed, 0, 0, 0);
+    // 64 channels staged: lane -> 16-B chunk (lane & 7) of positions (lane >> 3) + 8k, buffer
+    // stores against the window's range (positions past P fall outside it and are dropped by
+    // the hardware), so the store needs no branch
+    const char* os = ostage[wv];
 #pragma unroll
-    for (int s = 0; s < 9; ++s) {
-      f32x16 nxt;
-      if (s + 1 < 9) nxt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xa[s + 1], wcur, seed, 0, 0, 0);
-#ifndef CFM_FE_PK
-      // one v_max_f32 + one v_fma_f32 per value (IEEE mode off in build.py: no canonicalising
-      // max in front; no SLP packing: a v_pk_fma_f32 beside MFMAs issues slower than two v_fma_f32)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) o[r] = fmaf(fmaxf(acc[r], 0.f), wkc[s], o[r]);
+    for (int k = 0; k < 4; ++k) {
+      const u32x4 v = *reinterpret_cast<const u32x4*>(os + ((lane >> 3) + 8 * k) * OPITCH + (lane & 7) * 16);
+#ifndef CFM_FE_DIAG_NOSTORE   // timing-only build: no output stores
+      __builtin_amdgcn_raw_buffer_store_b128(v, ors, voff[k], ct * 2, 0);
 #else
-      const f32x2 w2 = (f32x2){wkc[s], wkc[s]};
-#pragma unroll
-      for (int r = 0; r < 16; r += 2) {
-        const f32x2 a2 = (f32x2){fmaxf(acc[r], 0.f), fmaxf(acc[r + 1], 0.f)};
-        const f32x2 o2 = __builtin_elementwise_fma(w2, a2, (f32x2){o[r], o[r + 1]});
-        o[r] = o2[0];
-        o[r + 1] = o2[1];
-      }
+      asm volatile("" ::"v"(v));
 #endif
-      asm volatile("" : "+v"(wcur), "+v"(o));
-      if (s + 1 < 9) acc = nxt;
-    }
-    char* os = ostage[wv];
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int m = 8 * (r >> 2) + 4 * hh + (r & 3);
-      *reinterpret_cast<bf16*>(os + m * OPITCH + ((ct & 32) + n) * 2) = (bf16)o[r];
-    }
-    if (ct & 32) {   // 64 channels staged: lane -> 16-B chunk (lane & 7) of positions (lane >> 3) + 8k
-      bf16* ow = out + (size_t)win * P * d + (ct - 32) + (lane & 7) * 8;   // 32-bit offsets inside the window
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int m = (lane >> 3) + 8 * k;
-        const u32x4 v = *reinterpret_cast<const u32x4*>(os + m * OPITCH + (lane & 7) * 16);
-        if (pw + m < P) *reinterpret_cast<u32x4*>(ow + (pw + m) * d) = v;
-      }
     }
   }
 }
