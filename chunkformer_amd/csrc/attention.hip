@@ -400,69 +400,43 @@ __global__ __launch_bounds__(512, 1) void chunk_attention_ring_kernel(
           for (int st = 0; st < 4; ++st) S[t][st] = (f32x4){-INFINITY, -INFINITY, -INFINITY, -INFINITY};
           continue;
         }
-        // all fragment reads of the tile first (K: 4 subtiles x 2, P: 5 band subtiles x 2), then the
-        // MFMAs back to back: one LDS latency per tile instead of one per MFMA pair
+        // the band first: its skewed values (bf16, through the per-wave scratch) become the C
+        // operand of the score MFMAs, so S = K.(q+u) + band costs no VALU add
         bf16x8 kf[4][2], pf[5][2];
+        const int kb0 = p_base - i0 - 15 + j0;
+        // band subtile 0 of tile t is subtile 4 of tile t - 1 (P rows kb0 .. kb0 + 15, 64 rows on):
+        // carried in registers (tiles past key_hi are skipped only at the end, so tile t - 1 ran)
+        const bool carry = t > 0 && reuse_band;
+#pragma unroll
+        for (int pt = 0; pt < 5; ++pt) {
+          if (pt == 0 && carry) continue;
+          const char* pb_ = pl + (kb0 + 16 * pt) * 128;
+#pragma unroll
+          for (int s = 0; s < 2; ++s) pf[pt][s] = *reinterpret_cast<const bf16x8*>(pb_ + frag_lane[s]);
+        }
 #pragma unroll
         for (int st = 0; st < 4; ++st) {
           const char* kb_ = kr + ring16(j0 + 16 * st) * 128;
 #pragma unroll
           for (int s = 0; s < 2; ++s) kf[st][s] = *reinterpret_cast<const bf16x8*>(kb_ + frag_lane[s]);
         }
-        // S^T[key 16st + 4g + rr][query fr]
-#pragma unroll
-        for (int st = 0; st < 4; ++st) {
-          f32x4 a = (f32x4){0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-          for (int s = 0; s < 2; ++s) a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[st][s], qu[s], a, 0, 0, 0);
-          S[t][st] = a;
-        }
-        const int kb0 = p_base - i0 - 15 + j0;
-        // band subtile 0 of tile t is subtile 4 of tile t - 1 (P rows kb0 .. kb0 + 15, 64 rows on):
-        // carried in registers (tiles past key_hi are skipped only at the end, so tile t - 1 ran)
-        const bool carry = t > 0 && reuse_band;
-        if (diag != 2) {
-#pragma unroll
-          for (int pt = 0; pt < 5; ++pt) {
-            if (pt == 0 && carry) continue;
-            const char* pb_ = pl + (kb0 + 16 * pt) * 128;
-#pragma unroll
-            for (int s = 0; s < 2; ++s) pf[pt][s] = *reinterpret_cast<const bf16x8*>(pb_ + frag_lane[s]);
-          }
-        }
         // band^T[P row kb0 + 16pt + 4g + rr][query fr], pt = 0..4 (80 rows for 64 keys + 15 skew); the
         // two 32-key halves use subtiles 0-2 and 2-4 -> scratch[query][band pos] (16 x 48 bf16 per wave)
         f32x4 band[5];
-        if (diag != 2) {
 #pragma unroll
-          for (int pt = 0; pt < 5; ++pt) {
-            if (pt == 0 && carry) {
-              band[0] = band_next;
-              continue;
-            }
-            f32x4 a = (f32x4){0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int s = 0; s < 2; ++s) a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pf[pt][s], qv[s], a, 0, 0, 0);
-            band[pt] = a;
-          }
-          band_next = band[4];
-        }
-#pragma unroll
-        for (int hh = 0; hh < 2; ++hh) {
-          if (diag == 2) {   // timing experiment: no band / skew
-#pragma unroll
-            for (int st2 = 0; st2 < 2; ++st2)
-#pragma unroll
-              for (int rr = 0; rr < 4; ++rr) {
-                const int st = 2 * hh + st2;
-                const int j = j0 + 32 * hh + 16 * st2 + 4 * g + rr;
-                float sv = S[t][st][rr];
-                if (j < key_lo || j >= key_hi) sv = -INFINITY;
-                S[t][st][rr] = sv;
-                mx = fmaxf(mx, sv);
-              }
+        for (int pt = 0; pt < 5; ++pt) {
+          if (pt == 0 && carry) {
+            band[0] = band_next;
             continue;
           }
+          f32x4 a = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int s = 0; s < 2; ++s) a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pf[pt][s], qv[s], a, 0, 0, 0);
+          band[pt] = a;
+        }
+        band_next = band[4];
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
 #pragma unroll
           for (int pt = 0; pt < 3; ++pt) {
             const f32x4 a = band[2 * hh + pt];
@@ -473,7 +447,7 @@ __global__ __launch_bounds__(512, 1) void chunk_attention_ring_kernel(
             const unsigned lo = pack_bf16x2_a(a[0], a[1]), hi = pack_bf16x2_a(a[2], a[3]);
             asm volatile("ds_write_b64 %0, %1" ::"v"(waddr), "v"((u32x2_a){lo, hi}) : "memory");
           }
-          // score(query fr, key j0+32hh+16st2+4g+rr) += band[fr][16st2 + 4g + rr + 15 - fr]
+          // band of (query fr, key j0+32hh+16st2+4g+rr) = scratch[fr][16st2 + 4g + rr + 15 - fr]
           typedef bf16 bf16x4 __attribute__((ext_vector_type(4)));
           bf16x4 bdv4[2];
 #pragma unroll
@@ -483,32 +457,32 @@ __global__ __launch_bounds__(512, 1) void chunk_attention_ring_kernel(
                          : "v"(scr_base + 2u * (unsigned)(fr * (SCR_PITCH - 1) + 16 + 16 * st2 + 4 * g))
                          : "memory");
           asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(bdv4[0]), "+v"(bdv4[1])::"memory");
-          if (need_mask) {
+          // S^T[key 16st + 4g + rr][query fr] = band + K.(q+u)
 #pragma unroll
-            for (int st2 = 0; st2 < 2; ++st2) {
-              const int st = 2 * hh + st2;
+          for (int st2 = 0; st2 < 2; ++st2) {
+            const int st = 2 * hh + st2;
+            f32x4 a = (f32x4){(float)bdv4[st2][0], (float)bdv4[st2][1], (float)bdv4[st2][2], (float)bdv4[st2][3]};
 #pragma unroll
-              for (int rr = 0; rr < 4; ++rr) {
-                const int jj = 16 * st2 + 4 * g + rr;
-                float sv = S[t][st][rr] + (float)bdv4[st2][rr];
-                const int j = j0 + 32 * hh + jj;
-                if (j < key_lo || j >= key_hi) sv = -INFINITY;
-                S[t][st][rr] = sv;
-                mx = fmaxf(mx, sv);
-              }
-            }
-          } else {
-#pragma unroll
-            for (int st2 = 0; st2 < 2; ++st2) {
-              const int st = 2 * hh + st2;
-#pragma unroll
-              for (int rr = 0; rr < 4; ++rr) {
-                const float sv = S[t][st][rr] + (float)bdv4[st2][rr];
-                S[t][st][rr] = sv;
-                mx = fmaxf(mx, sv);
-              }
-            }
+            for (int s = 0; s < 2; ++s) a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[st][s], qu[s], a, 0, 0, 0);
+            S[t][st] = a;
           }
+        }
+        if (need_mask) {
+#pragma unroll
+          for (int st = 0; st < 4; ++st)
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr) {
+              const int j = j0 + 16 * st + 4 * g + rr;
+              float sv = S[t][st][rr];
+              if (j < key_lo || j >= key_hi) sv = -INFINITY;
+              S[t][st][rr] = sv;
+              mx = fmaxf(mx, sv);
+            }
+        } else {
+#pragma unroll
+          for (int st = 0; st < 4; ++st)
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr) mx = fmaxf(mx, S[t][st][rr]);
         }
       }
       // ---- exact softmax per query (lanes fr, fr+16, fr+32, fr+48 share a query)
