@@ -709,15 +709,7 @@ __global__ __launch_bounds__(512, 1) void full_attention_bf16_kernel(
         for (int st = 0; st < 4; ++st) S[t][st] = (f32x4){-INFINITY, -INFINITY, -INFINITY, -INFINITY};
         continue;
       }
-#pragma unroll
-      for (int st = 0; st < 4; ++st) {
-        f32x4 a = (f32x4){0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int s = 0; s < 2; ++s)
-          a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-              *reinterpret_cast<const bf16x8*>(kr + (j0 + 16 * st) * 128 + frag_lane[s]), qu[s], a, 0, 0, 0);
-        S[t][st] = a;
-      }
+      // the band first; its skewed values are the C operand of the score MFMAs (no VALU add)
       f32x4 band[5];
 #pragma unroll
       for (int pt = 0; pt < 5; ++pt) {
@@ -755,9 +747,14 @@ __global__ __launch_bounds__(512, 1) void full_attention_bf16_kernel(
 #pragma unroll
         for (int st2 = 0; st2 < 2; ++st2) {
           const int st = 2 * hh + st2;
+          f32x4 a = (f32x4){(float)bdv4[st2][0], (float)bdv4[st2][1], (float)bdv4[st2][2], (float)bdv4[st2][3]};
+#pragma unroll
+          for (int s = 0; s < 2; ++s)
+            a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                *reinterpret_cast<const bf16x8*>(kr + (j0 + 16 * st) * 128 + frag_lane[s]), qu[s], a, 0, 0, 0);
 #pragma unroll
           for (int rr = 0; rr < 4; ++rr) {
-            float sv = S[t][st][rr] + (float)bdv4[st2][rr];
+            float sv = a[rr];
             if (tmask && j0 + 32 * hh + 16 * st2 + 4 * g + rr >= key_hi) sv = -INFINITY;
             S[t][st][rr] = sv;
             mx = fmaxf(mx, sv);
