@@ -490,21 +490,20 @@ __global__ __launch_bounds__(512, 1) void chunk_attention_ring_kernel(
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
       if (mx == -INFINITY) mx = 0.f;   // fully masked query: every p = 0, output 0 (reference: NaN -> 0)
       const float mxl = mx * 1.4426950408889634f;
-      float l = 0.f;
 #pragma unroll
       for (int t = 0; t < 5; ++t)
 #pragma unroll
         for (int st = 0; st < 4; ++st)
 #pragma unroll
-          for (int rr = 0; rr < 4; ++rr) {
-            const float p = __builtin_amdgcn_exp2f(fmaf(S[t][st][rr], 1.4426950408889634f, -mxl));
-            S[t][st][rr] = p;
-            l += p;
-          }
-      l += __shfl_xor(l, 16, 64);
-      l += __shfl_xor(l, 32, 64);
-      // ---- O^T[dim 16nt + 4g + rr][query fr] = sum_keys V^T . P^T (key order permuted, same for both)
-      f32x4 O[4];
+          for (int rr = 0; rr < 4; ++rr) S[t][st][rr] = __builtin_amdgcn_exp2f(fmaf(S[t][st][rr], 1.4426950408889634f, -mxl));
+      // ---- O^T[dim 16nt + 4g + rr][query fr] = sum_keys V^T . P^T (key order permuted, same for both);
+      // the softmax denominator as a fifth MFMA against a constant "ones" row (row 0 of an A
+      // fragment held in registers): l = sum over keys of the bf16 p the numerator uses, and no
+      // VALU add per score
+      f32x4 O[4], Ol = (f32x4){0.f, 0.f, 0.f, 0.f};
+      const bf16 one_or_zero = (bf16)(fr == 0 ? 1.f : 0.f);
+      const bf16x8 ones = (bf16x8){one_or_zero, one_or_zero, one_or_zero, one_or_zero,
+                                   one_or_zero, one_or_zero, one_or_zero, one_or_zero};
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt) O[nt] = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -529,8 +528,11 @@ __global__ __launch_bounds__(512, 1) void chunk_attention_ring_kernel(
             const bf16x8 va = (bf16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
             O[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va, pb, O[nt], 0, 0, 0);
           }
+          Ol = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pb, Ol, 0, 0, 0);
         }
       }
+      // row 0 of Ol^T (query fr) sits in register 0 of lane fr (g = 0)
+      const float l = __shfl(Ol[0], fr, 64);
       const int qi = i0 + fr;
       const bool live = qi < q_valid && l > 0.f;
       const float inv = live ? 1.f / l : 0.f;
