@@ -299,7 +299,8 @@ int frontend_conv0_dw(const float* feats, const int32_t* meta, int meta_stride, 
   if (T2 <= 0 || d % FE_CG) return (int)hipErrorInvalidValue;
   const dim3 grid((T2 + FE_T2_TILE - 1) / FE_T2_TILE, nwin);
   if constexpr (std::is_same<T, bf16>::value) {
-    if (d % 64) return (int)hipErrorInvalidValue;
+    // one window's dw1 output is addressed by 32-bit byte offsets (buffer stores)
+    if (d % 64 || (size_t)T2 * FE_F2 * d * sizeof(bf16) >= ((size_t)1 << 31)) return (int)hipErrorInvalidValue;
     hipLaunchKernelGGL(fe_conv0_dw_mfma_kernel, dim3((T2 * FE_F2 + FE_POS_BLOCK - 1) / FE_POS_BLOCK, nwin), dim3(256),
                        0, st, feats, meta, meta_stride, W, T2, cmvn_mean, cmvn_istd, wpack, d, out);
   } else {
