@@ -150,6 +150,21 @@ def committed_traffic(cls: str = "ffn_w1_gemm"):
         return None, None
 
 
+def committed_mfma_busy(cls: str = "ffn_w1_gemm"):
+    """MFMA busy fraction and effective clock of the roofline kernel from the newest committed PMC
+    summary (profiles/<round>_mfma_busy.json, tools/profile_round.sh: GRBM_GUI_ACTIVE +
+    SQ_VALU_MFMA_BUSY_CYCLES over this same workload); (None, None, None) if absent."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_mfma_busy.json")))
+    if not files:
+        return None, None, None
+    try:
+        ent = json.load(open(files[-1]))["kernels"].get(cls)
+        return ((ent["mfma_busy"], ent["clock_ghz"], os.path.relpath(files[-1], ROOT)) if ent else (None, None, None))
+    except (OSError, ValueError, KeyError):
+        return None, None, None
+
+
 def apply_opts(enc, opts):
     for kv in opts:
         k, v = kv.split("=")
@@ -263,6 +278,7 @@ def main():
     # GPU); other row counts report null rather than a number measured on a different launch size
     profiled = args.dtype == "bf16" and not sharded and world == 1 and n_chunks == 2845
     traffic, traffic_src = committed_traffic(roof_cls) if profiled else (None, None)
+    busy, busy_clk, busy_src = committed_mfma_busy(roof_cls) if profiled else (None, None, None)
     step_flops = n_chunks * flops_per_chunk(LARGE) + LARGE.num_blocks * 2 * (L + 2 * C + R - 1) * LARGE.d_model ** 2
 
     # ---- CTC head + the collectives (timed separately; not part of `value`)
@@ -341,7 +357,12 @@ def main():
                          "measured_mfma_ceiling": MEASURED_BF16_CEILING if args.dtype == "bf16" else None,
                          "frac_of_measured_ceiling": (round(achieved / MEASURED_BF16_CEILING, 4)
                                                       if achieved and args.dtype == "bf16" else None),
-                         "hipblaslt_same_shape_tflops": HIPBLASLT_W1 if args.dtype == "bf16" else None},
+                         "hipblaslt_same_shape_tflops": HIPBLASLT_W1 if args.dtype == "bf16" else None,
+                         # PMC: fraction of cycles the MFMA pipes were busy during this kernel, and the
+                         # clock the chip held (GRBM_GUI_ACTIVE / 8 XCDs / duration), from the committed pass
+                         "mfma_busy_pmc": busy if profiled else None,
+                         "clock_ghz_pmc": busy_clk if profiled else None,
+                         "mfma_busy_source": busy_src if profiled else None},
             "step_tflops_algorithmic": round(step_flops / (dt_max / args.steps) / 1e12, 1),
             "ctc_ms": round(ctc_ms, 3),
             "allgather_ids_ms": round(gather_ms, 3) if gather_ms is not None else None,
