@@ -42,6 +42,9 @@ constexpr int WST_DEPTH = WST_NSLOT - 1;         // steps in flight ahead of the
 #ifndef WSP_LGKM
 #define WSP_LGKM 1   // 0: every K-step closes with lgkmcnt(0) (re-seed reads waited at once)
 #endif
+#ifndef WSP_FULLROW
+#define WSP_FULLROW 1   // 0: permlane-swapped 64-B row pieces stored per step (A/B)
+#endif
 #define WST_VMCNT(N) asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory")
 
 // acc += W-fragment (AGPR, "a") x A-fragment (VGPR): the 256 weight registers per lane live in the
@@ -92,9 +95,18 @@ CFM_DEV void sfor(F&& f) {
 // store on odd s), 2 re-seeds.
 template <int ACT>
 constexpr int wsp_half() { return (ACT == ACT_SILU ? 20 : ACT == ACT_RELU ? 4 : 0) + 2; }
+// Full-row stores (non-GLU, WSP_FULLROW): per half q the activation ops, 2 packs, one ds_write_b64
+// of the 4 packed columns into the wave's 16 x 64 staging tile, the re-seed; an odd group then
+// reads the tile back as full 128-B rows (2 x ds_read_b128: rows 0-7, 8-15) and the next (even)
+// group stores them first thing (its step opened with lgkmcnt(0)).  2H + 4 ops either way.
+// Used where it measured faster (one-process A/B, tools/gemm_bench.py): QKV 285 -> 251 us,
+// out-proj / pw2 91 -> 89 us; the SiLU (FFN w1) and ReLU (front-end pw) epilogues are issue-bound
+// and got 3-5% slower with the extra ds_write per half, so they keep the swapped 64-B pieces.
+template <int EPI, int ACT>
+constexpr bool wsp_fullrow() { return WSP_FULLROW && (EPI == EPI_QKV || (EPI == EPI_STORE && ACT == ACT_NONE)); }
 template <int EPI, int ACT>
 constexpr int wsp_nops(int s) {
-  return EPI == EPI_GLU ? ((s & 1) ? 27 : 24) : 2 * wsp_half<ACT>() + 5;
+  return EPI == EPI_GLU ? ((s & 1) ? 27 : 24) : wsp_fullrow<EPI, ACT>() ? 2 * wsp_half<ACT>() + 6 : 2 * wsp_half<ACT>() + 5;
 }
 constexpr int wsp_lo(int i, int n) { return (i * n + 31) / 32; }   // first op of gap i
 constexpr int wsp_gap(int o, int n) {                                  // gap that carries op o
@@ -108,7 +120,9 @@ constexpr int wsp_gap(int o, int n) {                                  // gap th
 template <int EPI, int ACT>
 constexpr int wsp_late_seeds(int s) {
   const int n = wsp_nops<EPI, ACT>(s), H = wsp_half<ACT>() + 1;
-  const int o0 = EPI == EPI_GLU ? 22 : H - 1, o1 = EPI == EPI_GLU ? 23 : 2 * H - 1;
+  const int fb = (s & 1) ? 0 : 2;   // full-row: even groups open with the 2 deferred stores
+  const int o0 = EPI == EPI_GLU ? 22 : wsp_fullrow<EPI, ACT>() ? fb + H : H - 1;
+  const int o1 = EPI == EPI_GLU ? 23 : wsp_fullrow<EPI, ACT>() ? fb + 2 * H + 1 : 2 * H - 1;
   return (wsp_gap(o0, n) >= 14) + (wsp_gap(o1, n) >= 14);
 }
 }  // namespace
@@ -118,7 +132,9 @@ __global__ __launch_bounds__(256, 1) void gemm_wsp_kernel(const bf16* __restrict
                                                           const bf16* __restrict__ W, int ldw, int M, int N,
                                                           EpiArgs ep) {
   // A ring + the block's 256 bias values (the re-seed reads them straight into the accumulators)
-  __shared__ __attribute__((aligned(16))) char smem[WST_NSLOT * WST_SLOT + 1024];
+  // + per wave a 16-row x 64-column bf16 output staging tile (144-B rows) for full-row stores
+  constexpr int STG_PITCH = 144, STG_BYTES = 16 * STG_PITCH;
+  __shared__ __attribute__((aligned(16))) char smem[WST_NSLOT * WST_SLOT + 1024 + 4 * STG_BYTES];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int fr = lane & 15, g = lane >> 4;
@@ -203,6 +219,11 @@ __global__ __launch_bounds__(256, 1) void gemm_wsp_kernel(const bf16* __restrict
   unsigned voffS[2];
 #pragma unroll
   for (int p = 0; p < 2; ++p) voffS[p] = (unsigned)(fr * old[p] + lcol) * 2;
+  // full-row stores: lane -> row (lane >> 3) (+ 8), 16-B chunk (lane & 7) of the wave's 64 columns
+  // (contiguous in the output: obase[1] = obase[0] + 32 for STORE and for QKV with dk % 64 == 0)
+  unsigned voffF[2];
+#pragma unroll
+  for (int b = 0; b < 2; ++b) voffF[b] = (unsigned)(((lane >> 3) + 8 * b) * old[0] + 8 * (lane & 7)) * 2;
   if constexpr (DIAG == 7) {   // timing only (wrong layout): every store 8 full 128-B rows
 #pragma unroll
     for (int p = 0; p < 2; ++p) voffS[p] = (unsigned)(((fr & 7) + 8 * p) * old[p] - 32 * p + ((fr >> 3) * 4 + g) * 8) * 2;
@@ -220,6 +241,11 @@ __global__ __launch_bounds__(256, 1) void gemm_wsp_kernel(const bf16* __restrict
 
   // lane's bias f32x4 of n-block nb at bias_lds + 64 nb
   const unsigned bias_lds = lds_base + WST_NSLOT * WST_SLOT + (unsigned)(wv * 64 + 4 * g) * 4;
+  // staging tile: write (row fr, columns 32p + 16q + 4g ..), read (row lane >> 3 (+ 8), chunk lane & 7)
+  const unsigned stg = lds_base + WST_NSLOT * WST_SLOT + 1024 + (unsigned)wv * STG_BYTES;
+  const unsigned stg_w = stg + (unsigned)(fr * STG_PITCH + 8 * g);
+  const unsigned stg_r = stg + (unsigned)((lane >> 3) * STG_PITCH + 16 * (lane & 7));
+  u32x4 rowv[2] = {(u32x4){0u, 0u, 0u, 0u}, (u32x4){0u, 0u, 0u, 0u}};   // full rows read back, stored next group
   f32x4 acc[2][4][4];
   bf16x8 afr[2][4][2];
 #pragma unroll
@@ -258,7 +284,12 @@ __global__ __launch_bounds__(256, 1) void gemm_wsp_kernel(const bf16* __restrict
                                                   rows * old[p] * 2, 0x00020000);
     return sd;
   };
-  auto epi_op = [&](auto Sc, auto Oc, f32x4(&a)[4][4], const StoreD& sd, auto RSc) {
+  auto epi_op = [&](auto Sc, auto Oc, f32x4(&a)[4][4], const StoreD& sd, const StoreD& sdp, auto RSc) {
+    (void)stg_w;   // named outside the if-constexpr branches: clang's implicit capture in generic lambdas
+    (void)stg_r;
+    (void)voffF;
+    (void)rowv;
+    (void)sdp;
     constexpr int S = decltype(Sc)::value, O = decltype(Oc)::value;
     constexpr bool RESEED = decltype(RSc)::value;
     constexpr float NL2E = -1.4426950408889634f;
@@ -312,7 +343,7 @@ __global__ __launch_bounds__(256, 1) void gemm_wsp_kernel(const bf16* __restrict
       } else {   // O == 26
         store(0, jj);
       }
-    } else {
+    } else if constexpr (!wsp_fullrow<EPI, ACT>()) {
       // ops: per half q (one 16-column n-block) H - 2 activation ops, 2 packs and the re-seed of
       // that n-block's accumulator (dead after the packs), then 2 swaps and the store
       constexpr int p = S & 1, jj = S >> 1;   // the two 64-B halves of a 128-B row piece in consecutive steps
@@ -341,14 +372,55 @@ __global__ __launch_bounds__(256, 1) void gemm_wsp_kernel(const bf16* __restrict
       } else {   // O == 2H + 2
         store(p, jj);
       }
+    } else {
+      // full rows: even S opens with the 2 stores of the previous (odd) group's rows, then per half
+      // q (n-block 2p + q): activation ops, 2 packs, the ds_write_b64 into the staging tile, the
+      // re-seed; odd S closes with the 2 full-row reads
+      constexpr int p = S & 1, jj = S >> 1;
+      constexpr int H = wsp_half<ACT>() + 1;
+      constexpr int base = p ? 0 : 2;
+      if constexpr (p == 0 && O < 2) {
+        constexpr int jp = (S + 7) % 8 >> 1;   // rows of group S - 1 (S = 0: the previous tile's last)
+        if constexpr (!RESEED) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // drain: no step waits
+        if constexpr (DIAG != 5)
+          __builtin_amdgcn_raw_buffer_store_b128(rowv[O], (S == 0 ? sdp : sd).d[0],
+                                                 voffF[O] + (unsigned)(16 * jp * old[0] * 2), 0, 0);
+      } else if constexpr (O >= base && O < base + 2 * (H + 1)) {
+        constexpr int q = (O - base) / (H + 1), o = (O - base) % (H + 1);
+        auto val = [&](int i) -> float { return a[2 * p + q][jj][i]; };
+        if constexpr (o == H) {
+          seed(std::integral_constant<int, 2 * p + q>{}, jj);
+        } else if constexpr (DIAG == 3) {
+        } else if constexpr (o < H - 3) {
+          if constexpr (ACT == ACT_SILU) {
+            chain(o, val, val);
+          } else {
+            et[o] = fmaxf(val(o), 0.f);
+            pin(et[o]);
+          }
+        } else if constexpr (o < H - 1) {
+          constexpr int k = o - (H - 3);   // pack k of this half: values 2k, 2k+1
+          if constexpr (ACT == ACT_NONE) epk[2 * q + k] = pack_bf16x2(val(2 * k), val(2 * k + 1));
+          else epk[2 * q + k] = pack_bf16x2(et[2 * k], et[2 * k + 1]);
+          pin(epk[2 * q + k]);
+        } else {   // o == H - 1: 4 packed columns -> staging tile
+          typedef unsigned u32x2_w __attribute__((ext_vector_type(2)));
+          asm volatile("ds_write_b64 %0, %1 offset:%2" ::"v"(stg_w), "v"((u32x2_w){epk[2 * q], epk[2 * q + 1]}),
+                       "i"(64 * p + 32 * q) : "memory");
+        }
+      } else if constexpr (p == 1 && O >= 2 * H + 2) {
+        constexpr int b = O - (2 * H + 2);   // rows 8b .. 8b + 7 as full 128-B rows
+        if constexpr (DIAG != 3)
+          asm volatile("ds_read_b128 %0, %1 offset:%2" : "+v"(rowv[b]) : "v"(stg_r), "i"(b * 8 * STG_PITCH) : "memory");
+      }
     }
   };
 
-  // one 64-row tile into acc[BUF]; the gaps drain acc[1 - BUF] (tile rtp, stores below row lim)
-  auto tile = [&](auto BUFc, int rt, int rtp, int lim) {
+  // one 64-row tile into acc[BUF]; the gaps drain acc[1 - BUF] (store descriptor sd: tile rtp's
+  // rows below lim; sdp: the previously drained tile, whose last rows the full-row path stores here)
+  auto tile = [&](auto BUFc, int rt, const StoreD& sd, const StoreD& sdp) {
     constexpr int BUF = decltype(BUFc)::value;
     const __amdgpu_buffer_rsrc_t dA1 = tile_rsrc(rt + 1), dA2 = tile_rsrc(rt + 2);
-    const StoreD sd = store_rsrc(rtp, lim);
     sfor<0, WST_NK>([&](auto KSc) {
       constexpr int KS = decltype(KSc)::value;
       constexpr int slot_n = (8 * BUF + KS + 1) % WST_NSLOT;          // next step's slot (read)
@@ -359,7 +431,7 @@ __global__ __launch_bounds__(256, 1) void gemm_wsp_kernel(const bf16* __restrict
       // barrier, every wave's pieces of it; every wave is also past its reads of slot y-1, which
       // the DMA below refills
       if constexpr (DIAG != 2 && DIAG != 4) WST_VMCNT(26);
-      asm volatile("s_barrier" ::: "memory");
+      if constexpr (DIAG != 10) asm volatile("s_barrier" ::: "memory");
       bf16x8(&cur)[4][2] = afr[KS & 1];
       bf16x8(&nxt)[4][2] = afr[(KS + 1) & 1];
       sfor<0, 32>([&](auto Ic) {
@@ -374,11 +446,12 @@ __global__ __launch_bounds__(256, 1) void gemm_wsp_kernel(const bf16* __restrict
           issue_piece(KS == 0 ? dA1 : dA2, std::integral_constant<int, i == 22 ? 1 : 0>{},
                       std::integral_constant<int, (KS + WST_DEPTH) % WST_NK>{},
                       std::integral_constant<int, slot_d>{});
-        sfor<wsp_lo(i, n_ops), wsp_lo(i + 1, n_ops)>([&](auto Oc) { epi_op(KSc, Oc, acc[1 - BUF], sd, std::true_type{}); });
+        sfor<wsp_lo(i, n_ops), wsp_lo(i + 1, n_ops)>([&](auto Oc) { epi_op(KSc, Oc, acc[1 - BUF], sd, sdp, std::true_type{}); });
         __builtin_amdgcn_sched_barrier(0);
       });
       constexpr int late = wsp_late_seeds<EPI, ACT>(KS);
-      if constexpr (KS == WST_NK - 1 || late == 0 || !WSP_LGKM)
+      // (full-row: an odd group's row reads are the step's last LDS ops and the next group stores them)
+      if constexpr (KS == WST_NK - 1 || late == 0 || !WSP_LGKM || (wsp_fullrow<EPI, ACT>() && (KS & 1)))
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       else if constexpr (late == 1)
         asm volatile("s_waitcnt lgkmcnt(1)" ::: "memory");
@@ -386,13 +459,23 @@ __global__ __launch_bounds__(256, 1) void gemm_wsp_kernel(const bf16* __restrict
         asm volatile("s_waitcnt lgkmcnt(2)" ::: "memory");
     });
   };
-  auto drain = [&](f32x4(&a)[4][4], int rt) {
+  auto drain = [&](f32x4(&a)[4][4], int rt, const StoreD& sdp) {
     const StoreD sd = store_rsrc(rt, M);
     asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");   // last MFMA writes -> VALU reads
     sfor<0, 8>([&](auto Sc) {
       constexpr int S = decltype(Sc)::value;
-      sfor<0, wsp_nops<EPI, ACT>(S)>([&](auto Oc) { epi_op(Sc, Oc, a, sd, std::false_type{}); });
+      sfor<0, wsp_nops<EPI, ACT>(S)>([&](auto Oc) { epi_op(Sc, Oc, a, sd, sdp, std::false_type{}); });
     });
+    return sd;
+  };
+  // the full-row path's last pending rows (group 7 of the last drained tile, descriptor sd)
+  auto flush_rows = [&](const StoreD& sd) {
+    if constexpr (wsp_fullrow<EPI, ACT>() && DIAG != 5) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+        __builtin_amdgcn_raw_buffer_store_b128(rowv[b], sd.d[0], voffF[b] + (unsigned)(16 * 3 * old[0] * 2), 0, 0);
+    }
   };
 
   // prologue: weights in AGPRs (s_nop: AGPR writes -> MFMA reads), step 0 landed, its fragments read
@@ -415,14 +498,19 @@ __global__ __launch_bounds__(256, 1) void gemm_wsp_kernel(const bf16* __restrict
   // tiles in pairs (acc[0], acc[1]); an odd count runs one dummy tile past the block's range whose
   // results are never stored (lim = 0 in the drain), which keeps one straight loop body
   const int npair = (r1 - r0 + 1) >> 1;
+  // the first tile's gaps drain a fake previous tile: rows of a REAL tile (never negative, so the
+  // store descriptors' row bases stay inside the output) with lim = 0, i.e. zero-record stores
+  StoreD sd_prev = store_rsrc(r0, 0);
   for (int it = 0; it < npair; ++it) {
     const int rt = r0 + 2 * it;
-    // the first tile's gaps drain a fake previous tile: rows of a REAL tile (never negative, so the
-    // store descriptors' row bases stay inside the output) with lim = 0, i.e. zero-record stores
-    tile(std::integral_constant<int, 0>{}, rt, it > 0 ? rt - 1 : rt, it > 0 ? M : 0);
-    tile(std::integral_constant<int, 1>{}, rt + 1, rt, M);
+    const StoreD sd0 = store_rsrc(it > 0 ? rt - 1 : rt, it > 0 ? M : 0);
+    tile(std::integral_constant<int, 0>{}, rt, sd0, sd_prev);
+    const StoreD sd1 = store_rsrc(rt, M);
+    tile(std::integral_constant<int, 1>{}, rt + 1, sd1, sd0);
+    sd_prev = sd1;
   }
-  if (((r1 - r0) & 1) == 0) drain(acc[1], r1 - 1);
+  if (((r1 - r0) & 1) == 0) flush_rows(drain(acc[1], r1 - 1, sd_prev));
+  else flush_rows(sd_prev);   // odd count: the last tile call drained the last real tile
   // the pieces issued past the end land (and the drain's seed reads return) before the
   // workgroup's LDS is released
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
@@ -444,7 +532,7 @@ static int launch_wst(const bf16* A, int lda, const bf16* W, int ldw, int M, int
 #ifdef CFM_GEMM_DIAG
   // DIAG (timing experiments only, diagnostic builds, model option "gemm_diag"): 1 = no MFMAs,
   // 2 = no DMA wait (stale LDS), 3 = no epilogue (re-seeds only), 4 = no DMA in the loop (stale LDS),
-  // 5 = no stores, 7 = full-line stores (wrong layout)
+  // 5 = no stores, 7 = full-line stores (wrong layout), 10 = no per-step barrier (wrong results)
   switch (ep.diag) {
     case 1: WSP_LAUNCH(1); break;
     case 2: WSP_LAUNCH(2); break;
@@ -452,9 +540,10 @@ static int launch_wst(const bf16* A, int lda, const bf16* W, int ldw, int M, int
     case 4: WSP_LAUNCH(4); break;
     case 5: WSP_LAUNCH(5); break;
     case 7: WSP_LAUNCH(7); break;
+    case 10: WSP_LAUNCH(10); break;
     default: break;
   }
-  if (ep.diag >= 1 && ep.diag <= 7 && ep.diag != 6) {
+  if ((ep.diag >= 1 && ep.diag <= 7 && ep.diag != 6) || ep.diag == 10) {
     CFM_CHECK_LAUNCH();
     return 0;
   }
