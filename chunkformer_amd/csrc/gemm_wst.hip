@@ -45,6 +45,9 @@ constexpr int WST_DEPTH = WST_NSLOT - 1;         // steps in flight ahead of the
 #ifndef WSP_FULLROW
 #define WSP_FULLROW 1   // 0: permlane-swapped 64-B row pieces stored per step (A/B)
 #endif
+#ifndef WSP_FULLROW_ACT
+#define WSP_FULLROW_ACT 0   // 1: also the SiLU / ReLU epilogues (A/B)
+#endif
 #define WST_VMCNT(N) asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory")
 
 // acc += W-fragment (AGPR, "a") x A-fragment (VGPR): the 256 weight registers per lane live in the
@@ -100,10 +103,13 @@ constexpr int wsp_half() { return (ACT == ACT_SILU ? 20 : ACT == ACT_RELU ? 4 : 
 // reads the tile back as full 128-B rows (2 x ds_read_b128: rows 0-7, 8-15) and the next (even)
 // group stores them first thing (its step opened with lgkmcnt(0)).  2H + 4 ops either way.
 // Used where it measured faster (one-process A/B, tools/gemm_bench.py): QKV 285 -> 251 us,
-// out-proj / pw2 91 -> 89 us; the SiLU (FFN w1) and ReLU (front-end pw) epilogues are issue-bound
-// and got 3-5% slower with the extra ds_write per half, so they keep the swapped 64-B pieces.
+// out-proj / pw2 91 -> 89 us; the SiLU (FFN w1, N = 2048) and ReLU (front-end pw, N = 512)
+// epilogues measured 2-6% slower with it (WSP_FULLROW_ACT=1), so they keep the swapped 64-B pieces
+// (the same ReLU epilogue at N = 2048 gains 12%: the wider the layer, the more the store shape counts).
 template <int EPI, int ACT>
-constexpr bool wsp_fullrow() { return WSP_FULLROW && (EPI == EPI_QKV || (EPI == EPI_STORE && ACT == ACT_NONE)); }
+constexpr bool wsp_fullrow() {
+  return WSP_FULLROW && (EPI == EPI_QKV || (EPI == EPI_STORE && (ACT == ACT_NONE || WSP_FULLROW_ACT)));
+}
 template <int EPI, int ACT>
 constexpr int wsp_nops(int s) {
   return EPI == EPI_GLU ? ((s & 1) ? 27 : 24) : wsp_fullrow<EPI, ACT>() ? 2 * wsp_half<ACT>() + 6 : 2 * wsp_half<ACT>() + 5;
@@ -120,9 +126,11 @@ constexpr int wsp_gap(int o, int n) {                                  // gap th
 template <int EPI, int ACT>
 constexpr int wsp_late_seeds(int s) {
   const int n = wsp_nops<EPI, ACT>(s), H = wsp_half<ACT>() + 1;
-  const int fb = (s & 1) ? 0 : 2;   // full-row: even groups open with the 2 deferred stores
-  const int o0 = EPI == EPI_GLU ? 22 : wsp_fullrow<EPI, ACT>() ? fb + H : H - 1;
-  const int o1 = EPI == EPI_GLU ? 23 : wsp_fullrow<EPI, ACT>() ? fb + 2 * H + 1 : 2 * H - 1;
+  // full-row: even groups open with the 2 deferred stores (seeds at 2 + H, 2H + 3); odd groups
+  // end with the 2 row reads and then both seeds (2H + 2, 2H + 3)
+  const bool fr = wsp_fullrow<EPI, ACT>();
+  const int o0 = EPI == EPI_GLU ? 22 : fr ? ((s & 1) ? 2 * H + 2 : H + 2) : H - 1;
+  const int o1 = EPI == EPI_GLU ? 23 : fr ? 2 * H + 3 : 2 * H - 1;
   return (wsp_gap(o0, n) >= 14) + (wsp_gap(o1, n) >= 14);
 }
 }  // namespace
@@ -373,22 +381,24 @@ __global__ __launch_bounds__(256, 1) void gemm_wsp_kernel(const bf16* __restrict
         store(p, jj);
       }
     } else {
-      // full rows: even S opens with the 2 stores of the previous (odd) group's rows, then per half
-      // q (n-block 2p + q): activation ops, 2 packs, the ds_write_b64 into the staging tile, the
-      // re-seed; odd S closes with the 2 full-row reads
+      // full rows.  even S: the 2 stores of the previous (odd) group's rows, then per half q
+      // (n-block 2p + q) the activation ops, 2 packs, the ds_write_b64 into the staging tile and
+      // the re-seed.  odd S: per half the activation ops, packs and write, then the 2 full-row
+      // reads, then both re-seeds -- the reads are older than any re-seed, so the step's closing
+      // lgkmcnt(late) (re-seeds left in flight) covers them
       constexpr int p = S & 1, jj = S >> 1;
       constexpr int H = wsp_half<ACT>() + 1;
-      constexpr int base = p ? 0 : 2;
+      constexpr int base = p ? 0 : 2, per = p ? H : H + 1;   // ops per half
       if constexpr (p == 0 && O < 2) {
         constexpr int jp = (S + 7) % 8 >> 1;   // rows of group S - 1 (S = 0: the previous tile's last)
         if constexpr (!RESEED) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // drain: no step waits
         if constexpr (DIAG != 5)
           __builtin_amdgcn_raw_buffer_store_b128(rowv[O], (S == 0 ? sdp : sd).d[0],
                                                  voffF[O] + (unsigned)(16 * jp * old[0] * 2), 0, 0);
-      } else if constexpr (O >= base && O < base + 2 * (H + 1)) {
-        constexpr int q = (O - base) / (H + 1), o = (O - base) % (H + 1);
+      } else if constexpr (O >= base && O < base + 2 * per) {
+        constexpr int q = (O - base) / per, o = (O - base) % per;
         auto val = [&](int i) -> float { return a[2 * p + q][jj][i]; };
-        if constexpr (o == H) {
+        if constexpr (o == H) {   // even S only
           seed(std::integral_constant<int, 2 * p + q>{}, jj);
         } else if constexpr (DIAG == 3) {
         } else if constexpr (o < H - 3) {
@@ -408,10 +418,12 @@ __global__ __launch_bounds__(256, 1) void gemm_wsp_kernel(const bf16* __restrict
           asm volatile("ds_write_b64 %0, %1 offset:%2" ::"v"(stg_w), "v"((u32x2_w){epk[2 * q], epk[2 * q + 1]}),
                        "i"(64 * p + 32 * q) : "memory");
         }
-      } else if constexpr (p == 1 && O >= 2 * H + 2) {
-        constexpr int b = O - (2 * H + 2);   // rows 8b .. 8b + 7 as full 128-B rows
+      } else if constexpr (p == 1 && O < 2 * H + 2) {
+        constexpr int b = O - 2 * H;   // rows 8b .. 8b + 7 as full 128-B rows
         if constexpr (DIAG != 3)
           asm volatile("ds_read_b128 %0, %1 offset:%2" : "+v"(rowv[b]) : "v"(stg_r), "i"(b * 8 * STG_PITCH) : "memory");
+      } else if constexpr (p == 1) {   // O = 2H + 2, 2H + 3: re-seeds of both halves
+        seed(std::integral_constant<int, 2 * p + (O - (2 * H + 2))>{}, jj);
       }
     }
   };
@@ -450,8 +462,7 @@ __global__ __launch_bounds__(256, 1) void gemm_wsp_kernel(const bf16* __restrict
         __builtin_amdgcn_sched_barrier(0);
       });
       constexpr int late = wsp_late_seeds<EPI, ACT>(KS);
-      // (full-row: an odd group's row reads are the step's last LDS ops and the next group stores them)
-      if constexpr (KS == WST_NK - 1 || late == 0 || !WSP_LGKM || (wsp_fullrow<EPI, ACT>() && (KS & 1)))
+      if constexpr (KS == WST_NK - 1 || late == 0 || !WSP_LGKM)
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       else if constexpr (late == 1)
         asm volatile("s_waitcnt lgkmcnt(1)" ::: "memory");
