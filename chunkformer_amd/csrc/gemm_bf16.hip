@@ -191,49 +191,6 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_256_kernel(const bf16* __res
   if (grp == 0) asm volatile("s_barrier" ::: "memory");
 }
 
-// =====================================================================================
-// Ring variant: 5-slot LDS ring of K = 32 half-steps, buffer_load ... lds staging.
-//
-//   * a slot = A [256][32] + W [256][32] bf16 = 32 KiB; 5 slots = the CU's 160 KiB.  Each
-//     wave stages 2 + 2 KiB of a slot (4 `buffer_load_dwordx4 ... lds`), four slots ahead of
-//     the one being read, so three slots (96 KiB) stay in flight across barriers: Little's law
-//     on the per-CU DMA rate, which capped the 3+2-slot K = 64 ring (gemm_bf16_256_kernel);
-//   * DMA addressing is fixed per lane (a 32-bit voffset per operand block), the K step is
-//     the scalar soffset and the tile the descriptor base: no per-step VALU address math.
-//     Rows past M fall outside the A descriptor's range and read as 0;
-//   * LDS image of a [256][32] operand: row r at 64 r bytes, 16-B chunk c at position
-//     c ^ f((r >> 2) & 3), f(q) = (4 - q) & 3: every ds_read_b128 lane group of a 16-row
-//     fragment read covers the 64 banks once (conflict free); the DMA pre-swizzles the
-//     per-lane SOURCE chunk (LDS destination stays lane-linear);
-//   * same two ping-pong wave groups, tile walk, swapped-operand accumulators and tile
-//     epilogue as gemm_bf16_256_kernel; the bias seeds the accumulators through scalar loads
-//     (lgkmcnt), so the vector-memory counter only ever holds DMA and epilogue stores and
-//     every wait is a counted vmcnt (never a drain in the steady state).
-// =====================================================================================
-typedef int i32x4_t __attribute__((ext_vector_type(4)));
-
-// bias of this wave's 64 columns -> accumulator seeds; col0 wave-uniform
-CFM_DEV void seed_bias_smem(f32x4 (&acc)[4][8], const float* bias, int col0, int g) {
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    f32x4 b = (f32x4){0.f, 0.f, 0.f, 0.f};
-    if (bias) {
-      const float* bp = bias + col0 + 16 * i;
-      i32x4_t s0, s1, s2, s3;
-      asm volatile("s_load_dwordx4 %0, %4, 0x0\n\ts_load_dwordx4 %1, %4, 0x10\n\t"
-                   "s_load_dwordx4 %2, %4, 0x20\n\ts_load_dwordx4 %3, %4, 0x30\n\ts_waitcnt lgkmcnt(0)"
-                   : "=&s"(s0), "=&s"(s1), "=&s"(s2), "=&s"(s3)
-                   : "s"(bp)
-                   : "memory");
-      const i32x4_t lo = (g & 1) ? s1 : s0, hi = (g & 1) ? s3 : s2;
-      const i32x4_t v = (g & 2) ? hi : lo;
-      b = __builtin_bit_cast(f32x4, v);
-    }
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = b;
-  }
-}
-
 template <int EPI, int ACT>
 static int launch256(const bf16* A, int lda, const bf16* W, int ldw, int M, int N, int K, const EpiArgs& ep,
                      hipStream_t st) {
