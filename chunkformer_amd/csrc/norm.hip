@@ -5,7 +5,9 @@
 // a row is one coalesced 16/32-B-per-lane load.  Statistics are two-pass in
 // registers (mean, then mean of squared deviations = torch's biased variance).
 // `layernorm2` fuses norm_final of layer i with the first pre-norm of layer i+1
-// (or with after_norm): the row is read once and written twice.
+// (or with after_norm): the row is read once and written twice.  Row stores are non-temporal:
+// measured in the full step (one-process A/B) 52.8 -> 52.4 ms, LayerNorms 8.86 -> 8.74 ms, and the
+// GEMMs that read h next got faster too (FFN w1 9.28 -> 9.15, QKV 3.13 -> 3.06 ms).
 #include "cfm_common.h"
 #include "cfm_kernels.h"
 
@@ -54,7 +56,9 @@ CFM_DEV void store_row(float* p, const float (&v)[VPL]) {
     *reinterpret_cast<f32x2*>(p) = (f32x2){v[0], v[1]};
   } else {
 #pragma unroll
-    for (int e = 0; e < VPL; e += 4) *reinterpret_cast<f32x4*>(p + e) = (f32x4){v[e], v[e + 1], v[e + 2], v[e + 3]};
+    for (int e = 0; e < VPL; e += 4) {
+      __builtin_nontemporal_store((f32x4){v[e], v[e + 1], v[e + 2], v[e + 3]}, reinterpret_cast<f32x4*>(p + e));
+    }
   }
 }
 template <int VPL>
@@ -63,8 +67,10 @@ CFM_DEV void store_row(bf16* p, const float (&v)[VPL]) {
     *reinterpret_cast<bf16x2*>(p) = (bf16x2){(bf16)v[0], (bf16)v[1]};
   } else {
 #pragma unroll
-    for (int e = 0; e < VPL; e += 4)
-      *reinterpret_cast<bf16x4*>(p + e) = (bf16x4){(bf16)v[e], (bf16)v[e + 1], (bf16)v[e + 2], (bf16)v[e + 3]};
+    for (int e = 0; e < VPL; e += 4) {
+      __builtin_nontemporal_store((bf16x4){(bf16)v[e], (bf16)v[e + 1], (bf16)v[e + 2], (bf16)v[e + 3]},
+                                  reinterpret_cast<bf16x4*>(p + e));
+    }
   }
 }
 
