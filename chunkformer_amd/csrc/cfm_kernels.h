@@ -41,8 +41,10 @@ struct Tuning {
   int conv_dot2 = 1;             // conv module: bf16 dot2 kernel (0: per-tap f32 kernel)
   int conv_dma = 1;              // conv module: LDS-DMA window staging (0: register staging)
   int dw2_seg = 4;               // front-end dw2: row segments per walk
-  // GEMM sites whose bf16 outputs are stored non-temporally ("nt_sites" bit mask, SITE_* below)
-  int nt_sites = 0;
+  // GEMM sites whose bf16 outputs are stored non-temporally ("nt_sites" bit mask, SITE_* below).
+  // Default: FFN w2 (its y goes straight to the LayerNorm; bench A/B 52.2 -> 51.4 ms/step); nt on
+  // the front-end pointwise outputs (+0.45 ms) or FFN w1's hidden (w1 slower) measured worse.
+  int nt_sites = 8;   // SITE_FFN2
   void apply(EpiArgs& e, int site = 0) const {
     e.diag = gemm_diag;
     e.wst = gemm_wst;

@@ -392,9 +392,10 @@ __global__ __launch_bounds__(256, 1) void gemm_wsp_kernel(const bf16* __restrict
       if constexpr (p == 0 && O < 2) {
         constexpr int jp = (S + 7) % 8 >> 1;   // rows of group S - 1 (S = 0: the previous tile's last)
         if constexpr (!RESEED) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // drain: no step waits
+        constexpr int aux = DIAG == 8 ? 2 : DIAG == 9 ? 16 : 0;   // store policy as in `store`
         if constexpr (DIAG != 5)
           __builtin_amdgcn_raw_buffer_store_b128(rowv[O], (S == 0 ? sdp : sd).d[0],
-                                                 voffF[O] + (unsigned)(16 * jp * old[0] * 2), 0, 0);
+                                                 voffF[O] + (unsigned)(16 * jp * old[0] * 2), 0, aux);
       } else if constexpr (O >= base && O < base + 2 * per) {
         constexpr int q = (O - base) / per, o = (O - base) % per;
         auto val = [&](int i) -> float { return a[2 * p + q][jj][i]; };
@@ -485,7 +486,8 @@ __global__ __launch_bounds__(256, 1) void gemm_wsp_kernel(const bf16* __restrict
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
       for (int b = 0; b < 2; ++b)
-        __builtin_amdgcn_raw_buffer_store_b128(rowv[b], sd.d[0], voffF[b] + (unsigned)(16 * 3 * old[0] * 2), 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(rowv[b], sd.d[0], voffF[b] + (unsigned)(16 * 3 * old[0] * 2), 0,
+                                               DIAG == 8 ? 2 : DIAG == 9 ? 16 : 0);
     }
   };
 
