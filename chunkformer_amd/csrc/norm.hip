@@ -45,7 +45,7 @@ CFM_DEV void load_row(const float* p, float (&v)[VPL]) {
   } else {
 #pragma unroll
     for (int e = 0; e < VPL; e += 4) {
-      const f32x4 t = *reinterpret_cast<const f32x4*>(p + e);
+      const f32x4 t = *reinterpret_cast<const f32x4*>(p + e);   // (non-temporal here: LayerNorms +0.8 ms)
       v[e] = t[0]; v[e + 1] = t[1]; v[e + 2] = t[2]; v[e + 3] = t[3];
     }
   }
@@ -82,7 +82,8 @@ CFM_DEV void load_row(const bf16* p, float (&v)[VPL]) {
   } else {
 #pragma unroll
     for (int e = 0; e < VPL; e += 4) {
-      const bf16x4 t = *reinterpret_cast<const bf16x4*>(p + e);
+      // the branch outputs y are read once, here: non-temporal (A/B: LayerNorms 8.59 -> 8.14 ms/step)
+      const bf16x4 t = __builtin_nontemporal_load(reinterpret_cast<const bf16x4*>(p + e));
       v[e] = (float)t[0]; v[e + 1] = (float)t[1]; v[e + 2] = (float)t[2]; v[e + 3] = (float)t[3];
     }
   }
