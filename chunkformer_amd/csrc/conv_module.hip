@@ -278,7 +278,8 @@ CFM_DEV void conv_dot2_rows(const bf16* __restrict__ win, int nout, int out_row0
       const float y = (acc[r][e] - mean) * rstd * lw[e] + lb[e];
       o[e] = (bf16)(y * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-1.4426950408889634f * y)));
     }
-    *reinterpret_cast<bvec*>(out + (size_t)(out_row0 + i0 + r) * d + c0) = o;
+    // non-temporal: read once, by pw2 (A/B x3: this kernel 1.72 -> 1.66 ms/step, pw2 1.13 -> 1.09)
+    __builtin_nontemporal_store(o, reinterpret_cast<bvec*>(out + (size_t)(out_row0 + i0 + r) * d + c0));
   }
 }
 
