@@ -1,6 +1,11 @@
 """Benchmark: audio-frames/s through the ChunkFormer encoder (masked batch) on MI355X.
 
-    python bench.py --gpus N --steps K --warmup W            (N>1: launched by torch.distributed.run)
+    python bench.py --gpus N --steps K --warmup W
+
+N > 1: either launched by `python -m torch.distributed.run --nproc-per-node N bench.py --gpus N`
+(WORLD_SIZE must equal N, else the run exits non-zero), or started plainly, in which case bench.py
+starts that torch.distributed.run itself as a child process before any GPU call, relays its
+output and exits with its return code.
 
 Workload: chunkformer-large (12 layers, d=512, 8 heads, ff=2048, conv k=15,
 V=5000) with seeded synthetic weights, synthetic N(0,1) 80-dim fbank, utterance lengths
@@ -22,11 +27,12 @@ host packer (C++ planner) + plan upload + front-end + 12 blocks + after_norm, wi
 the features already resident in HBM.  value = all ranks' fbank frames / max-over-
 ranks step time.
 
-roofline: the dominant kernel is the FFN (bf16 MFMA): the fused w_2 . SiLU(w_1 . x) kernel
-(2 x 2 x 64N x 512 x 2048 FLOP per launch), or the w_1 GEMM on the two-GEMM path; its
-per-launch time is measured live with HIP events on the launch stream (libcfm in-stream
-profiler) over the timed steps.  cpu_baseline: the CPU oracle
-(oracle/encoder_ref.py, torch fp32) on a bounded sample of the same workload.
+roofline: the dominant kernel is the FFN w_1 GEMM with its fused bias + SiLU epilogue
+(2 x 64N x 512 x 2048 FLOP per launch); its per-launch time is measured live with HIP events on
+the launch stream (libcfm in-stream profiler) over the timed steps.  end_to_end_ms: the same step
+plus the fused CTC ids head and, at N > 1, the ids all-gather (max over ranks).  cpu_baseline:
+the CPU oracle (oracle/encoder_ref.py, torch fp32) on a bounded sample of the same workload, and
+on one 30 s utterance (configs[0]).
 """
 from __future__ import annotations
 
@@ -130,9 +136,21 @@ def cpu_baseline(lens_all, budget_s: float = 12.0):
         t_tot += time.perf_counter() - t0
         frames += sum(grp)
         groups += 1
-    return {"value": round(frames / t_tot, 1), "unit": "audio-frames/s", "cores": threads, "kind": "port",
+    # configs[0]: one 30 s utterance (3000 frames, 6 chunks) through the same oracle call
+    x1 = synthetic_features([3000], 999)
+    ref.forward_parallel_chunk(sd, LARGE, x1, [3000], C, L, R)   # untimed first call
+    t1, reps = 0.0, 0
+    while t1 < 3.0 and reps < 20:
+        c0 = time.perf_counter()
+        ref.forward_parallel_chunk(sd, LARGE, x1, [3000], C, L, R)
+        t1 += time.perf_counter() - c0
+        reps += 1
+    return {"value": round(frames / t_tot, 1), "unit": "audio-frames/s", "cores": threads, "cpu": model,
+            "kind": "port",
             "sample": f"{groups} masked-batch calls of the oracle (oracle/encoder_ref.py, torch fp32 CPU) over the "
-                      f"workload's first utterances (capped at 60k frames each), {frames} frames in {t_tot:.1f} s"}
+                      f"workload's first utterances (capped at 60k frames each), {frames} frames in {t_tot:.1f} s",
+            "config1_30s_utterance": {"value": round(3000 * reps / t1, 1), "unit": "audio-frames/s",
+                                      "ms_per_utterance": round(t1 / reps * 1e3, 1), "reps": reps}}
 
 
 def committed_traffic(cls: str = "ffn_w1_gemm"):
@@ -171,6 +189,33 @@ def apply_opts(enc, opts):
         enc.set_option(k, int(v, 0))
 
 
+def spawn_ranks(n: int) -> int:
+    """--gpus N > 1 without a torchrun environment: run `python -m torch.distributed.run
+    --nproc-per-node N bench.py <same args>` as a child process (this process has not touched the
+    GPU), its rank 0 printing the JSON line on the inherited stdout; returns its exit code."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *sys.argv[1:]]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+def model_config(heads: int):
+    """chunkformer-large (8 heads, BASELINE configs) or its 4-head d=512 variant (head_dim 128,
+    the reference's shipped recipes, examples/asr/rnnt/conf/chunkformer-rnnt-large-vie.yaml:5-6)."""
+    from chunkformer_amd.config import LARGE_4H
+    if heads == 8:
+        return LARGE
+    if heads == 4:
+        return LARGE_4H
+    raise SystemExit("--heads must be 8 or 4")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -195,24 +240,39 @@ def main():
     ap.add_argument("--batch", type=int, default=256, help="full: utterances of T=3000 frames")
     ap.add_argument("--opt", action="append", default=[], metavar="KEY=VALUE",
                     help="per-model kernel option (cfm_model_set_option), A/B runs only")
+    ap.add_argument("--heads", type=int, default=8, choices=[8, 4],
+                    help="attention heads of the d=512 model: 8 (chunkformer-large, BASELINE) or 4 (head_dim 128, "
+                         "the reference's shipped d=512 recipes)")
     args = ap.parse_args()
+    env_world = int(os.environ.get("WORLD_SIZE", "0") or 0)
+    if env_world == 0 and args.gpus > 1:
+        if args.config in ("endless", "full", "fbank"):
+            raise SystemExit(f"--config {args.config} runs on one GPU")
+        sys.exit(spawn_ranks(args.gpus))
+    if env_world and env_world != args.gpus:
+        raise SystemExit(f"WORLD_SIZE={env_world} but --gpus {args.gpus}: launch one rank per GPU")
     if args.config in ("endless", "full"):
         return bench_single(args)
     if args.config == "fbank":
         return bench_fbank(args)
 
     rank, world, local = init_from_env()
-    local = local % torch.cuda.device_count()   # (rehearsal of several ranks on one GPU: gloo backend)
+    ndev = torch.cuda.device_count()
+    if world > ndev and (os.environ.get("CFM_DIST_BACKEND") or "nccl") == "nccl":
+        raise SystemExit(f"{world} ranks but {ndev} GPU(s): RCCL needs one GPU per rank "
+                         "(CFM_DIST_BACKEND=gloo rehearses several ranks on one GPU)")
+    local = local % ndev   # (rehearsal of several ranks on one GPU: gloo backend)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     sharded = args.config == "sharded" or (args.config == "auto" and world > 1)
     minutes = args.minutes if args.minutes is not None else (980.0 if sharded else 240.0)
+    cfg = model_config(args.heads)
     if sharded:   # configs[2]: one batch of `minutes` over all ranks
         lens_all = workload_lengths(int(minutes * 60 * 100), seed=0)
-        shards = plan_shards(lens_all, world, C, L, R, LARGE.num_blocks)
+        shards = plan_shards(lens_all, world, C, L, R, cfg.num_blocks)
     else:         # configs[1]: `minutes` per rank, whole utterances LPT-placed
         lens_all = workload_lengths(int(minutes * 60 * 100) * world, seed=0)
-        shards = plan_shards(lens_all, world, C, L, R, LARGE.num_blocks, split=False)
+        shards = plan_shards(lens_all, world, C, L, R, cfg.num_blocks, split=False)
     mine = shards[rank]
     # features: utterance u from its own seed, so every rank sees the same audio for u
     need = sorted({p.utt for p in mine})
@@ -227,7 +287,7 @@ def main():
     real_frames = sum((lens_all[p.utt] if p.k1 == chunks_of(lens_all[p.utt], C) else p.k1 * 8 * C) - p.k0 * 8 * C
                       for p in mine)
 
-    enc = ChunkFormerEncoder(LARGE, synthetic_state_dict(LARGE, 0), device=dev, dtype=args.dtype)
+    enc = ChunkFormerEncoder(cfg, synthetic_state_dict(cfg, 0), device=dev, dtype=args.dtype)
     apply_opts(enc, args.opt)
 
     def step():
@@ -263,7 +323,7 @@ def main():
     # ---- dominant kernel: the FFN (fused kernel, or its w_1 GEMM on the two-GEMM path);
     # per-launch time from in-stream HIP events on the launch stream (libcfm profiler)
     rows = n_chunks * C
-    d_, ff_ = LARGE.d_model, LARGE.ffn_dim
+    d_, ff_ = cfg.d_model, cfg.ffn_dim
     roof_cls = "ffn_w1_gemm"
     roof_name = ("ffn_w1_gemm (gemm_wsp_kernel<EPI_STORE,SiLU>: K=512 weight-stationary bf16 MFMA)"
                  if args.dtype == "bf16" else "ffn_w1_gemm (gemm_kernel<float,EPI_STORE,SiLU>)")
@@ -276,10 +336,10 @@ def main():
     peak = PEAK_TFLOPS[args.dtype]
     # the committed PMC traffic was collected on the default workload (configs[1], 2,845 chunks on one
     # GPU); other row counts report null rather than a number measured on a different launch size
-    profiled = args.dtype == "bf16" and not sharded and world == 1 and n_chunks == 2845
+    profiled = args.dtype == "bf16" and not sharded and world == 1 and n_chunks == 2845 and args.heads == 8
     traffic, traffic_src = committed_traffic(roof_cls) if profiled else (None, None)
     busy, busy_clk, busy_src = committed_mfma_busy(roof_cls) if profiled else (None, None, None)
-    step_flops = n_chunks * flops_per_chunk(LARGE) + LARGE.num_blocks * 2 * (L + 2 * C + R - 1) * LARGE.d_model ** 2
+    step_flops = n_chunks * flops_per_chunk(cfg) + cfg.num_blocks * 2 * (L + 2 * C + R - 1) * cfg.d_model ** 2
 
     # ---- CTC head + the collectives (timed separately; not part of `value`)
     enc_out = out[0]
@@ -290,11 +350,10 @@ def main():
     torch.cuda.synchronize()
     ctc_ms = (time.perf_counter() - tc) * 1e3
     gather_ms = gather_lp_ms = None
+    # the kept rows of every piece, in shard order (the layout gather_* expects)
+    starts = torch.tensor([0] + list(out[2][:-1])).cumsum(0) * C
+    idx = torch.cat([torch.arange(int(s) + p.skip, int(s) + p.skip + p.rows) for s, p in zip(starts, mine)]).to(dev)
     if world > 1:
-        # the kept rows of every piece, in shard order (the layout gather_* expects)
-        starts = torch.tensor([0] + list(out[2][:-1])).cumsum(0) * C
-        idx = torch.cat([torch.arange(int(s) + p.skip, int(s) + p.skip + p.rows) for s, p in zip(starts, mine)])
-        idx = idx.to(dev)
         flat = ids.reshape(-1).index_select(0, idx)
         dist.barrier()
         torch.cuda.synchronize()
@@ -303,7 +362,7 @@ def main():
         torch.cuda.synchronize()
         gather_ms = (time.perf_counter() - tg) * 1e3
         if sharded and not args.no_gather_logp:
-            logp, _ = enc.ctc_log_softmax(enc_out.reshape(-1, LARGE.d_model).index_select(0, idx), want_logp=True,
+            logp, _ = enc.ctc_log_softmax(enc_out.reshape(-1, cfg.d_model).index_select(0, idx), want_logp=True,
                                           want_ids=False)
             dist.barrier()
             torch.cuda.synchronize()
@@ -312,6 +371,29 @@ def main():
             torch.cuda.synchronize()
             gather_lp_ms = (time.perf_counter() - tg) * 1e3
             del logp
+    del out, enc_out, ids
+
+    # ---- end to end: the step + the fused CTC ids head + (N > 1) the ids all-gather with the
+    # per-utterance reassembly on every rank; K steps between barriers, max over ranks
+    def e2e():
+        o = step()
+        _, ids_ = enc.ctc_log_softmax(o[0], want_logp=False)
+        if world > 1:
+            gather_ids(ids_.reshape(-1).index_select(0, idx), shards, lens_all)
+        return ids_
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        e2e()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    te = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(te, op=dist.ReduceOp.MAX)
+    e2e_ms = float(te.item()) / args.steps * 1e3
 
     breakdown = None
     if not args.no_breakdown:
@@ -342,6 +424,7 @@ def main():
                                     f"configs[1]: masked batch, {minutes:g} min of audio per GPU (log-uniform 1 s-30 "
                                     f"min utterances, seed 0), forward_parallel_chunk C=64 L=128 R=128"),
                        "config_index": 2 if sharded else 1,
+                       "heads": cfg.n_heads, "head_dim": cfg.head_dim,
                        "pieces_rank0": len(mine), "chunks_rank0": n_chunks, "frames_total": int(total_frames),
                        "parallelism": f"dp{world} ({'plan_shards: LPT pieces, halo cuts' if sharded else 'LPT utterance sharding'})"},
             "roofline": {"bound": "mfma", "kernel": roof_name,
@@ -366,6 +449,10 @@ def main():
             "step_tflops_algorithmic": round(step_flops / (dt_max / args.steps) / 1e12, 1),
             "ctc_ms": round(ctc_ms, 3),
             "allgather_ids_ms": round(gather_ms, 3) if gather_ms is not None else None,
+            "end_to_end_ms": round(e2e_ms, 3),
+            "end_to_end_value": round(total_frames / (e2e_ms / 1e3), 1),
+            "end_to_end_note": ("encoder step + fused CTC ids head" +
+                                (" + ids all_gather_into_tensor and per-utterance reassembly" if world > 1 else "")),
             "allgather_logp_bf16_ms": round(gather_lp_ms, 3) if gather_lp_ms is not None else None,
             "breakdown_ms": breakdown,
         }

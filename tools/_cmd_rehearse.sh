@@ -1,7 +1,10 @@
 # Rehearsal of the N-rank bench on ONE GPU (both ranks share cuda:0, gloo collectives on host
-# copies): exercises plan_shards, the per-rank encoder runs and the ids / log-prob gathers.
+# copies): a plain `bench.py --gpus 2` starts torch.distributed.run itself (bench.spawn_ranks),
+# which exercises plan_shards, the per-rank encoder runs, the ids / log-prob gathers and the
+# end-to-end timing.  The numbers are NOT a scaling measurement (two ranks share one GPU).
 set -e
 R=$GRAFT_REPO_ROOT
+mkdir -p $R/gpurun_out
 export CFM_DIST_BACKEND=gloo
-timeout -k 10 400 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 $R/bench.py --gpus 2 --steps 2 --warmup 1 --minutes 120 --no-cpu-baseline > $R/gpurun_out/rehearse2.log 2>&1
-tail -1 $R/gpurun_out/rehearse2.log | cut -c1-1200
+timeout -k 10 400 python3 $R/bench.py --gpus 2 --steps 2 --warmup 1 --no-cpu-baseline > $R/gpurun_out/rehearse2.log 2>&1
+grep '^{' $R/gpurun_out/rehearse2.log | tail -1 | cut -c1-1500
