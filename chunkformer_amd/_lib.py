@@ -59,6 +59,7 @@ cfm_model_create = _sig("cfm_model_create", I32, ctypes.POINTER(CfmConfig), ctyp
 cfm_model_destroy = _sig("cfm_model_destroy", None, P)
 cfm_model_set_option = _sig("cfm_model_set_option", I32, P, ctypes.c_char_p, I64)
 cfm_plan_masked = _sig("cfm_plan_masked", I32, P, P, I32, I32, I32, I32, P, P, PI32, P, PI64)
+cfm_plan_masked_ex = _sig("cfm_plan_masked_ex", I32, P, P, P, I32, I32, I32, I32, P, P, PI32, P, PI64)
 cfm_plan_padded = _sig("cfm_plan_padded", I32, P, I32, I32, I32, I32, I32, PI32, P, PI64)
 cfm_plan_stream = _sig("cfm_plan_stream", I32, I32, I32, I32, I32, I32, PI32, P, PI64)
 cfm_workspace_bytes_stream = _sig("cfm_workspace_bytes_stream", SZ, P, I32, I32, I32, I32)
@@ -87,17 +88,29 @@ cfm_fbank_create = _sig("cfm_fbank_create", I32, ctypes.POINTER(CfmFbankConfig),
 cfm_fbank_destroy = _sig("cfm_fbank_destroy", None, P)
 cfm_fbank_num_frames = _sig("cfm_fbank_num_frames", I64, P, I64)
 cfm_fbank_compute = _sig("cfm_fbank_compute", I32, P, P, I64, P, P)
+# RNN-T greedy search (include/cfm.h)
+class CfmRnntConfig(ctypes.Structure):
+    _fields_ = [("vocab", I32), ("enc_dim", I32), ("embed_size", I32), ("hidden", I32), ("num_layers", I32),
+                ("pred_out", I32), ("join_dim", I32), ("blank", I32)]
+
+
+cfm_rnnt_create = _sig("cfm_rnnt_create", I32, ctypes.POINTER(CfmRnntConfig), ctypes.POINTER(CfmTensorView), I32, I32,
+                       ctypes.POINTER(P))
+cfm_rnnt_destroy = _sig("cfm_rnnt_destroy", None, P)
+cfm_rnnt_workspace_bytes = _sig("cfm_rnnt_workspace_bytes", SZ, P, I32)
+cfm_rnnt_greedy = _sig("cfm_rnnt_greedy", I32, P, P, I32, P, P, I32, I32, P, P, SZ, P)
 # include/cfm_ops.h
 cfm_op_gemm = _sig("cfm_op_gemm", I32, I32, I32, I32, P, I32, P, I32, I32, I32, I32, P, ctypes.c_float, P, I32, I32, P,
                    I32, P, I32, P, I32, P)
 EXPORTED_OPS = ["cfm_op_gemm"]
 
 EXPORTED = ["cfm_version", "cfm_last_error", "cfm_model_create", "cfm_model_destroy", "cfm_model_set_option",
-            "cfm_plan_masked", "cfm_plan_padded", "cfm_workspace_bytes_masked", "cfm_workspace_bytes_padded",
+            "cfm_plan_masked", "cfm_plan_masked_ex", "cfm_plan_padded", "cfm_workspace_bytes_masked", "cfm_workspace_bytes_padded",
             "cfm_encode_masked", "cfm_encode_padded", "cfm_masks_from_plan", "cfm_profile_read", "cfm_ctc_workspace_bytes",
             "cfm_ctc_logprobs", "cfm_ctc_ids_workspace_bytes", "cfm_ctc_ids", "cfm_ctc_collapse",
             "cfm_plan_stream", "cfm_workspace_bytes_stream", "cfm_encode_stream",
-            "cfm_fbank_create", "cfm_fbank_destroy", "cfm_fbank_num_frames", "cfm_fbank_compute"]
+            "cfm_fbank_create", "cfm_fbank_destroy", "cfm_fbank_num_frames", "cfm_fbank_compute",
+            "cfm_rnnt_create", "cfm_rnnt_destroy", "cfm_rnnt_workspace_bytes", "cfm_rnnt_greedy"]
 
 
 def profile_read(h):
@@ -131,20 +144,22 @@ def ptr(t) -> int:
     return 0 if t is None else t.data_ptr()
 
 
-def plan_masked(lens, offsets, C: int, L: int, R: int):
-    """Host planner (no GPU): returns (plan int32 CPU tensor, n_chunks list, out_lens list)."""
+def plan_masked(lens, offsets, C: int, L: int, R: int, mask_lens=None):
+    """Host planner (no GPU): returns (plan int32 CPU tensor, n_chunks list, out_lens list).
+    lens: feature rows per utterance; mask_lens: xs_origin_lens when it differs (None = lens)."""
     B = len(lens)
     lens_t = torch.tensor([int(x) for x in lens], dtype=torch.int32)
+    ml_t = torch.tensor([int(x) for x in mask_lens], dtype=torch.int32) if mask_lens is not None else None
     offs_t = torch.tensor([int(x) for x in offsets], dtype=torch.int32) if offsets is not None else None
     nch = torch.zeros(B, dtype=torch.int32)
     olen = torch.zeros(B, dtype=torch.int32)
     total = I32(0)
     n = I64(0)
-    check(cfm_plan_masked(lens_t.data_ptr(), ptr(offs_t), B, C, L, R, nch.data_ptr(), olen.data_ptr(),
-                          ctypes.byref(total), None, ctypes.byref(n)))
+    check(cfm_plan_masked_ex(lens_t.data_ptr(), ptr(ml_t), ptr(offs_t), B, C, L, R, nch.data_ptr(), olen.data_ptr(),
+                             ctypes.byref(total), None, ctypes.byref(n)))
     plan = torch.zeros(n.value, dtype=torch.int32)
-    check(cfm_plan_masked(lens_t.data_ptr(), ptr(offs_t), B, C, L, R, None, None, ctypes.byref(total),
-                          plan.data_ptr(), ctypes.byref(n)))
+    check(cfm_plan_masked_ex(lens_t.data_ptr(), ptr(ml_t), ptr(offs_t), B, C, L, R, None, None, ctypes.byref(total),
+                             plan.data_ptr(), ctypes.byref(n)))
     return plan, nch.tolist(), olen.tolist()
 
 

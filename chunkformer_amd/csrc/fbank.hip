@@ -360,6 +360,7 @@ struct cfm_fbank {
   int *mel_lo = nullptr, *mel_off = nullptr;
   float* mel_w = nullptr;
   int device = 0;
+  int n_cu = 256;   // compute units of `device` (launch sizing)
 };
 
 namespace {
@@ -462,6 +463,8 @@ cfm_status cfm_fbank_create(const cfm_fbank_config* cfg, int32_t device, cfm_fba
   h->logm = logm;
   h->nbins = cfg->num_mel_bins;
   h->device = device;
+  if (hipDeviceGetAttribute(&h->n_cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || h->n_cu <= 0)
+    h->n_cu = 256;
   const int M = 1 << logm;
   std::vector<float> w = make_window(cfg->window_type, win);
   std::vector<float2> tw(M / 2), tw2(M / 2 + 1);
@@ -531,13 +534,10 @@ cfm_status cfm_fbank_compute(const cfm_fbank* h, const float* wave_dev, int64_t 
   if (!wave_dev || !out_dev) return set_error(CFM_ERR_VALUE, "fbank: null buffer");
   const int M = 1 << h->logm;
   const size_t lds = h->logm == 8 ? fbank512_lds(h->nbins, h->n_mel_w) : fbank_lds(M, h->shift, h->win, h->nbins, h->n_mel_w);
+  // the handle's device (its constants live there), whatever the caller's current device
+  if (hipSetDevice(h->device) != hipSuccess) return set_error(CFM_ERR_RUNTIME, "fbank: hipSetDevice");
   // persistent blocks (constants staged once each): three resident per CU for N = 512, else two
-  static int n_cu = 0;
-  if (!n_cu) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0) n_cu = 256;
-  }
+  const int n_cu = h->n_cu;
   const long long groups = (nf + cfm::FB - 1) / cfm::FB;
   const dim3 grid((unsigned)std::min<long long>(groups, (h->logm == 8 ? 3LL : 2LL) * n_cu));
   const hipStream_t st = (hipStream_t)stream;

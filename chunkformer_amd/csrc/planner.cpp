@@ -15,6 +15,7 @@
 // conv chunks of C over [7 cached | T'] with the right edge zero-padded (convolution.py:148-180).
 #include <algorithm>
 #include <cstring>
+#include <string>
 #include <vector>
 
 #include "../../include/cfm.h"
@@ -42,9 +43,14 @@ int calc_length(int T) {
 
 using namespace cfm;
 
-extern "C" cfm_status cfm_plan_masked(const int32_t* lens, const int32_t* offsets, int32_t B, int32_t C, int32_t L,
-                                      int32_t R, int32_t* n_chunks_out, int32_t* out_lens, int32_t* total_chunks,
-                                      int32_t* plan, int64_t* plan_n) {
+// rows[b]: feature rows of utterance b (x.size(0): padding, unfold and window validity,
+// encoder.py:556-564, 598); mask_lens[b] (NULL = rows): xs_origin_lens[b], which bounds the masks
+// and gives the output length (encoder.py:567-596, 673).  The reference builds one bound per
+// arange(0, 1 + (len + n_pad - 15) // 8, C) entry; a count different from the window count is its
+// shape-mismatch RuntimeError.
+extern "C" cfm_status cfm_plan_masked_ex(const int32_t* lens, const int32_t* mask_lens, const int32_t* offsets,
+                                         int32_t B, int32_t C, int32_t L, int32_t R, int32_t* n_chunks_out,
+                                         int32_t* out_lens, int32_t* total_chunks, int32_t* plan, int64_t* plan_n) {
   if (B <= 0 || !lens) return set_error(CFM_ERR_VALUE, "plan_masked: empty batch");
   if (C <= 0 || L < 0 || R < 0) return set_error(CFM_ERR_VALUE, "plan_masked: chunk_size must be > 0, contexts >= 0");
   const int size = (C - 1) * 8 + 15, step = 8 * C;
@@ -56,9 +62,19 @@ extern "C" cfm_status cfm_plan_masked(const int32_t* lens, const int32_t* offset
     if (T < 0) return set_error(CFM_ERR_VALUE, "plan_masked: negative length");
     const int n_pad = (T >= size) ? (int)floormod((int64_t)step - floormod(T - size, step), step) : size - T;
     nch[b] = (T + n_pad - size) / step + 1;
+    const int Tm = mask_lens ? mask_lens[b] : T;
+    if (mask_lens) {
+      const int64_t stop = 1 + floordiv((int64_t)Tm + n_pad - 15, 8);
+      const int64_t nb = stop > 0 ? (stop + C - 1) / C : 0;
+      if (nb != nch[b])
+        return set_error(CFM_ERR_RUNTIME, "plan_masked: utterance " + std::to_string(b) + ": " + std::to_string(T) +
+                                              " feature rows make " + std::to_string(nch[b]) +
+                                              " chunks but xs_origin_lens " + std::to_string(Tm) + " bounds " +
+                                              std::to_string(nb) + " (shape mismatch, encoder.py:567-612)");
+    }
     N += nch[b];
     if (n_chunks_out) n_chunks_out[b] = nch[b];
-    if (out_lens) out_lens[b] = calc_length(T);
+    if (out_lens) out_lens[b] = calc_length(Tm);
   }
   if (N * C >= (int64_t)1 << 31) return set_error(CFM_ERR_VALUE, "plan_masked: batch too large");
   const int rows = (int)(N * C);
@@ -82,7 +98,7 @@ extern "C" cfm_status cfm_plan_masked(const int32_t* lens, const int32_t* offset
   for (int b = 0; b < B; ++b) {
     const int T = lens[b];
     const int o = offsets ? offsets[b] : 0;
-    const int max_len = 1 + (int)floordiv(T - 15, 8);
+    const int max_len = 1 + (int)floordiv((mask_lens ? mask_lens[b] : T) - 15, 8);
     for (int c = 0; c < nch[b]; ++c, ++n) {
       int32_t* m = meta + n * PLAN_REC;
       const int base = C * c;
@@ -109,6 +125,12 @@ extern "C" cfm_status cfm_plan_masked(const int32_t* lens, const int32_t* offset
     src += T;
   }
   return CFM_OK;
+}
+
+extern "C" cfm_status cfm_plan_masked(const int32_t* lens, const int32_t* offsets, int32_t B, int32_t C, int32_t L,
+                                      int32_t R, int32_t* n_chunks_out, int32_t* out_lens, int32_t* total_chunks,
+                                      int32_t* plan, int64_t* plan_n) {
+  return cfm_plan_masked_ex(lens, nullptr, offsets, B, C, L, R, n_chunks_out, out_lens, total_chunks, plan, plan_n);
 }
 
 extern "C" cfm_status cfm_plan_padded(const int32_t* lens, int32_t B, int32_t T, int32_t C, int32_t L, int32_t R,

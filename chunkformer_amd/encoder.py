@@ -102,16 +102,15 @@ class ChunkFormerEncoder:
         dev = self.device
         if offset.shape[0] == 0:
             offset = torch.zeros(B, dtype=torch.long, device=xs_origin_lens.device)
-        lens = [int(t) for t in xs_origin_lens.tolist()]
-        for i, (x, t) in enumerate(zip(xs, lens)):
-            # the reference pads / unfolds on x.size(0) but bounds the masks by xs_origin_lens
-            # (encoder.py:556-580); the two only give consistent chunk and bound counts when equal
-            n = x.reshape(-1, self.cfg.input_dim).shape[0]
-            if n != t:
-                raise ValueError(f"xs[{i}] has {n} frames but xs_origin_lens[{i}] = {t}: forward_parallel_chunk "
-                                 "needs each utterance passed at its own length")
+        mask_lens = [int(t) for t in xs_origin_lens.tolist()]
+        if len(mask_lens) != B:
+            raise ValueError(f"{B} utterances but {len(mask_lens)} xs_origin_lens")
+        # the reference pads / unfolds x.size(0) rows (encoder.py:556-564) and bounds the masks and the
+        # output lengths by xs_origin_lens (567-596, 673); the planner takes both
+        lens = [x.reshape(-1, self.cfg.input_dim).shape[0] for x in xs]
         offs = [int(o) for o in offset.tolist()]
-        plan, n_chunks, out_lens = _lib.plan_masked(lens, offs, C, L, R)
+        plan, n_chunks, out_lens = _lib.plan_masked(lens, offs, C, L, R,
+                                                    mask_lens=None if lens == mask_lens else mask_lens)
         N = sum(n_chunks)
         d = self.cfg.d_model
         feats = torch.cat([x.to(dev, torch.float32).reshape(-1, self.cfg.input_dim) for x in xs], 0).contiguous()

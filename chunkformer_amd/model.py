@@ -16,6 +16,12 @@ CTC post-processing (remove_duplicates_and_blank and get_output_with_timestamps'
 split, chunkformer/utils/model_utils.py:23-221) runs on the device (cfm_ctc_collapse); only
 the id -> text mapping (class2str) and the hh:mm:ss:ms formatting stay on the host, so
 `char_dict` models return strings like the reference.
+
+`model: transducer` checkpoints (config.yaml, init_model.py:118-135) decode with the RNN-T greedy
+search on the device (transducer.py, cfm_rnnt_greedy) exactly where the reference calls
+optimized_search / batch_greedy_search (chunkformer_model.py:439-448, 533-543); their per-frame
+decisions [T, n_steps] go through get_output_with_timestamps' transducer branch (no collapse).
+`model: classification` checkpoints are out of scope and refused.
 """
 from __future__ import annotations
 
@@ -30,6 +36,7 @@ import torch
 from .config import EncoderConfig
 from .encoder import ChunkFormerEncoder
 from .streaming import EndlessGraphRunner
+from .transducer import RNNTConfig, RNNTGreedy
 
 Features = Union[torch.Tensor, np.ndarray, str]
 
@@ -77,6 +84,31 @@ def format_segments(segs, char_dict: Dict[int, str]) -> List[dict]:
     {"decode", "start", "end"} (model_utils.py:203-218: class2str(...).strip(), 80 ms frames)."""
     return [{"decode": class2str(toks, char_dict).strip(), "start": milliseconds_to_hhmmssms(st * 80),
              "end": milliseconds_to_hhmmssms(en * 80)} for toks, st, en in segs]
+
+
+def transducer_segments(dense, max_silence: int):
+    """get_output_with_timestamps (model_utils.py:174-221) for model_type "transducer": dense
+    per-frame decisions [T, n_steps] (0 = blank; a frame is silent when all are blank, its tokens
+    are the non-blank decisions in step order, no duplicate removal) -> [(tokens, start, end)] in
+    80 ms frames.  Walks the non-blank frames only (a blank run closes the sentence when it
+    reaches max_silence frames)."""
+    d = np.asarray(dense)
+    T = d.shape[0]
+    nbf = np.nonzero((d != 0).any(1))[0].tolist()
+    segs, toks, start, prev_end = [], [], -1, -1
+    for i, t in enumerate(nbf):
+        if start == -1:
+            start = max(math.ceil((t + prev_end) / 2), t - 2) if prev_end != -1 else max(t - 2, 0)
+        row = d[t]
+        toks.extend(int(v) for v in row[row != 0])
+        gap = (nbf[i + 1] if i + 1 < len(nbf) else T) - t - 1   # blank frames after t
+        end = t if max_silence == 0 else (t + max_silence if 0 < max_silence <= gap else -1)
+        if end != -1:
+            segs.append((toks, start, end))
+            prev_end, toks, start = end, [], -1
+    if start != -1 and toks:
+        segs.append((toks, start, T - 1))
+    return segs
 
 
 # ----------------------------------------------------------------------------- segment math
@@ -154,10 +186,18 @@ class ChunkFormerModel:
 
     def __init__(self, cfg: EncoderConfig, state_dict: Dict[str, torch.Tensor], dtype: str = "bf16", device=None,
                  char_dict: Optional[Dict[int, str]] = None, fbank_conf: Optional[dict] = None,
-                 resample_conf: Optional[dict] = None):
+                 resample_conf: Optional[dict] = None, model_type: str = "asr_model",
+                 rnnt_config: Optional[RNNTConfig] = None):
+        if model_type not in ("asr_model", "transducer"):
+            raise AssertionError(f"model: {model_type} is out of scope (asr_model / transducer decoders only)")
         self.config = cfg
+        self.model_type = model_type
         self.encoder = ChunkFormerEncoder(cfg, state_dict, device=device, dtype=dtype)
         self.device = self.encoder.device
+        self.rnnt = None
+        if model_type == "transducer":
+            rc = rnnt_config or RNNTConfig(vocab=cfg.vocab, enc_dim=cfg.d_model)
+            self.rnnt = RNNTGreedy(rc, state_dict, self.device)
         self.char_dict = char_dict
         self.fbank_conf = dict(fbank_conf or {})
         self.resample_conf = dict(resample_conf or {})
@@ -215,21 +255,24 @@ class ChunkFormerModel:
                     break
             else:
                 raise ValueError(f"No checkpoint found in {path}. Expected one of: {cands}")
+        # chunkformer_model.py:153-160, 91-100: GlobalCMVN exists exactly when the directory holds a
+        # global_cmvn file (whatever config.yaml's `cmvn` key says), JSON unless the config's top-level
+        # is_json_cmvn is false
         cmvn_path = os.path.join(path, "global_cmvn")
-        has_cmvn = conf.get("cmvn", None) == "global_cmvn"
+        has_cmvn = os.path.exists(cmvn_path)
         if has_cmvn:
-            if not os.path.exists(cmvn_path):
-                raise FileNotFoundError(f"config asks for global_cmvn but {cmvn_path} is missing")
-            is_json = bool((conf.get("cmvn_conf") or {}).get("is_json_cmvn", True))
+            is_json = bool(conf.get("is_json_cmvn", True))
             mean, istd = load_json_cmvn(cmvn_path) if is_json else load_kaldi_cmvn(cmvn_path)
             sd.setdefault("encoder.global_cmvn.mean", torch.tensor(mean, dtype=torch.float64).float())
             sd.setdefault("encoder.global_cmvn.istd", torch.tensor(istd, dtype=torch.float64).float())
         else:   # no GlobalCMVN module: checkpoint buffers would be unexpected keys (ignored)
             sd.pop("encoder.global_cmvn.mean", None)
             sd.pop("encoder.global_cmvn.istd", None)
+        model_type = conf.get("model", "asr_model")   # ChunkFormerConfig default (chunkformer_model.py:47-48)
         vocab = int(conf.get("output_dim", sd["ctc.ctc_lo.weight"].shape[0] if "ctc.ctc_lo.weight" in sd else 0))
         cfg = EncoderConfig.from_encoder_conf(conf.get("encoder_conf", {}), input_dim=int(conf.get("input_dim", 80)),
                                               output_dim=vocab, cmvn=has_cmvn)
+        rnnt_cfg = RNNTConfig.from_conf(conf, vocab, cfg.d_model) if model_type == "transducer" else None
         char_dict = None
         vp = os.path.join(path, "vocab.txt")
         if os.path.exists(vp):
@@ -241,7 +284,7 @@ class ChunkFormerModel:
                         raise AssertionError(f"bad vocab line {line!r}")
                     char_dict[int(arr[1])] = arr[0]
         return cls(cfg, sd, dtype=dtype, device=device, char_dict=char_dict, fbank_conf=conf.get("fbank_conf"),
-                   resample_conf=conf.get("resample_conf"))
+                   resample_conf=conf.get("resample_conf"), model_type=model_type, rnnt_config=rnnt_cfg)
 
     # ---------------------------------------------------------------- API
     def encode(self, xs: torch.Tensor, xs_lens: torch.Tensor, chunk_size: Optional[int] = None,
@@ -275,10 +318,12 @@ class ChunkFormerModel:
         xs_dev = xs.to(dev, torch.float32)
         ids, outs = [], []
         seg_len = max(stop - start for start, stop, _, _ in segs) if segs else 0
-        key = (C, L, R, trunc, seg_len, bool(return_encoder_out), bool(cuda_graph))
+        transducer = self.model_type == "transducer"
+        want_eo = bool(return_encoder_out) or transducer   # the RNN-T search consumes the encoder rows
+        key = (C, L, R, trunc, seg_len, want_eo, bool(cuda_graph))
         runner = self._endless_runners.get(key)
         if runner is None:   # graphs are captured once per segment geometry and reused across calls
-            runner = EndlessGraphRunner(enc, C, L, R, trunc, seg_len, return_encoder_out, use_graph=cuda_graph)
+            runner = EndlessGraphRunner(enc, C, L, R, trunc, seg_len, want_eo, use_graph=cuda_graph)
             self._endless_runners = {key: runner}
         runner.reset()
         offset = 0
@@ -293,6 +338,23 @@ class ChunkFormerModel:
         # the caches carried out of the last segment (r_att_cache / r_cnn_cache of its
         # forward_parallel_chunk call, chunkformer_model.py:407-417)
         self.last_endless_caches = (runner.att[runner.cur], runner.cnn[runner.cur])
+        if transducer:
+            # optimized_search over the concatenated encoder output (chunkformer_model.py:439-448):
+            # decisions [1, T, n_steps], text by get_output_with_timestamps' transducer branch
+            enc_all = torch.cat(outs) if outs else torch.zeros(0, cfg.d_model, device=dev)
+            T = enc_all.shape[0]
+            dense = self.rnnt.greedy_packed(enc_all, [0], [T])
+            tokens = dense.long().reshape(1, T, -1)
+            if self.char_dict is not None:
+                segs_t = transducer_segments(dense.cpu().numpy(), max_silence_frames(max_silence_duration))
+                res = format_segments(segs_t, self.char_dict)
+                if not return_timestamps:
+                    res = " ".join(item["decode"] for item in res).strip()
+            else:
+                res = tokens
+            if return_encoder_out:
+                return res, enc_all.unsqueeze(0)
+            return res
         tokens = torch.cat(ids).long().reshape(1, -1, 1) if ids else None
         if self.char_dict is not None and tokens is not None:
             # get_output_with_timestamps (model_utils.py:174-221) on the device: sentence split at
@@ -324,6 +386,18 @@ class ChunkFormerModel:
             lens = torch.tensor([x.shape[0] for x in xs], dtype=torch.int)
             offset = torch.zeros(len(xs), dtype=torch.int)
             eo, el, n_chunks, _, _, _ = self.encoder.forward_parallel_chunk(xs, lens, C, L, R, offset=offset)
+            if self.model_type == "transducer":
+                # batch_greedy_search over each utterance's rows (chunkformer_model.py:533-543): the
+                # packed rows go straight in (no pad_sequence), one workgroup per utterance
+                starts = (np.cumsum([0] + list(n_chunks[:-1])) * C).tolist()
+                dense = self.rnnt.greedy_packed(eo.reshape(-1, eo.shape[-1]), starts, el.tolist()).cpu()
+                hyps = [dense[s0: s0 + int(n)].reshape(-1) for s0, n in zip(starts, el.tolist())]
+                hyps = [h[h != self.rnnt.cfg.blank].tolist() for h in hyps]
+                if self.char_dict is not None:
+                    decodes.extend(class2str(h, self.char_dict).strip() for h in hyps)
+                else:
+                    decodes.extend(hyps)
+                continue
             _, hyp = self.encoder.ctc_log_softmax(eo, want_logp=False)   # fused argmax head
             if self.char_dict is not None:
                 # remove_duplicates_and_blank on the device, per utterance rows [64 * chunk0, +len)

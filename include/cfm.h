@@ -40,7 +40,7 @@ typedef enum { CFM_DTYPE_F32 = 0, CFM_DTYPE_BF16 = 1 } cfm_dtype;
 typedef struct {
   int32_t input_dim;      /* 80 */
   int32_t d_model;        /* output_size: 128, 256 or 512 */
-  int32_t n_heads;        /* attention_heads (head dim must be 64) */
+  int32_t n_heads;        /* attention_heads: head dim d_model / n_heads must be 64 or 128 */
   int32_t ffn_dim;        /* linear_units */
   int32_t num_blocks;
   int32_t kernel_size;    /* cnn_module_kernel (15) */
@@ -98,6 +98,15 @@ int32_t cfm_profile_read(const cfm_model* m, const char** names, double* total_m
 cfm_status cfm_plan_masked(const int32_t* lens_host, const int32_t* offsets_host, int32_t B, int32_t chunk_size,
                            int32_t left_context, int32_t right_context, int32_t* n_chunks_host,
                            int32_t* out_lens_host, int32_t* total_chunks, int32_t* plan_host, int64_t* plan_ints);
+/* cfm_plan_masked_ex: the same with the feature row count of each utterance (lens_host: x.size(0),
+ * which the reference pads and unfolds, encoder.py:556-564) separate from xs_origin_lens
+ * (mask_lens_host, NULL = lens_host), which bounds the masks and gives out_lens (encoder.py:567-596,
+ * 673).  A length pair whose bound count differs from the window count is the reference's shape
+ * mismatch: CFM_ERR_RUNTIME. */
+cfm_status cfm_plan_masked_ex(const int32_t* lens_host, const int32_t* mask_lens_host, const int32_t* offsets_host,
+                              int32_t B, int32_t chunk_size, int32_t left_context, int32_t right_context,
+                              int32_t* n_chunks_host, int32_t* out_lens_host, int32_t* total_chunks, int32_t* plan_host,
+                              int64_t* plan_ints);
 
 /* cfm_plan_padded: padded-batch geometry of forward_encoder (encoder.py:220-274,
  * attention.py:334-386, convolution.py:148-167).  chunk_size <= 0 -> full
@@ -219,6 +228,37 @@ int64_t cfm_fbank_num_frames(const cfm_fbank* h, int64_t num_samples);
  * int16 scale); stream-ordered, no allocation, no host synchronisation */
 cfm_status cfm_fbank_compute(const cfm_fbank* h, const float* wave_dev, int64_t num_samples, float* out_dev,
                              cfm_stream stream);
+
+/* ---- RNN-T consumer (model: transducer checkpoints): greedy search over encoder outputs, the
+ * reference's optimized_search / batch_greedy_search (transducer/search/greedy_search.py:6-92) as
+ * endless_decode / batch_decode call them (chunkformer_model.py:439-448, 533-543), with the shipped
+ * RNNPredictor (lstm; transducer/predictor.py:66-208) and TransducerJoint (prejoin_linear, add,
+ * tanh, ffn_out; transducer/joint.py:74-111).  Predictor and joint compute in f32. */
+typedef struct {
+  int32_t vocab;        /* output_dim */
+  int32_t enc_dim;      /* joint_conf.enc_output_size (the encoder's d_model) */
+  int32_t embed_size;   /* predictor_conf.embed_size */
+  int32_t hidden;       /* predictor_conf.hidden_size */
+  int32_t num_layers;   /* predictor_conf.num_layers (<= 4) */
+  int32_t pred_out;     /* predictor_conf.output_size = joint_conf.pred_output_size */
+  int32_t join_dim;     /* joint_conf.join_dim */
+  int32_t blank;        /* 0 (init_model.py:125-128) */
+} cfm_rnnt_config;
+typedef struct cfm_rnnt cfm_rnnt;
+
+/* weights by reference key: predictor.embed.weight, predictor.rnn.{weight,bias}_{ih,hh}_l{k},
+ * predictor.projection.{weight,bias}, joint.{enc_ffn,pred_ffn,ffn_out}.{weight,bias} */
+cfm_status cfm_rnnt_create(const cfm_rnnt_config* cfg, const cfm_tensor_view* weights, int32_t n_weights,
+                           int32_t device, cfm_rnnt** out);
+void cfm_rnnt_destroy(cfm_rnnt* h);
+size_t cfm_rnnt_workspace_bytes(const cfm_rnnt* h, int32_t rows);
+/* Greedy search of utterances b = rows [row_start[b], row_start[b] + row_len[b]) of enc_dev
+ * [rows, enc_dim] f32 (device int32 row arrays).  out_dev [rows, n_steps] int32 must be zeroed by the
+ * caller; row t of an utterance receives the ids decided at its frame t in step order, exactly the
+ * reference's output[:, t * n_steps + step] with the sos column removed (0 = blank). */
+cfm_status cfm_rnnt_greedy(const cfm_rnnt* h, const float* enc_dev, int32_t rows, const int32_t* row_start_dev,
+                           const int32_t* row_len_dev, int32_t B, int32_t n_steps, int32_t* out_dev, void* workspace,
+                           size_t workspace_bytes, cfm_stream stream);
 
 #ifdef __cplusplus
 }

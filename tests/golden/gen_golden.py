@@ -301,6 +301,19 @@ def gen_text(path):
            "timestamps": {str(ms): mu.get_output_with_timestamps([torch.tensor(s).reshape(-1, 1) for s in streams],
                                                                  cd, "asr_model", ms)
                           for ms in (0.5, 0.24, 1.0)}}
+    # transducer branch (model_type "transducer"): per-frame decision rows [T, n_steps], no collapse
+    tstreams = []
+    for T in (1, 9, 60, 333):
+        d = np.zeros((T, 4), np.int64)
+        for t in range(T):
+            if rng.random() < 0.4:
+                k = int(rng.integers(1, 4))
+                d[t, :k] = rng.integers(1, V, size=k)
+        tstreams.append(d)
+    out["transducer_streams"] = [d.tolist() for d in tstreams]
+    out["transducer_timestamps"] = {str(ms): mu.get_output_with_timestamps([torch.tensor(d) for d in tstreams], cd,
+                                                                           "transducer", ms)
+                                    for ms in (0.5, 0.24, 0.0, 1.0)}
     g = np.load(os.path.join(HERE, "large_4h.npz"))
     starts = np.cumsum([0] + g["nchunks"].tolist())
     hyps = [g["ids"][starts[u]: starts[u + 1]].reshape(-1)[: int(n)].tolist() for u, n in enumerate(g["outlens"])]
@@ -368,9 +381,76 @@ def gen_endless_tbd(path, cfg=SMALL, seed=1):
                         ids=ids.numpy().astype(np.int32), att=ac.numpy(), cnn=cc.numpy())
 
 
+def gen_rows_neq(path, cfg=SMALL, seed=1):
+    """forward_parallel_chunk with x.size(0) != xs_origin_lens (encoder.py:556-596, 673): the rows are
+    padded and unfolded from x.size(0) while the masks and output lengths follow xs_origin_lens; the
+    lengths keep the reference's bound count equal to its window count (else it fails on shapes)."""
+    enc, _, sd = build_reference(cfg, seed)
+    rows, lens, C, L, R = [700, 237, 1100, 300], [690, 230, 1100, 271], 16, 32, 32
+    xs = feats(rows, 55)
+    with torch.no_grad():
+        r = enc.forward_parallel_chunk(xs, torch.tensor(lens), C, L, R)
+    np.savez_compressed(path, sd_digest=sd_digest(sd), seed=np.array(seed), feat_seed=np.array(55),
+                        rows=np.array(rows, np.int32), lens=np.array(lens, np.int32), clr=np.array([C, L, R], np.int32),
+                        out=r[0].numpy(), outlens=r[1].numpy(), nchunks=np.array(r[2], np.int32))
+
+
+ENDLESS_RNNT_FRAMES = 480
+
+
+def gen_rnnt(path, seed=3, n_steps=64):
+    """The RNN-T consumer (chunkformer_model.py:439-448, 533-543): the reference's optimized_search /
+    batch_greedy_search (transducer/search/greedy_search.py:6-92) with its RNNPredictor (lstm) and
+    TransducerJoint built from the vie recipe's shapes (examples/asr/rnnt/conf/
+    chunkformer-rnnt-large-vie.yaml: embed 256, hidden 512 x 2 layers, output 512, join 512,
+    V = 1024) and seeded weights (chunkformer_amd.transducer.synthetic_transducer_state_dict), over
+    encoder outputs the reference produced: (a) large_4h.npz's two utterances as one padded batch
+    (batch_decode's call) and (b) the first ENDLESS_RNNT_FRAMES frames of large_endless.npz's
+    4-segment output (endless_decode's call, B=1)."""
+    from chunkformer.transducer.joint import TransducerJoint
+    from chunkformer.transducer.predictor import RNNPredictor
+    from chunkformer.transducer.search.greedy_search import batch_greedy_search, optimized_search
+
+    from chunkformer_amd.transducer import RNNTConfig, synthetic_transducer_state_dict
+    c = RNNTConfig()
+    sd = synthetic_transducer_state_dict(c, seed)
+    pred = RNNPredictor(c.vocab, c.embed_size, c.pred_out, 0.1, c.hidden, c.num_layers, True, "lstm", 0.1).eval()
+    joint = TransducerJoint(c.vocab, c.enc_dim, c.pred_out, c.join_dim, True, False, "add", "tanh").eval()
+    pred.load_state_dict({k[len("predictor."):]: v for k, v in sd.items() if k.startswith("predictor.")}, strict=True)
+    joint.load_state_dict({k[len("joint."):]: v for k, v in sd.items() if k.startswith("joint.")}, strict=True)
+    model = types.SimpleNamespace(predictor=pred, joint=joint, blank=0)
+    g4 = np.load(os.path.join(HERE, "large_4h.npz"))
+    starts = np.cumsum([0] + g4["nchunks"].tolist())
+    utts = [torch.from_numpy(g4["out"][starts[u]: starts[u + 1]].reshape(-1, c.enc_dim)[: int(n)])
+            for u, n in enumerate(g4["outlens"])]
+    lens = torch.tensor([u.shape[0] for u in utts])
+    enc_b = torch.nn.utils.rnn.pad_sequence(utts, batch_first=True)
+    ge = np.load(os.path.join(HERE, "large_endless.npz"))
+    enc_e = torch.from_numpy(ge["out"][:ENDLESS_RNNT_FRAMES]).unsqueeze(0)
+    with torch.no_grad():
+        out_b = optimized_search(model, enc_b, lens, n_steps)
+        hyps_b = batch_greedy_search(model, enc_b, lens, n_steps)
+        out_e = optimized_search(model, enc_e, torch.tensor([enc_e.shape[1]]), n_steps)
+    from oracle import rnnt_ref
+    _, m_b = rnnt_ref.optimized_search(sd, c.num_layers, c.hidden, enc_b, lens, n_steps)
+    _, m_e = rnnt_ref.optimized_search(sd, c.num_layers, c.hidden, enc_e, [enc_e.shape[1]], n_steps)
+    for nm, o in (("batch", out_b), ("endless", out_e)):
+        d = o.reshape(o.shape[0], -1, n_steps)
+        first = d[..., 0]
+        print(f"rnnt {nm}: frames {first.numel()}, blank-first {float((first == 0).float().mean()):.3f}, "
+              f"tokens {int((d != 0).sum())}, max steps/frame {int((d != 0).sum(-1).max())}")
+    print(f"rnnt min top-2 margins: batch {m_b:.2e}, endless {m_e:.2e}")
+    flat = [t for h in hyps_b for t in h]
+    np.savez_compressed(path, seed=np.array(seed), n_steps=np.array(n_steps),
+                        vocab=np.array(c.vocab), batch_lens=lens.numpy().astype(np.int32),
+                        batch_out=out_b.numpy().astype(np.int32), batch_hyp_lens=np.array([len(h) for h in hyps_b]),
+                        batch_hyps=np.array(flat, np.int32), endless_out=out_e.numpy().astype(np.int32),
+                        margin_batch=np.array(m_b), margin_endless=np.array(m_e))
+
+
 if __name__ == "__main__":
     which = sys.argv[1:] or ["masks", "small", "large", "large_4h", "large_endless", "large_full", "text", "stream",
-                             "endless_tbd"]
+                             "endless_tbd", "rnnt", "rows_neq"]
     if "masks" in which:
         gen_masks(os.path.join(HERE, "masks.npz"))
     if "small" in which:
@@ -389,4 +469,8 @@ if __name__ == "__main__":
         gen_stream(os.path.join(HERE, "stream.npz"))
     if "endless_tbd" in which:
         gen_endless_tbd(os.path.join(HERE, "endless_tbd80.npz"))
+    if "rows_neq" in which:
+        gen_rows_neq(os.path.join(HERE, "rows_neq.npz"))
+    if "rnnt" in which:
+        gen_rnnt(os.path.join(HERE, "rnnt.npz"))
     print("ok", which)

@@ -95,3 +95,15 @@ def test_plan_stream_geometry():
         _lib.plan_stream(8 * (C + R) + 15 + 8, C, L, R, 0)   # more than C + R frames
     with pytest.raises(ValueError):
         _lib.plan_stream(8 * 3 + 15, C, L, R, 0)             # fewer than R frames
+
+
+def test_planner_rows_differ_from_origin_lens(lib, golden_dir):
+    """x.size(0) != xs_origin_lens (encoder.py:556-596, 673): windows from the rows, bounds and out
+    lengths from xs_origin_lens; a bound count that differs from the window count is the
+    reference's shape-mismatch RuntimeError."""
+    g = np.load(os.path.join(golden_dir, "rows_neq.npz"))
+    C, L, R = (int(v) for v in g["clr"])
+    plan, nch, olens = lib.plan_masked(g["rows"].tolist(), [0] * len(g["rows"]), C, L, R, mask_lens=g["lens"].tolist())
+    assert nch == g["nchunks"].tolist() and olens == g["outlens"].tolist()
+    with pytest.raises(RuntimeError):
+        lib.plan_masked([700], [0], C, L, R, mask_lens=[300])

@@ -24,11 +24,12 @@ ENCODER_CONF = {"output_size": 512, "attention_heads": 4, "linear_units": 2048, 
                 "dynamic_conv": True}
 
 
-def write_checkpoint_dir(path, sd, cfg, with_cmvn_buffers: bool):
+def write_checkpoint_dir(path, sd, cfg, with_cmvn_buffers: bool, cmvn_key: bool = True):
     from chunkformer_amd.weights import synthetic_vocab
     conf = {"encoder": "chunkformer", "encoder_conf": ENCODER_CONF, "input_dim": 80, "output_dim": cfg.vocab,
-            "cmvn": "global_cmvn", "cmvn_conf": {"cmvn_file": "global_cmvn", "is_json_cmvn": True},
             "model": "asr_model", "ctc_conf": {"ctc_blank_id": 0}}
+    if cmvn_key:   # the reference enables CMVN from the global_cmvn FILE alone (chunkformer_model.py:153-160)
+        conf.update(cmvn="global_cmvn", cmvn_conf={"cmvn_file": "global_cmvn", "is_json_cmvn": True})
     with open(os.path.join(path, "config.yaml"), "w") as f:
         yaml.safe_dump(conf, f)
     # stats whose (mean, istd) reproduce the seeded CMVN tensors (up to f32 rounding)
@@ -46,8 +47,8 @@ def write_checkpoint_dir(path, sd, cfg, with_cmvn_buffers: bool):
             f.write(f"{tok} {i}\n")
 
 
-@pytest.mark.parametrize("with_cmvn_buffers", [True, False])
-def test_from_pretrained_batch_decode(tmp_path, golden_dir, with_cmvn_buffers):
+@pytest.mark.parametrize("with_cmvn_buffers,cmvn_key", [(True, True), (False, True), (False, False)])
+def test_from_pretrained_batch_decode(tmp_path, golden_dir, with_cmvn_buffers, cmvn_key):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     from chunkformer_amd.config import LARGE_4H
@@ -57,8 +58,9 @@ def test_from_pretrained_batch_decode(tmp_path, golden_dir, with_cmvn_buffers):
     with open(os.path.join(golden_dir, "text.json"), encoding="utf8") as f:
         text = json.load(f)
     sd = synthetic_state_dict(LARGE_4H, int(g["seed"]))
-    write_checkpoint_dir(str(tmp_path), sd, LARGE_4H, with_cmvn_buffers)
+    write_checkpoint_dir(str(tmp_path), sd, LARGE_4H, with_cmvn_buffers, cmvn_key)
     m = ChunkFormerModel.from_pretrained(str(tmp_path), dtype="fp32")
+    assert m.config.cmvn
     assert m.config.n_heads == 4 and m.config.head_dim == 128 and m.config.vocab == LARGE_4H.vocab
     assert m.char_dict is not None and m.char_dict[0] == "<blank>"
     xs = synthetic_features(g["lens"].tolist(), int(g["feat_seed"]))

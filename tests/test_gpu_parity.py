@@ -210,3 +210,27 @@ def test_masked_batch_rejects_length_mismatch(cfm, small_models):
     xs = [torch.randn(300, 80), torch.randn(200, 80)]
     with pytest.raises(ValueError):
         enc.forward_parallel_chunk(xs, torch.tensor([300, 150], dtype=torch.int32), 16, 32, 32)
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_rows_differ_from_origin_lens(golden_dir, dtype):
+    """forward_parallel_chunk with utterances longer than xs_origin_lens (the reference unfolds
+    x.size(0) rows and bounds masks / output lengths by xs_origin_lens) against the reference."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from chunkformer_amd.config import SMALL
+    from chunkformer_amd.encoder import ChunkFormerEncoder
+    from chunkformer_amd.weights import synthetic_features, synthetic_state_dict
+    g = np.load(os.path.join(golden_dir, "rows_neq.npz"))
+    C, L, R = (int(v) for v in g["clr"])
+    enc = ChunkFormerEncoder(SMALL, synthetic_state_dict(SMALL, int(g["seed"])), dtype=dtype)
+    xs = synthetic_features(g["rows"].tolist(), int(g["feat_seed"]))
+    off = torch.zeros(len(xs), dtype=torch.long)
+    out, olens, nch, _, _, off2 = enc.forward_parallel_chunk(xs, torch.tensor(g["lens"]), C, L, R, offset=off)
+    assert nch == g["nchunks"].tolist() and olens.tolist() == g["outlens"].tolist()
+    assert off2.tolist() == g["outlens"].tolist()
+    if dtype == "fp32":
+        np.testing.assert_allclose(out.cpu().numpy(), g["out"], atol=1e-4, rtol=0)
+    else:
+        o = out.cpu().numpy().astype(np.float64)
+        assert np.linalg.norm(o - g["out"]) / np.linalg.norm(g["out"]) <= 2e-2

@@ -1,0 +1,7 @@
+# round 3: RNN-T consumer, checkpoint CMVN, rows != origin lens
+set -e
+R=$GRAFT_REPO_ROOT
+mkdir -p $R/gpurun_out
+cd $R
+timeout -k 10 900 python3 -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_rnnt.py tests/test_gpu_checkpoint.py "tests/test_gpu_parity.py::test_rows_differ_from_origin_lens" > gpurun_out/r3b.log 2>&1 || { tail -60 gpurun_out/r3b.log; exit 1; }
+tail -15 gpurun_out/r3b.log
