@@ -101,6 +101,13 @@ int chunk_attention_masked_bf16(const bf16* q, const bf16* kv, int kv_rows, cons
                                 const float* pos_u, const float* pos_v, const int32_t* desc, int n_chunks, int H,
                                 int C, int W, bf16* out, hipStream_t st, int diag = 0, int p_ld = 0, int reuse = 1);
 
+// masked-batch attention for head_dim 128 (attention128.hip): V^T copy of the KV stream, then the
+// band / score / P.V kernel; -1 when the shape is not eligible (C = 64, W <= 320, W % 64 == 0)
+bool attention_a128_eligible(int C, int W, int p_rows, int dk);
+int vt_transpose_bf16(const bf16* kv, int kv_rows, int H, bf16* vt, int vt_ld, hipStream_t st);
+int chunk_attention_masked_a128(const bf16* q, const bf16* kv, int kv_rows, const bf16* vt, int vt_ld, const bf16* P,
+                                int p_rows, int p_ld, const float* pos_u, const float* pos_v, const int32_t* desc,
+                                int n_chunks, int H, int C, int W, bf16* out, hipStream_t st);
 
 // conv module: depthwise k=15 + bias + LayerNorm + SiLU (conv_module.hip)
 template <typename T>

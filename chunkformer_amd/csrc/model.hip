@@ -189,7 +189,14 @@ struct ModelT : public cfm_model {
   struct WS {
     float* x;
     T *h, *hid, *q, *kv, *ao, *glu, *cv, *y, *y2, *P, *pos, *feA, *feB, *feC;
+    T* vt = nullptr;   // head_dim 128 masked batch: V^T copy of the KV stream [H][128][vt_ld]
+    int vt_ld = 0;
   };
+  // the head_dim 128 attention kernel's V^T buffer is needed (bf16 masked batch)
+  bool uses_vt(const int32_t* h) const {
+    return sizeof(T) == 2 && h[PH_KIND] == 1 && use_ring_attention && cfg.d_model == 128 * cfg.n_heads &&
+           attention_a128_eligible(h[PH_C], h[PH_L] + h[PH_C] + h[PH_R], h[PH_PROWS], 128);
+  }
 
   WS carve(void* base, const int32_t* h, size_t* total) const {
     const int d = cfg.d_model, ff = cfg.ffn_dim, nb = cfg.num_blocks;
@@ -218,6 +225,10 @@ struct ModelT : public cfm_model {
     // all windows after the group loop (per group it is too small to fill the chip)
     const int T3 = (T2 - 3) / 2 + 1;
     w.feC = c.take<T>((size_t)h[PH_NWIN] * T3 * 9 * d);
+    if (uses_vt(h)) {
+      w.vt_ld = (h[PH_KVROWS] + 7) / 8 * 8;
+      w.vt = c.take<T>((size_t)d * w.vt_ld);
+    }
     if (total) *total = c.off;
     return w;
   }
@@ -340,6 +351,11 @@ struct ModelT : public cfm_model {
             r = chunk_attention_masked_bf16(w.q, w.kv, kv_rows, w.P + (size_t)l * d, p_rows, Lw.pu, Lw.pv,
                                             attd, natt, H, C, hh[PH_L] + C + hh[PH_R], w.ao, st, attn_diag, p_ld,
                                             tune.attn_reuse);
+          else if (w.vt) {   // head_dim 128 (4-head d=512): V^T copy, then the band / score / P.V kernel
+            KCHK(vt_transpose_bf16(w.kv, kv_rows, H, w.vt, w.vt_ld, st));
+            r = chunk_attention_masked_a128(w.q, w.kv, kv_rows, w.vt, w.vt_ld, w.P + (size_t)l * d, p_rows, p_ld,
+                                            Lw.pu, Lw.pv, attd, natt, H, C, hh[PH_L] + C + hh[PH_R], w.ao, st);
+          }
           // full attention (padded plan, one chunk of T' per utterance: key window [0, T')) -> dense kernel
           else if (!masked && !stream && hh[PH_L] == 0 && hh[PH_R] == 0 && hh[PH_C] == hh[PH_TOUT] &&
                    use_ring_attention && natt == hh[PH_NWIN] * ((hh[PH_TOUT] + 63) / 64))

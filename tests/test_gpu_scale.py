@@ -239,3 +239,28 @@ def test_wide_windows_fall_back_correctly(C, L, R):
             np.testing.assert_allclose(out, r_out, atol=1e-4, rtol=0)
         else:
             assert _rel_l2(out, r_out) <= BF16_RELL2
+
+
+def test_head_dim_128_kernel_vs_generic():
+    """The head_dim 128 masked-batch kernel (attention128.hip) against the generic per-block kernel
+    (model option ring_attention = 0) on the 4-head d=512 model, 12 layers, a batch with utterance
+    starts / ends (masked key ranges), a 1-chunk utterance and a T < 15 one."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from chunkformer_amd.config import LARGE_4H
+    from chunkformer_amd.encoder import ChunkFormerEncoder
+    from chunkformer_amd.weights import synthetic_features, synthetic_state_dict
+    enc = ChunkFormerEncoder(LARGE_4H, synthetic_state_dict(LARGE_4H, 0), dtype="bf16")
+    lens = [30_000, 519, 3000, 7, 12_345, 1100, 64_000]
+    xs = synthetic_features(lens, 17)
+    tl = torch.tensor(lens, dtype=torch.int32)
+    fast = enc.forward_parallel_chunk(xs, tl, 64, 128, 128)[0].cpu().numpy()
+    enc.set_option("ring_attention", 0)
+    try:
+        gen = enc.forward_parallel_chunk(xs, tl, 64, 128, 128)[0].cpu().numpy()
+    finally:
+        enc.set_option("ring_attention", 1)
+    assert np.isfinite(fast).all()
+    rel = _rel_l2(fast, gen)
+    print(f"head_dim 128 kernel vs generic: rel-L2 {rel:.2e}")
+    assert rel <= 5e-3
