@@ -204,12 +204,13 @@ def test_dense_attention_matches_generic(cfm, small_models, clr):
 
 
 def test_masked_batch_rejects_length_mismatch(cfm, small_models):
-    """xs[i] must be passed at xs_origin_lens[i] frames (encoder.py:556-580 plans from x.size(0) and
-    bounds from xs_origin_lens; they only agree when equal)."""
+    """x.size(0) rows and xs_origin_lens whose chunk counts differ: the reference's bound tensors
+    then mismatch its windows (encoder.py:567-612, a RuntimeError on shapes); so does this build.
+    Equal counts are accepted (test_rows_differ_from_origin_lens)."""
     enc = small_models["fp32"]
     xs = [torch.randn(300, 80), torch.randn(200, 80)]
-    with pytest.raises(ValueError):
-        enc.forward_parallel_chunk(xs, torch.tensor([300, 150], dtype=torch.int32), 16, 32, 32)
+    with pytest.raises(RuntimeError):
+        enc.forward_parallel_chunk(xs, torch.tensor([300, 40], dtype=torch.int32), 16, 32, 32)
 
 
 @pytest.mark.parametrize("dtype", ["fp32", "bf16"])
