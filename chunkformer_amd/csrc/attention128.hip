@@ -78,7 +78,7 @@ __global__ __launch_bounds__(256) void vt_transpose_kernel(const bf16* __restric
 }
 
 // NT = W / 64 key tiles per window (W = L + C + R; 5 at C = 64, L = R = 128)
-template <int NT>
+template <int NT, int VAR>
 __global__ __launch_bounds__(512, 1) void chunk_attention_a128_kernel(
     const bf16* __restrict__ Q, const bf16* __restrict__ KV, int kv_rows, const bf16* __restrict__ VT, int vt_ld,
     const bf16* __restrict__ P, int p_rows, int p_ld, const float* __restrict__ pos_u, const float* __restrict__ pos_v,
@@ -202,20 +202,30 @@ __global__ __launch_bounds__(512, 1) void chunk_attention_a128_kernel(
     const bool need_mask = __builtin_amdgcn_readfirstlane(key_lo != 0 || key_hi != W) != 0;
     f32x4 S[NSUB];
     float mx = -INFINITY;
+    // subtiles in pairs: two independent MFMA chains interleaved, the pair's fragments loaded together
+    // (VAR 0: one subtile at a time)
+    constexpr int PAIR = VAR == 1 ? 2 : 1;
 #pragma unroll
-    for (int t = 0; t < NSUB; ++t) {
-      const int j0 = 16 * (kh + 2 * t);
-      const bf16x4_ bv = *reinterpret_cast<const bf16x4_*>(bb + 2 * (qi * A8_BAND_PITCH + j0 + 4 * g + 4));
-      int slot = rb + j0;
-      if (slot >= RING) slot -= RING;
-      bf16x8 kf[4];
+    for (int t0 = 0; t0 < NSUB; t0 += PAIR) {
+      bf16x8 kf[PAIR][4];
+      f32x4 a[PAIR];
 #pragma unroll
-      for (int s = 0; s < 4; ++s) kf[s] = *reinterpret_cast<const bf16x8*>(kr + sw256(slot + fr, 4 * s + g));
-      f32x4 a = (f32x4){(float)bv[0], (float)bv[1], (float)bv[2], (float)bv[3]};
+      for (int u = 0; u < PAIR; ++u) {
+        const int j0 = 16 * (kh + 2 * (t0 + u));
+        const bf16x4_ bv = *reinterpret_cast<const bf16x4_*>(bb + 2 * (qi * A8_BAND_PITCH + j0 + 4 * g + 4));
+        int slot = rb + j0;
+        if (slot >= RING) slot -= RING;
 #pragma unroll
-      for (int s = 0; s < 4; ++s) a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[s], quf[s], a, 0, 0, 0);
-      S[t] = a * scale;
-      __builtin_amdgcn_sched_barrier(0);   // keep each subtile's fragment loads next to its MFMAs
+        for (int s = 0; s < 4; ++s) kf[u][s] = *reinterpret_cast<const bf16x8*>(kr + sw256(slot + fr, 4 * s + g));
+        a[u] = (f32x4){(float)bv[0], (float)bv[1], (float)bv[2], (float)bv[3]};
+      }
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int u = 0; u < PAIR; ++u) a[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[u][s], quf[s], a[u], 0, 0, 0);
+#pragma unroll
+      for (int u = 0; u < PAIR; ++u) S[t0 + u] = a[u] * scale;
+      __builtin_amdgcn_sched_barrier(0);   // keep each group's fragment loads next to its MFMAs
     }
     if (need_mask) {
 #pragma unroll
@@ -304,7 +314,7 @@ bool attention_a128_eligible(int C, int W, int p_rows, int dk) {
 
 int chunk_attention_masked_a128(const bf16* q, const bf16* kv, int kv_rows, const bf16* vt, int vt_ld, const bf16* P,
                                 int p_rows, int p_ld, const float* pos_u, const float* pos_v, const int32_t* desc,
-                                int n_chunks, int H, int C, int W, bf16* out, hipStream_t st) {
+                                int n_chunks, int H, int C, int W, bf16* out, hipStream_t st, int var) {
   if (!attention_a128_eligible(C, W, p_rows, 128) || n_chunks <= 0) return -1;
   static int n_cu = 0;
   if (!n_cu) {
@@ -316,15 +326,19 @@ int chunk_attention_masked_a128(const bf16* q, const bf16* kv, int kv_rows, cons
   int nch = (int)(((long long)n_chunks * H + n_cu - 1) / n_cu);
   nch = std::max(4, nch);
   const dim3 grid((n_chunks + nch - 1) / nch, H);
-#define A128(NT_)                                                                                                   \
-  hipLaunchKernelGGL(chunk_attention_a128_kernel<NT_>, grid, dim3(512), 0, st, q, kv, kv_rows, vt, vt_ld, P, p_rows, \
-                     p_ld, pos_u, pos_v, desc, n_chunks, H, nch, out)
+#define A128(NT_, V_)                                                                                                \
+  hipLaunchKernelGGL((chunk_attention_a128_kernel<NT_, V_>), grid, dim3(512), 0, st, q, kv, kv_rows, vt, vt_ld, P,   \
+                     p_rows, p_ld, pos_u, pos_v, desc, n_chunks, H, nch, out)
+  // var ("attn128_var" model option, A/B): 1 = paired score subtiles (default), 0 = one at a time
   switch (W / 64) {
-    case 1: A128(1); break;
-    case 2: A128(2); break;
-    case 3: A128(3); break;
-    case 4: A128(4); break;
-    default: A128(5); break;
+    case 1: A128(1, 1); break;
+    case 2: A128(2, 1); break;
+    case 3: A128(3, 1); break;
+    case 4: A128(4, 1); break;
+    default:
+      if (var == 0) A128(5, 0);
+      else A128(5, 1);
+      break;
   }
 #undef A128
   CFM_CHECK_LAUNCH();

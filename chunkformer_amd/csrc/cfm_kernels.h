@@ -41,6 +41,7 @@ struct Tuning {
   int conv_dot2 = 1;             // conv module: bf16 dot2 kernel (0: per-tap f32 kernel)
   int conv_dma = 1;              // conv module: LDS-DMA window staging (0: register staging)
   int dw2_seg = 4;               // front-end dw2: row segments per walk
+  int attn128_var = 1;           // head_dim 128 attention kernel variant (A/B)
   // GEMM sites whose bf16 outputs are stored non-temporally ("nt_sites" bit mask, SITE_* below).
   // Default: FFN w2 (its y goes straight to the LayerNorm; bench A/B 52.2 -> 51.4 ms/step); nt on
   // the front-end pointwise outputs (+0.45 ms) or FFN w1's hidden (w1 slower) measured worse.
@@ -107,7 +108,7 @@ bool attention_a128_eligible(int C, int W, int p_rows, int dk);
 int vt_transpose_bf16(const bf16* kv, int kv_rows, int H, bf16* vt, int vt_ld, hipStream_t st);
 int chunk_attention_masked_a128(const bf16* q, const bf16* kv, int kv_rows, const bf16* vt, int vt_ld, const bf16* P,
                                 int p_rows, int p_ld, const float* pos_u, const float* pos_v, const int32_t* desc,
-                                int n_chunks, int H, int C, int W, bf16* out, hipStream_t st);
+                                int n_chunks, int H, int C, int W, bf16* out, hipStream_t st, int var = 1);
 
 // conv module: depthwise k=15 + bias + LayerNorm + SiLU (conv_module.hip)
 template <typename T>

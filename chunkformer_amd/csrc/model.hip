@@ -354,7 +354,8 @@ struct ModelT : public cfm_model {
           else if (w.vt) {   // head_dim 128 (4-head d=512): V^T copy, then the band / score / P.V kernel
             KCHK(vt_transpose_bf16(w.kv, kv_rows, H, w.vt, w.vt_ld, st));
             r = chunk_attention_masked_a128(w.q, w.kv, kv_rows, w.vt, w.vt_ld, w.P + (size_t)l * d, p_rows, p_ld,
-                                            Lw.pu, Lw.pv, attd, natt, H, C, hh[PH_L] + C + hh[PH_R], w.ao, st);
+                                            Lw.pu, Lw.pv, attd, natt, H, C, hh[PH_L] + C + hh[PH_R], w.ao, st,
+                                            tune.attn128_var);
           }
           // full attention (padded plan, one chunk of T' per utterance: key window [0, T')) -> dense kernel
           else if (!masked && !stream && hh[PH_L] == 0 && hh[PH_R] == 0 && hh[PH_C] == hh[PH_TOUT] &&
@@ -673,7 +674,8 @@ cfm_status cfm_model_set_option(cfm_model* m, const char* key, int64_t value) {
     const std::pair<const char*, int*> knobs[] = {
         {"gemm_diag", &m->tune.gemm_diag}, {"gemm_wst", &m->tune.gemm_wst},   {"store_mode", &m->tune.store_mode},
         {"col_group", &m->tune.col_group}, {"attn_reuse", &m->tune.attn_reuse}, {"conv_dot2", &m->tune.conv_dot2},
-        {"conv_dma", &m->tune.conv_dma},   {"dw2_seg", &m->tune.dw2_seg},   {"nt_sites", &m->tune.nt_sites}};
+        {"conv_dma", &m->tune.conv_dma},   {"dw2_seg", &m->tune.dw2_seg},   {"nt_sites", &m->tune.nt_sites},
+        {"attn128_var", &m->tune.attn128_var}};
     for (auto& k : knobs)
       if (!std::strcmp(key, k.first)) { *k.second = (int)value; return CFM_OK; }
   }

@@ -24,11 +24,14 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--minutes", type=float, default=240)
     ap.add_argument("--variant", action="append", default=[])
+    ap.add_argument("--heads", type=int, default=8)
     a = ap.parse_args()
     lens = workload_lengths(int(a.minutes * 6000), 0)
     g = torch.Generator(device="cuda").manual_seed(1)
     xs = [torch.randn(t, 80, generator=g, device="cuda") for t in lens]
-    enc = ChunkFormerEncoder(LARGE, synthetic_state_dict(LARGE, 0), dtype="bf16")
+    from chunkformer_amd.config import LARGE_4H
+    cfg = LARGE if a.heads == 8 else LARGE_4H
+    enc = ChunkFormerEncoder(cfg, synthetic_state_dict(cfg, 0), dtype="bf16")
     enc.set_option("max_layers", a.layers)
     xl = torch.tensor(lens, dtype=torch.int32)
     variants = [dict(kv.split("=") for kv in v.split(",")) for v in a.variant] or [{}]
