@@ -50,30 +50,29 @@ CFM_DEV unsigned pk2(float a, float b) {
 }
 }  // namespace
 
-// V of the KV stream ([rows][H][K dk | V dk], dk = 128) -> V^T [H][128][vt_ld]; one block per 64
-// rows x head, through an LDS tile (rows past kv_rows are not written: never read)
+// V of the KV stream ([rows][H][K dk | V dk], dk = 128) -> V^T [H][128][vt_ld].  Each thread
+// transposes an 8-row x 8-dim bf16 block in registers (8 x 16-B loads, 32 v_perm_b32, 8 x 16-B
+// stores): a wave's loads cover 2 full 256-B V rows per load slot, its stores 64-B runs per dim.
+// Rows past kv_rows are not written (never read).
 __global__ __launch_bounds__(256) void vt_transpose_kernel(const bf16* __restrict__ kv, int kv_rows, int H,
                                                            bf16* __restrict__ vt, int vt_ld) {
-  __shared__ bf16 tile[64][128 + 8];
-  const int tid = threadIdx.x, h = blockIdx.y, r0 = blockIdx.x * 64;
+  const int tid = threadIdx.x, h = blockIdx.y;
+  const int dg = tid & 15, rg = tid >> 4;             // 16 dim groups x 16 row groups (128 rows per block)
+  const int r0 = blockIdx.x * 128 + rg * 8, d0 = dg * 8;
+  if (r0 >= kv_rows) return;
   const int d = H * 128;
+  u32x4 v[8];
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {   // 64 rows x 16 chunks of 8 dims
-    const int idx = tid + 256 * k, r = idx >> 4, ch = idx & 15;
-    const int row = min(r0 + r, kv_rows - 1);
-    const bf16x8 v = *reinterpret_cast<const bf16x8*>(kv + (size_t)row * 2 * d + h * 256 + 128 + ch * 8);
+  for (int i = 0; i < 8; ++i)
+    v[i] = *reinterpret_cast<const u32x4*>(kv + (size_t)min(r0 + i, kv_rows - 1) * 2 * d + h * 256 + 128 + d0);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) tile[r][ch * 8 + e] = v[e];
-  }
-  __syncthreads();
+  for (int k = 0; k < 8; ++k) {   // output dim d0 + k: rows r0 .. r0 + 7
+    u32x4 o;
+    // word j = (row 2j, row 2j+1) of dim k: the low / high halves of word k/2 of both rows
+    const unsigned sel = (k & 1) ? 0x07060302u : 0x05040100u;
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {   // 128 dims x 8 chunks of 8 rows
-    const int idx = tid + 256 * k, dim = idx >> 3, rc = idx & 7;
-    if (r0 + rc * 8 >= kv_rows) continue;
-    bf16x8 v;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] = tile[rc * 8 + e][dim];
-    *reinterpret_cast<bf16x8*>(vt + ((size_t)h * 128 + dim) * vt_ld + r0 + rc * 8) = v;
+    for (int j = 0; j < 4; ++j) o[j] = __builtin_amdgcn_perm(v[2 * j + 1][k >> 1], v[2 * j][k >> 1], sel);
+    *reinterpret_cast<u32x4*>(vt + ((size_t)h * 128 + d0 + k) * vt_ld + r0) = o;
   }
 }
 
@@ -152,7 +151,10 @@ __global__ __launch_bounds__(512, 1) void chunk_attention_a128_kernel(
   auto load_vt = [&](int c) {
     const bf16* vp = VT + ((size_t)h * 128 + 16 * w + fr) * vt_ld + (size_t)(kvb + (c - c0) * 64) + 8 * g;
 #pragma unroll
-    for (int ks = 0; ks < 2 * NT; ++ks) vf[ks] = *reinterpret_cast<const bf16x8*>(vp + 32 * ks);
+    for (int ks = 0; ks < 2 * NT; ++ks) {
+      if constexpr (VAR == 13) vf[ks] = (bf16x8){};   // timing only: no V^T loads
+      else vf[ks] = *reinterpret_cast<const bf16x8*>(vp + 32 * ks);
+    }
   };
   __syncthreads();
 
@@ -180,8 +182,10 @@ __global__ __launch_bounds__(512, 1) void chunk_attention_a128_kernel(
 #pragma unroll
       for (int rs = 0; rs < 3; ++rs) {
         f32x4 a = (f32x4){0.f, 0.f, 0.f, 0.f};
+        if constexpr (VAR != 10) {
 #pragma unroll
-        for (int s = 0; s < 4; ++s) a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pf[rs][s], qvf[s], a, 0, 0, 0);
+          for (int s = 0; s < 4; ++s) a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pf[rs][s], qvf[s], a, 0, 0, 0);
+        }
         const int i = 16 * qs + fr;
         const int col = 48 * w + 16 * rs + 4 * g + i - 59;
         if (col >= 1 && col <= W + 3) {   // groups that reach a read column j + 4, j in [0, W)
@@ -204,7 +208,7 @@ __global__ __launch_bounds__(512, 1) void chunk_attention_a128_kernel(
     float mx = -INFINITY;
     // subtiles in pairs: two independent MFMA chains interleaved, the pair's fragments loaded together
     // (VAR 0: one subtile at a time)
-    constexpr int PAIR = VAR == 1 ? 2 : 1;
+    constexpr int PAIR = VAR == 0 ? 1 : 2;
 #pragma unroll
     for (int t0 = 0; t0 < NSUB; t0 += PAIR) {
       bf16x8 kf[PAIR][4];
@@ -219,10 +223,12 @@ __global__ __launch_bounds__(512, 1) void chunk_attention_a128_kernel(
         for (int s = 0; s < 4; ++s) kf[u][s] = *reinterpret_cast<const bf16x8*>(kr + sw256(slot + fr, 4 * s + g));
         a[u] = (f32x4){(float)bv[0], (float)bv[1], (float)bv[2], (float)bv[3]};
       }
+      if constexpr (VAR != 11) {
 #pragma unroll
-      for (int s = 0; s < 4; ++s)
+        for (int s = 0; s < 4; ++s)
 #pragma unroll
-        for (int u = 0; u < PAIR; ++u) a[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[u][s], quf[s], a[u], 0, 0, 0);
+          for (int u = 0; u < PAIR; ++u) a[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[u][s], quf[s], a[u], 0, 0, 0);
+      }
 #pragma unroll
       for (int u = 0; u < PAIR; ++u) S[t0 + u] = a[u] * scale;
       __builtin_amdgcn_sched_barrier(0);   // keep each group's fragment loads next to its MFMAs
@@ -285,7 +291,8 @@ __global__ __launch_bounds__(512, 1) void chunk_attention_a128_kernel(
 #pragma unroll
       for (int qs = 0; qs < 4; ++qs) {
         const bf16x8 pb = *reinterpret_cast<const bf16x8*>(bb + ((16 * qs + fr) * A8_PROB_PITCH + 32 * ks + 8 * g) * 2);
-        O[qs] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf[ks], pb, O[qs], 0, 0, 0);
+        if constexpr (VAR != 12) O[qs] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf[ks], pb, O[qs], 0, 0, 0);
+        else O[qs][0] += (float)pb[0];
       }
     }
 #pragma unroll
@@ -303,7 +310,8 @@ __global__ __launch_bounds__(512, 1) void chunk_attention_a128_kernel(
 
 int vt_transpose_bf16(const bf16* kv, int kv_rows, int H, bf16* vt, int vt_ld, hipStream_t st) {
   if (kv_rows <= 0) return 0;
-  hipLaunchKernelGGL(vt_transpose_kernel, dim3((kv_rows + 63) / 64, H), dim3(256), 0, st, kv, kv_rows, H, vt, vt_ld);
+  if (kv_rows % 8) return (int)hipErrorInvalidValue;   // whole 8-row groups (masked plans: L + 64N + R)
+  hipLaunchKernelGGL(vt_transpose_kernel, dim3((kv_rows + 127) / 128, H), dim3(256), 0, st, kv, kv_rows, H, vt, vt_ld);
   CFM_CHECK_LAUNCH();
   return 0;
 }
@@ -336,8 +344,14 @@ int chunk_attention_masked_a128(const bf16* q, const bf16* kv, int kv_rows, cons
     case 3: A128(3, 1); break;
     case 4: A128(4, 1); break;
     default:
-      if (var == 0) A128(5, 0);
-      else A128(5, 1);
+      switch (var) {   // 10-13: timing-only diagnostics (no band / score / P.V MFMAs, no V^T loads)
+        case 0: A128(5, 0); break;
+        case 10: A128(5, 10); break;
+        case 11: A128(5, 11); break;
+        case 12: A128(5, 12); break;
+        case 13: A128(5, 13); break;
+        default: A128(5, 1); break;
+      }
       break;
   }
 #undef A128

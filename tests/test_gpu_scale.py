@@ -103,6 +103,7 @@ def test_golden_utterances_inside_bench_batch(large, dtype, minutes):
             sure = margin[gstart[k]: gstart[k + 1]] > 1e-3
             np.testing.assert_array_equal(i[sure], ei[sure])
         else:
+            print(f"bf16 golden utt {k}: rel-L2 {_rel_l2(o, exp):.2e}, CTC argmax agreement {(i == ei).mean():.4f}")
             assert _rel_l2(o, exp) <= BF16_RELL2, f"utt {k}: {_rel_l2(o, exp)}"
             assert (i == ei).mean() >= 0.99
 
