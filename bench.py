@@ -233,6 +233,9 @@ def main():
                          "configs[3] (16 h endless_decode, graph-replayed segments); full = configs[4] (full "
                          "attention, B=256)")
     ap.add_argument("--hours", type=float, default=16.0, help="endless: audio hours")
+    ap.add_argument("--endless-mode", default="pipeline", choices=["pipeline", "graph"],
+                    help="endless: two segments in flight on two streams (pipeline) or one captured HIP graph "
+                         "replayed per middle segment (graph); both are bit-identical to the eager loop")
     ap.add_argument("--tbd", type=int, default=7200,
                     help="endless: total_batch_duration (s); a memory budget that does not change results "
                          "(tests/test_gpu_model.py): 7200 s segments fill one MI355X better than the "
@@ -483,7 +486,8 @@ def bench_single(args):
         frames = T
 
         def step():
-            return model.endless_decode(x, C, L, R, total_batch_duration=args.tbd, return_timestamps=False)
+            return model.endless_decode(x, C, L, R, total_batch_duration=args.tbd, return_timestamps=False,
+                                        pipeline=args.endless_mode == "pipeline")
         from chunkformer_amd.model import endless_segments
         trunc, segs = endless_segments(T, C, L, R, args.tbd, LARGE.num_blocks, LARGE.kernel_size)
         seg_len = max(b - a for a, b, _, _ in segs)
@@ -493,9 +497,13 @@ def bench_single(args):
         roof_cls, attn_fl = "ffn_w1_gemm", None
         workload = (f"endless_decode over one {args.hours:g} h utterance (synthetic N(0,1) fbank), C=64 L=128 "
                     f"R=128, total_batch_duration={args.tbd}: {len(segs)} segments of <= {seg_len} frames "
-                    f"(trunc {trunc} rows kept each), att/cnn caches carried, middle segments replayed from one "
-                    f"captured HIP graph (front-end + 12 blocks + after_norm + CTC argmax)")
-        extra = {"segments": len(segs), "segment_frames": seg_len, "truncated_context_size": trunc}
+                    f"(trunc {trunc} rows kept each), att/cnn caches carried, " +
+                    ("two segments in flight on two HIP streams (segment k+1 layer l waits for segment k layer l)"
+                     if args.endless_mode == "pipeline" else
+                     "middle segments replayed from one captured HIP graph (front-end + 12 blocks + after_norm + "
+                     "CTC argmax)"))
+        extra = {"segments": len(segs), "segment_frames": seg_len, "truncated_context_size": trunc,
+                 "endless_mode": args.endless_mode}
     else:
         B, T = args.batch, 3000
         xs = torch.randn(B, T, 80, generator=g, device=dev)

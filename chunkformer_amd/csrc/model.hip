@@ -153,9 +153,13 @@ struct cfm_model {
   }
   // cache_b: batch size of a streaming-chunk call (plan kind 3): its caches are [nb, cache_b, H, L, 2dk] /
   // [nb, cache_b, d, 7] (forward_chunk layout) and `aci` etc. point at this element's [H, L, 2dk] slice
+  // stages [stage_lo, stage_hi]: -1 = front-end, relative positions, stream padding and the first
+  // LayerNorm; l = encoder layer l (its caches, ending with norm_final fused into the next layer's
+  // first LayerNorm or after_norm).  One call with (-1, num_blocks - 1) is the whole encoder; calls
+  // over consecutive stage ranges with the same workspace give the same result.
   virtual cfm_status encode(const float* feats, const int32_t* plan_dev, const int32_t* plan_hdr, const float* aci,
                             const float* cci, int trunc, float* aco, float* cco, float* out, void* ws, size_t wsb,
-                            hipStream_t st, int cache_b = 1) const = 0;
+                            hipStream_t st, int cache_b = 1, int stage_lo = -1, int stage_hi = 1 << 30) const = 0;
   virtual cfm_status ctc(const float* enc, int rows, float* logp, int32_t* ids, void* ws, size_t wsb,
                          hipStream_t st) const = 0;
   virtual size_t ws_bytes(const int32_t* hdr) const = 0;
@@ -246,7 +250,7 @@ struct ModelT : public cfm_model {
 
   cfm_status encode(const float* feats, const int32_t* plan_dev, const int32_t* hh, const float* aci, const float* cci,
                     int trunc, float* aco, float* cco, float* out, void* ws, size_t wsb,
-                    hipStream_t st, int cache_b) const override {
+                    hipStream_t st, int cache_b, int stage_lo, int stage_hi) const override {
     const int d = cfg.d_model, ff = cfg.ffn_dim, H = cfg.n_heads, dk = d / H;
     const float eps = cfg.norm_eps;
     const int rows = hh[PH_ROWS], C = hh[PH_C], L = hh[PH_L];
@@ -269,6 +273,11 @@ struct ModelT : public cfm_model {
     const int T1 = (Wn - 3) / 2 + 1, T2 = (T1 - 3) / 2 + 1, T3 = (T2 - 3) / 2 + 1;
     if (T3 != tout) return set_error(CFM_ERR_RUNTIME, "plan / front-end geometry mismatch");
 
+    const int nl = (max_layers >= 0 && max_layers < cfg.num_blocks) ? max_layers : cfg.num_blocks;
+    const int p_ld = cfg.num_blocks * d;
+    const int natt = hh[PH_NATT], nconv = hh[PH_NCONV];
+    const int cache_start = std::min(trunc, rows);   // new cache = stream[:trunc + L][-L:] (attention.py:467)
+    if (stage_lo < 0) {
     // ---------------- front-end
     const int G = fe_group(hh);
     for (int g0 = 0; g0 < nwin; g0 += G) {
@@ -285,8 +294,6 @@ struct ModelT : public cfm_model {
       PROF(PC_FE_GEMM, gemm<T>(EPI_STORE_F32, ACT_NONE, w.feC, 9 * d, (const T*)fe.wout, 9 * d, nwin * T3, d, 9 * d, e3, st)); }
     // ---------------- relative positions: P_l = pos . W_pos_l^T for every layer in ONE GEMM against
     // the stacked weights: P is [p_rows, nb * d], layer l at column l * d (row stride nb * d)
-    const int nl = (max_layers >= 0 && max_layers < cfg.num_blocks) ? max_layers : cfg.num_blocks;
-    const int p_ld = cfg.num_blocks * d;
     PROF(PC_POS, pos_table<T>(d, p_rows, hh[PH_PANCHOR], w.pos, st));
     { EpiArgs e = E(); e.out = w.P; e.ldo = p_ld;
       PROF(PC_POS, gemm<T>(EPI_STORE, ACT_NONE, w.pos, d, (const T*)fe.pos_all, d, p_rows, p_ld, d, e, st)); }
@@ -298,13 +305,12 @@ struct ModelT : public cfm_model {
     if (glu_rows > gluoff + rows)
       HIPC(hipMemsetAsync(w.glu + (size_t)(gluoff + rows) * d, 0, (size_t)(glu_rows - gluoff - rows) * d * sizeof(T), st));
 
-    const int natt = hh[PH_NATT], nconv = hh[PH_NCONV];
-    const int cache_start = std::min(trunc, rows);   // new cache = stream[:trunc + L][-L:] (attention.py:467)
     if (nl == 0) {
       PROF(PC_LN, layernorm2_f32<T>(w.x, ResidAdd<T>(), rows, d, fe.an_w, fe.an_b, nullptr, nullptr, eps, out, st));
       return CFM_OK;
     }
     PROF(PC_LN, layernorm<T>(w.x, ResidAdd<T>(), rows, d, layers[0].ln_ffm_w, layers[0].ln_ffm_b, eps, w.h, nullptr, st));
+    }   // stage -1
     // Each residual branch's last GEMM writes y = branch + bias (bf16/T); the residual add
     // x += alpha * y (0.5 for the FFNs, encoder_layer.py:196/246; the conv branch masked by
     // the padded path's row mask) is fused into the LayerNorm that reads x next.
@@ -325,7 +331,7 @@ struct ModelT : public cfm_model {
         PROF(PC_FFN2, gemm<T>(EPI_STORE, ACT_NONE, w.hid, ff, (const T*)w2, ff, rows, d, ff, e, st)); }
       return CFM_OK;
     };
-    for (int l = 0; l < nl; ++l) {
+    for (int l = std::max(0, stage_lo); l < nl && l <= stage_hi; ++l) {
       const LayerW& Lw = layers[l];
       // macaron FFN (x 0.5)
       { const cfm_status fs = ffn(Lw.ff1m, Lw.b_ff1m, Lw.ff2m, Lw.b_ff2m, w.y); if (fs != CFM_OK) return fs; }
@@ -718,6 +724,18 @@ cfm_status cfm_encode_masked(const cfm_model* m, const float* feats, const int32
   if ((aci == nullptr) != (cci == nullptr)) return set_error(CFM_ERR_VALUE, "att_cache and cnn_cache must be given together");
   HIPC(hipSetDevice(m->device));
   return m->encode(feats, plan_dev, h, aci, cci, trunc, aco, cco, out, ws, wsb, (hipStream_t)stream);
+}
+
+cfm_status cfm_encode_masked_stages(const cfm_model* m, const float* feats, const int32_t* h, const int32_t* plan_dev,
+                                    const float* aci, const float* cci, int32_t trunc, float* aco, float* cco, float* out,
+                                    void* ws, size_t wsb, int32_t stage_lo, int32_t stage_hi, cfm_stream stream) {
+  if (!m || !feats || !h || !plan_dev || !out) return set_error(CFM_ERR_VALUE, "null argument");
+  if (h[PH_KIND] != 1) return set_error(CFM_ERR_VALUE, "not a masked-batch plan");
+  if ((aci == nullptr) != (cci == nullptr)) return set_error(CFM_ERR_VALUE, "att_cache and cnn_cache must be given together");
+  if (stage_lo < -1 || stage_hi < stage_lo) return set_error(CFM_ERR_VALUE, "bad stage range");
+  HIPC(hipSetDevice(m->device));
+  return m->encode(feats, plan_dev, h, aci, cci, trunc, aco, cco, out, ws, wsb, (hipStream_t)stream, 1, stage_lo,
+                   stage_hi);
 }
 
 cfm_status cfm_encode_padded(const cfm_model* m, const float* xs, const int32_t* h, const int32_t* plan_dev, float* out,

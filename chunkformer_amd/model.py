@@ -35,7 +35,7 @@ import torch
 
 from .config import EncoderConfig
 from .encoder import ChunkFormerEncoder
-from .streaming import EndlessGraphRunner
+from .streaming import EndlessGraphRunner, EndlessPipeline
 from .transducer import RNNTConfig, RNNTGreedy
 
 Features = Union[torch.Tensor, np.ndarray, str]
@@ -299,7 +299,7 @@ class ChunkFormerModel:
                        left_context_size: Optional[int] = 128, right_context_size: Optional[int] = 128,
                        total_batch_duration: int = 1800, return_timestamps: bool = True,
                        max_silence_duration: float = 0.5, return_encoder_out: bool = False,
-                       cuda_graph: bool = True):
+                       cuda_graph: bool = True, pipeline: Optional[bool] = None):
         """chunkformer_model.py:321-459.  Segments of `total_batch_duration` seconds (halved,
         like the reference) go through forward_parallel_chunk with the attention/conv caches
         and `offset` carried; the CTC argmax runs per segment on the kept rows (row-wise, so
@@ -307,8 +307,10 @@ class ChunkFormerModel:
         Returns text (with char_dict) or ids [1, T', 1] like the reference; with
         `return_encoder_out` also the concatenated encoder output [1, T', d] (fp32).
         `cuda_graph`: the full-size middle segments replay one captured HIP graph (front-end,
-        blocks with the caches carried, after_norm, CTC argmax); see streaming.py.  The
-        result is identical to the eager loop (same kernels, same plans)."""
+        blocks with the caches carried, after_norm, CTC argmax); see streaming.py.  `pipeline`
+        (default: on from 3 segments up): two segments in flight on two streams instead, segment
+        k + 1's layer l waiting only for segment k's layer l (EndlessPipeline).  Every mode gives
+        the same result as the eager loop (same kernels, same plans)."""
         C = chunk_size if chunk_size is not None else 64
         L = left_context_size if left_context_size is not None else 128
         R = right_context_size if right_context_size is not None else 128
@@ -320,24 +322,33 @@ class ChunkFormerModel:
         seg_len = max(stop - start for start, stop, _, _ in segs) if segs else 0
         transducer = self.model_type == "transducer"
         want_eo = bool(return_encoder_out) or transducer   # the RNN-T search consumes the encoder rows
-        key = (C, L, R, trunc, seg_len, want_eo, bool(cuda_graph))
+        if pipeline is None:
+            pipeline = len(segs) >= 3
+        key = (C, L, R, trunc, seg_len, want_eo, bool(cuda_graph), bool(pipeline))
         runner = self._endless_runners.get(key)
         if runner is None:   # graphs are captured once per segment geometry and reused across calls
-            runner = EndlessGraphRunner(enc, C, L, R, trunc, seg_len, want_eo, use_graph=cuda_graph)
+            runner = (EndlessPipeline(enc, C, L, R, trunc, want_eo) if pipeline else
+                      EndlessGraphRunner(enc, C, L, R, trunc, seg_len, want_eo, use_graph=cuda_graph))
             self._endless_runners = {key: runner}
-        runner.reset()
-        offset = 0
-        for start, stop, keep_trunc, _ in segs:
-            # forward_parallel_chunk with att/cnn caches carried; offset += len, then -= dropped rows
-            tok, eo, kept = runner.step(xs_dev[start:stop], offset, keep_trunc)
-            offset += kept
-            if tok is not None:
-                ids.append(tok)
-            if eo is not None:
-                outs.append(eo)
-        # the caches carried out of the last segment (r_att_cache / r_cnn_cache of its
-        # forward_parallel_chunk call, chunkformer_model.py:407-417)
-        self.last_endless_caches = (runner.att[runner.cur], runner.cnn[runner.cur])
+        if pipeline:
+            tids, teos, cur = runner.run(xs_dev, segs)
+            ids = [t for t in tids if t is not None]
+            outs = [e for e in teos if e is not None]
+            self.last_endless_caches = (runner.att[cur], runner.cnn[cur])
+        else:
+            runner.reset()
+            offset = 0
+            for start, stop, keep_trunc, _ in segs:
+                # forward_parallel_chunk with att/cnn caches carried; offset += len, then -= dropped rows
+                tok, eo, kept = runner.step(xs_dev[start:stop], offset, keep_trunc)
+                offset += kept
+                if tok is not None:
+                    ids.append(tok)
+                if eo is not None:
+                    outs.append(eo)
+            # the caches carried out of the last segment (r_att_cache / r_cnn_cache of its
+            # forward_parallel_chunk call, chunkformer_model.py:407-417)
+            self.last_endless_caches = (runner.att[runner.cur], runner.cnn[runner.cur])
         if transducer:
             # optimized_search over the concatenated encoder output (chunkformer_model.py:439-448):
             # decisions [1, T, n_steps], text by get_output_with_timestamps' transducer branch

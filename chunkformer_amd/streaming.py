@@ -147,3 +147,94 @@ class EndlessGraphRunner:
         if self.vocab > 0 and eo.shape[0] > 0:
             ids = self.enc.ctc_log_softmax(eo, want_logp=False)[1]
         return ids, (eo if self.want_out else None), eo.shape[0]
+
+
+class EndlessPipeline:
+    """endless_decode's segments with TWO in flight (MI355X streams, no graph): segment k runs on
+    stream k % 2 and its encoder layer l waits only for segment k - 1's layer l (the attention /
+    conv caches it carries, attention.py:466-467, convolution.py:228-230), so segment k + 1's
+    front-end and early layers overlap segment k's later layers.  At the reference's default
+    total_batch_duration (1800 s: 12.7k-row segments) single launches leave most CUs idle in their
+    tail rounds; the second segment's kernels fill them.  Each stage is a cfm_encode_masked_stages
+    call (stage -1: front-end + relative positions; stage l: layer l), so the result is bit-identical
+    to the one-call-per-segment loop (same kernels, same inputs, same order per segment)."""
+
+    def __init__(self, encoder, C: int, L: int, R: int, trunc: int, want_out: bool):
+        self.enc = encoder
+        cfg = encoder.cfg
+        self.C, self.L, self.R, self.trunc = C, L, R, trunc
+        self.want_out = want_out
+        dev = encoder.device
+        self.dev = dev
+        nb, H, dk, d = cfg.num_blocks, cfg.n_heads, cfg.head_dim, cfg.d_model
+        self.att = [torch.zeros(nb, L, H, 2 * dk, device=dev) for _ in range(2)]
+        self.cnn = [torch.zeros(nb, d, cfg.conv_lorder, device=dev) for _ in range(2)]
+        self.streams = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
+        self.ws: List[Optional[torch.Tensor]] = [None, None]
+        self.out: List[Optional[torch.Tensor]] = [None, None]
+
+    def _buf(self, lst, i, nbytes, dtype, shape=None):
+        t = lst[i]
+        need = nbytes if shape is None else int(torch.Size(shape).numel())
+        if t is None or t.numel() < need:
+            lst[i] = torch.empty(need, dtype=dtype, device=self.dev)
+        return lst[i]
+
+    def run(self, xs_dev: torch.Tensor, segs):
+        """Returns (per-segment CTC ids of the kept rows, per-segment kept encoder rows or None,
+        index of the cache pair holding the caches after the last segment); the tensors are ready on
+        the caller's current stream."""
+        enc, C, L, R = self.enc, self.C, self.L, self.R
+        nb, d = enc.cfg.num_blocks, enc.cfg.d_model
+        self.att[0].zero_()
+        self.cnn[0].zero_()
+        caller = torch.cuda.current_stream(self.dev)
+        for s in self.streams:
+            s.wait_stream(caller)   # inputs and the zeroed caches
+        ids_out, eo_out, keep = [], [], []
+        prev = None
+        offset = 0
+        for k, (start, stop, keep_trunc, _) in enumerate(segs):
+            p = k % 2
+            st = self.streams[p]
+            x = xs_dev[start:stop]
+            n_frames = stop - start
+            plan, n_chunks, out_lens = _lib.plan_masked([n_frames], [offset], C, L, R)
+            N = n_chunks[0]
+            wsb = int(_lib.cfm_workspace_bytes_masked(enc._h, N, C, L, R))
+            cur = []
+            with torch.cuda.stream(st):
+                plan_dev = plan.pin_memory().to(self.dev, non_blocking=True)
+                ws = self._buf(self.ws, p, wsb, torch.uint8)
+                out = self._buf(self.out, p, None, torch.float32, (N * C, d))
+                src, dst = self.att[p], self.att[1 - p]
+                csrc, cdst = self.cnn[p], self.cnn[1 - p]
+                for stage in range(-1, nb):
+                    if stage >= 0 and prev is not None:
+                        st.wait_event(prev[stage])
+                    _lib.check(_lib.cfm_encode_masked_stages(
+                        enc._h, x.data_ptr(), plan.data_ptr(), plan_dev.data_ptr(), src.data_ptr(), csrc.data_ptr(),
+                        int(self.trunc), dst.data_ptr(), cdst.data_ptr(), out.data_ptr(), ws.data_ptr(), wsb,
+                        stage, stage, st.cuda_stream))
+                    if stage >= 0:
+                        ev = torch.cuda.Event()
+                        ev.record(st)
+                        cur.append(ev)
+                n = out_lens[0]
+                eo = out[: N * C].view(N * C, d)[:n]
+                if keep_trunc:
+                    eo = eo[: self.trunc]
+                ids = enc.ctc_log_softmax(eo, want_logp=False)[1] if enc.cfg.vocab > 0 and eo.shape[0] else None
+                eo_c = eo.clone() if self.want_out else None
+                for t in (ids, eo_c):
+                    if t is not None:
+                        t.record_stream(caller)
+                ids_out.append(ids)
+                eo_out.append(eo_c)
+            keep.append((plan, plan_dev))
+            offset += eo.shape[0]
+            prev = cur
+        for s in self.streams:
+            caller.wait_stream(s)
+        self._keep = keep
+        return ids_out, eo_out, len(segs) % 2

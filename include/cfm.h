@@ -131,6 +131,17 @@ cfm_status cfm_encode_masked(const cfm_model* m, const float* feats_dev, const i
                              float* att_cache_out, float* cnn_cache_out, float* out_dev, void* workspace,
                              size_t workspace_bytes, cfm_stream stream);
 
+/* cfm_encode_masked in stages, for pipelining consecutive endless_decode segments (segment k + 1's
+ * layer l needs only segment k's layer-l caches): stage -1 = the front-end, relative positions and the
+ * first LayerNorm; stage l = encoder layer l (the last one ends with after_norm into out_dev).  Calls
+ * over consecutive stage ranges [stage_lo, stage_hi] with the same plan, caches and workspace equal one
+ * cfm_encode_masked call bit for bit; the workspace carries the state between them. */
+cfm_status cfm_encode_masked_stages(const cfm_model* m, const float* feats_dev, const int32_t* plan_host,
+                                    const int32_t* plan_dev, const float* att_cache_in, const float* cnn_cache_in,
+                                    int32_t truncated_context_size, float* att_cache_out, float* cnn_cache_out,
+                                    float* out_dev, void* workspace, size_t workspace_bytes, int32_t stage_lo,
+                                    int32_t stage_hi, cfm_stream stream);
+
 /* cfm_encode_padded replaces ChunkFormerEncoder.forward_encoder (encoder.py:220-274)
  * and therefore ChunkFormerModel.encode (chunkformer_model.py:256-274).
  * xs_dev: [B, T, 80] f32 padded batch; out_dev: [B, T', d] f32. */

@@ -87,11 +87,20 @@ def test_endless_graph_replay_equals_eager(small, dtype):
     C, L, R, tbd = (int(v) for v in g["endless_clrt"])
     x = synthetic_features([6000], int(g["endless_seed"]))[0]
     m = models[dtype]
-    ids_e, eo_e = m.endless_decode(x, C, L, R, total_batch_duration=tbd, return_encoder_out=True, cuda_graph=False)
-    ids_g, eo_g = m.endless_decode(x, C, L, R, total_batch_duration=tbd, return_encoder_out=True, cuda_graph=True)
+    ids_e, eo_e = m.endless_decode(x, C, L, R, total_batch_duration=tbd, return_encoder_out=True, cuda_graph=False,
+                                   pipeline=False)
+    ca_e = [c.clone() for c in m.last_endless_caches]
+    ids_g, eo_g = m.endless_decode(x, C, L, R, total_batch_duration=tbd, return_encoder_out=True, cuda_graph=True,
+                                   pipeline=False)
     assert eo_g.shape == eo_e.shape
     assert torch.equal(eo_g, eo_e)
     assert torch.equal(ids_g, ids_e)
+    # two segments in flight on two streams (streaming.py EndlessPipeline): same rows, ids and caches
+    ids_p, eo_p = m.endless_decode(x, C, L, R, total_batch_duration=tbd, return_encoder_out=True, pipeline=True)
+    assert torch.equal(eo_p, eo_e)
+    assert torch.equal(ids_p, ids_e)
+    for a, b in zip(m.last_endless_caches, ca_e):
+        assert torch.equal(a, b)
 
 
 @pytest.mark.parametrize("dtype", ["fp32", "bf16"])

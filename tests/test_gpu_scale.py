@@ -161,6 +161,13 @@ def test_large_endless_decode(large, dtype):
         assert _rel_l2(att, g["att"]) <= BF16_RELL2
         assert _rel_l2(cc.cpu().numpy(), g["cnn"]) <= BF16_RELL2
         assert (ids == g["ids"]).mean() >= 0.99
+    # 4 segments: endless_decode ran them pipelined (two streams); the one-call-per-segment loop
+    # gives bit-identical rows, ids and carried caches
+    ids_s, eo_s = m.endless_decode(x, C, L, R, total_batch_duration=tbd, return_encoder_out=True, pipeline=False,
+                                   cuda_graph=False)
+    assert torch.equal(eo_s[0].cpu(), torch.from_numpy(eo))
+    assert np.array_equal(ids_s.reshape(-1).cpu().numpy(), ids)
+    assert torch.equal(m.last_endless_caches[0], ac) and torch.equal(m.last_endless_caches[1], cc)
 
 
 @pytest.mark.parametrize("dtype", ["fp32", "bf16"])
