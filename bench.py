@@ -236,6 +236,7 @@ def main():
     ap.add_argument("--endless-mode", default="pipeline", choices=["pipeline", "graph"],
                     help="endless: two segments in flight on two streams (pipeline) or one captured HIP graph "
                          "replayed per middle segment (graph); both are bit-identical to the eager loop")
+    ap.add_argument("--pipeline-depth", type=int, default=3, help="endless pipeline: segments in flight")
     ap.add_argument("--tbd", type=int, default=7200,
                     help="endless: total_batch_duration (s); a memory budget that does not change results "
                          "(tests/test_gpu_model.py): 7200 s segments fill one MI355X better than the "
@@ -487,7 +488,7 @@ def bench_single(args):
 
         def step():
             return model.endless_decode(x, C, L, R, total_batch_duration=args.tbd, return_timestamps=False,
-                                        pipeline=args.endless_mode == "pipeline")
+                                        pipeline=args.endless_mode == "pipeline", pipeline_depth=args.pipeline_depth)
         from chunkformer_amd.model import endless_segments
         trunc, segs = endless_segments(T, C, L, R, args.tbd, LARGE.num_blocks, LARGE.kernel_size)
         seg_len = max(b - a for a, b, _, _ in segs)
@@ -503,7 +504,7 @@ def bench_single(args):
                      "middle segments replayed from one captured HIP graph (front-end + 12 blocks + after_norm + "
                      "CTC argmax)"))
         extra = {"segments": len(segs), "segment_frames": seg_len, "truncated_context_size": trunc,
-                 "endless_mode": args.endless_mode}
+                 "endless_mode": args.endless_mode, "pipeline_depth": args.pipeline_depth}
     else:
         B, T = args.batch, 3000
         xs = torch.randn(B, T, 80, generator=g, device=dev)

@@ -299,7 +299,7 @@ class ChunkFormerModel:
                        left_context_size: Optional[int] = 128, right_context_size: Optional[int] = 128,
                        total_batch_duration: int = 1800, return_timestamps: bool = True,
                        max_silence_duration: float = 0.5, return_encoder_out: bool = False,
-                       cuda_graph: bool = True, pipeline: Optional[bool] = None):
+                       cuda_graph: bool = True, pipeline: Optional[bool] = None, pipeline_depth: int = 3):
         """chunkformer_model.py:321-459.  Segments of `total_batch_duration` seconds (halved,
         like the reference) go through forward_parallel_chunk with the attention/conv caches
         and `offset` carried; the CTC argmax runs per segment on the kept rows (row-wise, so
@@ -308,8 +308,8 @@ class ChunkFormerModel:
         `return_encoder_out` also the concatenated encoder output [1, T', d] (fp32).
         `cuda_graph`: the full-size middle segments replay one captured HIP graph (front-end,
         blocks with the caches carried, after_norm, CTC argmax); see streaming.py.  `pipeline`
-        (default: on from 3 segments up): two segments in flight on two streams instead, segment
-        k + 1's layer l waiting only for segment k's layer l (EndlessPipeline).  Every mode gives
+        (default: on from 3 segments up): `pipeline_depth` segments in flight on as many streams
+        instead, segment k + 1's layer l waiting only for segment k's layer l (EndlessPipeline).  Every mode gives
         the same result as the eager loop (same kernels, same plans)."""
         C = chunk_size if chunk_size is not None else 64
         L = left_context_size if left_context_size is not None else 128
@@ -324,10 +324,10 @@ class ChunkFormerModel:
         want_eo = bool(return_encoder_out) or transducer   # the RNN-T search consumes the encoder rows
         if pipeline is None:
             pipeline = len(segs) >= 3
-        key = (C, L, R, trunc, seg_len, want_eo, bool(cuda_graph), bool(pipeline))
+        key = (C, L, R, trunc, seg_len, want_eo, bool(cuda_graph), bool(pipeline), int(pipeline_depth))
         runner = self._endless_runners.get(key)
         if runner is None:   # graphs are captured once per segment geometry and reused across calls
-            runner = (EndlessPipeline(enc, C, L, R, trunc, want_eo) if pipeline else
+            runner = (EndlessPipeline(enc, C, L, R, trunc, want_eo, pipeline_depth) if pipeline else
                       EndlessGraphRunner(enc, C, L, R, trunc, seg_len, want_eo, use_graph=cuda_graph))
             self._endless_runners = {key: runner}
         if pipeline:
