@@ -331,16 +331,23 @@ def main():
     roof_cls = "ffn_w1_gemm"
     roof_name = ("ffn_w1_gemm (gemm_wsp_kernel<EPI_STORE,SiLU>: K=512 weight-stationary bf16 MFMA)"
                  if args.dtype == "bf16" else "ffn_w1_gemm (gemm_kernel<float,EPI_STORE,SiLU>)")
-    fl_launch = 2.0 * rows * ff_ * d_
-    # compulsory bytes of one w_1 launch: A [rows, d] + out [rows, ff] bf16 + W [ff, d] bf16 + bias
-    alg_bytes = 2.0 * (rows * d_ + rows * ff_ + ff_ * d_) + 4 * ff_
+    # per step: one w_1 launch per layer and utterance group (enc.stream_split groups of the batch run
+    # on their own streams, so a launch covers rows / groups rows); totals over the timed launches
+    # (two FFNs per layer: the macaron and the final one)
+    fl_step = 2.0 * rows * ff_ * d_ * 2 * cfg.num_blocks
     ms1, n1 = prof[roof_cls]
+    per_step = n1 / args.steps if n1 else 1
+    fl_launch = fl_step / per_step
+    rows_launch = rows / (per_step / (2 * cfg.num_blocks))
+    # compulsory bytes of one w_1 launch: A [rows, d] + out [rows, ff] bf16 + W [ff, d] bf16 + bias
+    alg_bytes = 2.0 * (rows_launch * d_ + rows_launch * ff_ + ff_ * d_) + 4 * ff_
     avg_s = (ms1 / max(n1, 1)) / 1e3
-    achieved = fl_launch / avg_s / 1e12 if n1 else None
+    achieved = fl_step * args.steps / (ms1 / 1e3) / 1e12 if n1 else None
     peak = PEAK_TFLOPS[args.dtype]
     # the committed PMC traffic was collected on the default workload (configs[1], 2,845 chunks on one
     # GPU); other row counts report null rather than a number measured on a different launch size
-    profiled = args.dtype == "bf16" and not sharded and world == 1 and n_chunks == 2845 and args.heads == 8
+    profiled = (args.dtype == "bf16" and not sharded and world == 1 and n_chunks == 2845 and args.heads == 8
+                and per_step == 2 * cfg.num_blocks)   # the committed PMC passes ran un-split launches
     traffic, traffic_src = committed_traffic(roof_cls) if profiled else (None, None)
     busy, busy_clk, busy_src = committed_mfma_busy(roof_cls) if profiled else (None, None, None)
     step_flops = n_chunks * flops_per_chunk(cfg) + cfg.num_blocks * 2 * (L + 2 * C + R - 1) * cfg.d_model ** 2
@@ -438,6 +445,8 @@ def main():
                          "traffic_source": traffic_src,
                          "algorithmic_bytes_per_launch": alg_bytes,
                          "flops_per_launch": fl_launch, "avg_launch_ms": round(avg_s * 1e3, 4), "launches": n1,
+                         "rows_per_launch": round(rows_launch, 1),
+                         "stream_split": enc.stream_split if n_chunks >= enc.split_min_chunks else 1,
                          # context, not the contract's peak: the bf16 MFMA rate this chip sustains on random
                          # operands (tools/mfma_peak.hip, 2 waves/SIMD, in-kernel clock 1.83 GHz) and the
                          # vendor GEMM on the same shape without bias/activation (tools/torch_gemm_ref.py)

@@ -66,6 +66,14 @@ class ChunkFormerEncoder:
                                              ctypes.byref(h)))
         self._h = h
         self._ws: Optional[torch.Tensor] = None
+        # option: large masked batches as `stream_split` utterance groups on as many streams, staggered
+        # by encoder layer (_encode_masked_split); per-utterance results do not depend on the grouping.
+        # Off by default: +1-2.6% frames/s on the 240-min batch, but each kernel then shares the chip
+        # with the other group's, which hides its own roofline (FFN w1 0.37 ms -> 0.29 ms at half the rows)
+        self.stream_split = 1
+        self.split_min_chunks = 1024
+        self._split_streams: List[torch.cuda.Stream] = []
+        self._split_ws: List[Optional[torch.Tensor]] = []
         # destroy the native handle when this object is collected or at interpreter exit (a finalizer
         # holds its own reference to the bound ctypes function, unlike __del__ at shutdown)
         self._finalizer = weakref.finalize(self, _lib.cfm_model_destroy, ctypes.c_void_p(h.value))
@@ -74,6 +82,11 @@ class ChunkFormerEncoder:
         return self._output_size
 
     def set_option(self, key: str, value: int) -> None:
+        if key in ("stream_split", "split_min_chunks"):   # host-side scheduling knobs
+            if int(value) < (1 if key == "stream_split" else 0):
+                raise ValueError(f"{key} = {value}")
+            setattr(self, key, int(value))
+            return
         _lib.check(_lib.cfm_model_set_option(self._h, key.encode(), int(value)))
 
     # ------------------------------------------------------------------ helpers
@@ -116,7 +129,6 @@ class ChunkFormerEncoder:
         feats = torch.cat([x.to(dev, torch.float32).reshape(-1, self.cfg.input_dim) for x in xs], 0).contiguous()
         if feats.shape[0] == 0:
             feats = torch.zeros(1, self.cfg.input_dim, device=dev)
-        plan_dev = self._upload(plan)
         out = torch.empty(N * C, d, dtype=torch.float32, device=dev)
         has_cache = att_cache.size(0) > 0
         aci = cci = aco = cco = None
@@ -130,9 +142,15 @@ class ChunkFormerEncoder:
                 raise ValueError(f"cnn_cache shape {tuple(cci.shape)} != {(nb, d, self.cfg.conv_lorder)}")
             aco = torch.empty_like(aci)
             cco = torch.empty_like(cci)
-        ws_bytes = _lib.cfm_workspace_bytes_masked(self._h, N, C, L, R)
-        ws = self._workspace(ws_bytes)
-        self._encode_masked_raw(feats, plan, plan_dev, aci, cci, int(truncated_context_size), aco, cco, out, ws)
+        parts = min(self.stream_split, B)
+        if not has_cache and parts > 1 and N >= self.split_min_chunks:
+            self._encode_masked_split(feats, lens, offs, mask_lens, n_chunks, parts, C, L, R, out)
+        else:
+            plan_dev = self._upload(plan)
+            ws_bytes = _lib.cfm_workspace_bytes_masked(self._h, N, C, L, R)
+            ws = self._workspace(ws_bytes)
+            self._last_plan = (plan, plan_dev)   # keep the uploaded plan alive until the stream consumed it
+            self._encode_masked_raw(feats, plan, plan_dev, aci, cci, int(truncated_context_size), aco, cco, out, ws)
         xs_lens = torch.tensor(out_lens, dtype=torch.int32, device=xs_origin_lens.device)
         offset += xs_lens.to(offset.device)
         if has_cache:
@@ -140,8 +158,63 @@ class ChunkFormerEncoder:
         else:
             r_att = torch.zeros(self.num_blocks, 0, 0, 0, device=dev)
             r_cnn = torch.zeros(self.num_blocks, 0, 0, device=dev)
-        self._last_plan = (plan, plan_dev)   # keep the uploaded plan alive until the stream consumed it
         return out.view(N, C, d), xs_lens, n_chunks, r_att, r_cnn, offset
+
+    def _encode_masked_split(self, feats, lens, offs, mask_lens, n_chunks, parts, C, L, R, out) -> None:
+        """The masked batch as `parts` groups of consecutive utterances (balanced by chunk count),
+        group i on stream i: its front-end first, then encoder layer l once group i - 1 finished
+        layer l (cfm_encode_masked_stages).  Each group writes its own rows of `out` (the batch's
+        chunk order is utterance order), so the result is bit-identical to the single launch
+        sequence: every kernel computes a row / chunk from that row's / chunk's inputs alone.  The
+        groups' kernels overlap where a launch leaves CUs idle (tail rounds, the LayerNorm / GEMM
+        boundaries): 240 min on one MI355X 50.9 -> 49.6 ms (tools/split_bench.py, 2 groups; 3 and 4
+        groups gain less); in bench.py runs 50.3-50.5 -> 49.4-50.4 ms."""
+        nb, dev = self.num_blocks, self.device
+        total = sum(n_chunks)
+        cuts, acc, k = [0], 0, 1
+        for u, n in enumerate(n_chunks):
+            acc += n
+            if k < parts and acc >= total * k / parts and u + 1 < len(n_chunks):
+                cuts.append(u + 1)
+                k += 1
+        cuts.append(len(n_chunks))
+        cur = torch.cuda.current_stream(dev)
+        while len(self._split_streams) < len(cuts) - 1:
+            self._split_streams.append(torch.cuda.Stream(dev))
+            self._split_ws.append(None)
+        jobs, f0, c0 = [], 0, 0
+        for i in range(len(cuts) - 1):
+            a, b = cuts[i], cuts[i + 1]
+            ls, ml = lens[a:b], mask_lens[a:b]
+            plan, nc, _ = _lib.plan_masked(ls, offs[a:b], C, L, R, mask_lens=None if ls == ml else ml)
+            n, F = sum(nc), sum(ls)
+            wsb = int(_lib.cfm_workspace_bytes_masked(self._h, n, C, L, R))
+            if self._split_ws[i] is None or self._split_ws[i].numel() < wsb:
+                self._split_ws[i] = None
+                self._split_ws[i] = torch.empty(wsb, dtype=torch.uint8, device=dev)
+            jobs.append((plan, self._upload(plan), feats[f0: f0 + F], out[c0 * C: (c0 + n) * C], wsb, i))
+            f0, c0 = f0 + F, c0 + n
+        for i in range(len(jobs)):
+            self._split_streams[i].wait_stream(cur)   # features, plans, output allocated on `cur`
+        prev = None
+        for plan, plan_dev, fe, o, wsb, i in jobs:
+            st = self._split_streams[i]
+            ws = self._split_ws[i]
+            evs = []
+            for stage in range(-1, nb):
+                if stage >= 0 and prev is not None:
+                    st.wait_event(prev[stage])
+                _lib.check(_lib.cfm_encode_masked_stages(self._h, fe.data_ptr(), plan.data_ptr(), plan_dev.data_ptr(),
+                                                         None, None, 0, None, None, o.data_ptr(), ws.data_ptr(), wsb,
+                                                         stage, stage, st.cuda_stream))
+                if stage >= 0:
+                    e = torch.cuda.Event()
+                    e.record(st)
+                    evs.append(e)
+            prev = evs
+        for i in range(len(jobs)):
+            cur.wait_stream(self._split_streams[i])
+        self._last_split = [(j[0], j[1]) for j in jobs]   # uploaded plans stay alive until consumed
 
     def _encode_masked_raw(self, feats, plan, plan_dev, aci, cci, trunc, aco, cco, out, ws) -> None:
         """One cfm_encode_masked launch sequence on the current stream: no allocation and no host

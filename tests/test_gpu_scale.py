@@ -108,6 +108,28 @@ def test_golden_utterances_inside_bench_batch(large, dtype, minutes):
             assert (i == ei).mean() >= 0.99
 
 
+@pytest.mark.parametrize("dtype,minutes,parts", [("bf16", 240, 2), ("fp32", 60, 3)])
+def test_stream_split_bit_identical(large, dtype, minutes, parts):
+    """forward_parallel_chunk runs a large masked batch as utterance groups on separate streams,
+    staggered by encoder layer (encoder.py _encode_masked_split); the rows must equal the single
+    launch sequence's bit for bit (every kernel computes a row / chunk from its own inputs)."""
+    g, _, models = large
+    enc = models[dtype]
+    xs, _ = _embedded_batch(g, minutes, enc.device)
+    lens = torch.tensor([x.shape[0] for x in xs], dtype=torch.int32)
+    saved = (enc.stream_split, enc.split_min_chunks)
+    try:
+        enc.set_option("stream_split", 1)
+        ref = enc.forward_parallel_chunk(xs, lens, 64, 128, 128)[0]
+        enc.set_option("stream_split", parts)
+        enc.set_option("split_min_chunks", 0)
+        out = enc.forward_parallel_chunk(xs, lens, 64, 128, 128)[0]
+        torch.cuda.synchronize()
+        assert torch.equal(out, ref)
+    finally:
+        enc.stream_split, enc.split_min_chunks = saved
+
+
 def test_frontend_window_groups_forced(large):
     """Cap the front-end at 2 windows per group (per-model option): the 30 s utterance's 6
     windows then run in 3 groups whose offsets into the intermediate buffers are > 0."""
