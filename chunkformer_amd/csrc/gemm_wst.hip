@@ -6,8 +6,8 @@
 // byte filled, and its per-CU L2 -> LDS fill rate caps it well below the MFMA rate.  With K = 512 a
 // 256-column weight tile is 256 KiB of bf16: spread over the 4 waves of a CU (one wave per SIMD,
 // 512 registers each) it fits in registers, 256 AGPRs per lane.  Only A is streamed, 64 rows x 512
-// per 64 x 256 output tile: 256 FLOP per byte filled, and a 16-slot LDS ring keeps 15 K-steps
-// (120 KiB) of A in flight per CU.
+// per 64 x 256 output tile: 256 FLOP per byte filled, and a 16-slot LDS ring keeps 14 K-steps
+// (112 KiB) of A in flight per CU.
 //
 //   * block = 4 waves (256 threads), one per CU; wave w owns output columns 64w .. 64w+63 of the
 //     block's column tile: W fragments wf[n-block 0..3][k32 0..15] (bf16x8), loaded once;
@@ -36,7 +36,12 @@ constexpr int WST_KS = 64;              // K per step
 constexpr int WST_NK = WST_K / WST_KS;  // 8 steps per tile
 constexpr int WST_SLOT = WST_MT * WST_KS * 2;   // 8 KiB
 constexpr int WST_NSLOT = 16;
-constexpr int WST_DEPTH = WST_NSLOT - 1;         // steps in flight ahead of the one being read
+#ifndef WSP_BARP
+#define WSP_BARP 2   // K-steps per barrier (1, 2 or 4): the DMA runs 16 - WSP_BARP steps ahead and refills
+                     // the slot of step y - WSP_BARP, so only every WSP_BARP-th step needs the barrier
+#endif
+constexpr int WST_DEPTH = WST_NSLOT - WSP_BARP;   // steps in flight ahead of the one being read
+static_assert(WSP_BARP == 1 || WSP_BARP == 2 || WSP_BARP == 4, "barrier period");
 }  // namespace
 
 #ifndef WSP_LGKM
@@ -63,7 +68,7 @@ CFM_DEV void mfma_wa(f32x4& acc, const bf16x8& w, const bf16x8& a) {
 // Software pipelining ("wsp"): with ONE wave per SIMD nothing else hides the non-MFMA work, so
 // every K-step is laid out by hand as 32 MFMA gaps:
 //   * the 8 ds_read_b128 of the NEXT step's A fragments sit in gaps 0, 2, .., 14;
-//   * the 2 LDS-DMA pieces of step y + 15 in gaps 6 and 22;
+//   * the 2 LDS-DMA pieces of step y + 14 in gaps 6 and 22 (one barrier per two steps);
 //   * the PREVIOUS tile's epilogue (bias-seeded accumulators double-buffered: the tile computes
 //     into acc[BUF] while acc[1 - BUF] is drained) is cut into micro-ops (scale, exp2, +1, rcp,
 //     mul, pack, permlane16 swap, one 16-B store, re-seed) spread evenly over the gaps, one
@@ -437,14 +442,22 @@ __global__ __launch_bounds__(256, 1) void gemm_wsp_kernel(const bf16* __restrict
     sfor<0, WST_NK>([&](auto KSc) {
       constexpr int KS = decltype(KSc)::value;
       constexpr int slot_n = (8 * BUF + KS + 1) % WST_NSLOT;          // next step's slot (read)
-      constexpr int slot_d = (8 * BUF + KS + WST_DEPTH) % WST_NSLOT;  // step y + 15's slot (DMA)
+      constexpr int slot_d = (8 * BUF + KS + WST_DEPTH) % WST_NSLOT;  // step y + DEPTH's slot (DMA)
       constexpr int n_ops = wsp_nops<EPI, ACT>(KS);
       // step y+1 landed (2 pieces per step, issued unconditionally -- past the block's end they
       // land in dead slots -- so exactly 28 loads are younger-or-equal here) and, after the
       // barrier, every wave's pieces of it; every wave is also past its reads of slot y-1, which
       // the DMA below refills
-      if constexpr (DIAG != 2 && DIAG != 4) WST_VMCNT(26);
-      if constexpr (DIAG != 10) asm volatile("s_barrier" ::: "memory");
+      // every WSP_BARP-th step: steps y+1 .. y+WSP_BARP landed (the younger DMA steps y+WSP_BARP+1 ..
+      // y+DEPTH-1 may be in flight, 2 pieces each), then one barrier for all of them
+      if constexpr (KS % WSP_BARP == 0) {
+        if constexpr (DIAG != 2 && DIAG != 4) {
+          if constexpr (WSP_BARP == 1) WST_VMCNT(26);
+          else if constexpr (WSP_BARP == 2) WST_VMCNT(22);
+          else WST_VMCNT(14);
+        }
+        if constexpr (DIAG != 10) asm volatile("s_barrier" ::: "memory");
+      }
       bf16x8(&cur)[4][2] = afr[KS & 1];
       bf16x8(&nxt)[4][2] = afr[(KS + 1) & 1];
       sfor<0, 32>([&](auto Ic) {
@@ -456,7 +469,7 @@ __global__ __launch_bounds__(256, 1) void gemm_wsp_kernel(const bf16* __restrict
           lds_read_into<(slot_n & 7) * WST_SLOT + rmb * 2048>(nxt[rmb][rkh], rdb[slot_n >> 3][rkh]);
         }
         if constexpr ((i == 6 || i == 22) && DIAG != 4)
-          issue_piece(KS == 0 ? dA1 : dA2, std::integral_constant<int, i == 22 ? 1 : 0>{},
+          issue_piece(KS < WSP_BARP ? dA1 : dA2, std::integral_constant<int, i == 22 ? 1 : 0>{},
                       std::integral_constant<int, (KS + WST_DEPTH) % WST_NK>{},
                       std::integral_constant<int, slot_d>{});
         sfor<wsp_lo(i, n_ops), wsp_lo(i + 1, n_ops)>([&](auto Oc) { epi_op(KSc, Oc, acc[1 - BUF], sd, sdp, std::true_type{}); });
@@ -493,7 +506,9 @@ __global__ __launch_bounds__(256, 1) void gemm_wsp_kernel(const bf16* __restrict
 
   // prologue: weights in AGPRs (s_nop: AGPR writes -> MFMA reads), step 0 landed, its fragments read
   asm volatile("s_nop 7" ::: "memory");
-  WST_VMCNT(28);
+  if constexpr (WSP_BARP == 1) WST_VMCNT(28);   // step 0 landed: DEPTH - 1 younger steps in flight
+  else if constexpr (WSP_BARP == 2) WST_VMCNT(26);
+  else WST_VMCNT(22);
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // + the bias in LDS
 #pragma unroll
   for (int nb = 0; nb < 4; ++nb)
