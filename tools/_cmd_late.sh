@@ -1,0 +1,17 @@
+# A/B: 256x256 GEMM, group 0's DMA wait after (product) / before (early) its MFMA segment
+set -e
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+VD=$GRAFT_REPO_ROOT/chunkformer_amd/_build/variants
+timeout -k 10 300 python3 -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_ops.py 2>&1 | tail -1
+for r in 1 2; do
+  for v in early prod; do
+    if [ $v = prod ]; then unset CFM_LIB; else export CFM_LIB=$VD/libcfm_$v.so; fi
+    echo "== $v"; timeout -k 10 120 python3 tools/gemm_bench.py --iters 20 --only ffn_w2 2>&1 | grep -v amdgpu.ids
+  done
+done
+for v in early prod early prod; do
+  if [ $v = prod ]; then unset CFM_LIB; else export CFM_LIB=$VD/libcfm_$v.so; fi
+  timeout -k 10 300 python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline > gpurun_out/late_b.json 2>/dev/null
+  python3 -c "import json; d=json.loads(open('gpurun_out/late_b.json').read().strip().splitlines()[-1]); b=d['breakdown_ms']; print('$v', d['value'], d['ms_per_step'], b['ffn_w2_gemm'], b['frontend_pw_gemm'])"
+done
