@@ -51,7 +51,7 @@ static_assert(WSP_BARP == 1 || WSP_BARP == 2 || WSP_BARP == 4, "barrier period")
 #define WSP_FULLROW 1   // 0: permlane-swapped 64-B row pieces stored per step (A/B)
 #endif
 #ifndef WSP_FULLROW_ACT
-#define WSP_FULLROW_ACT 0   // 1: also the SiLU / ReLU epilogues (A/B)
+#define WSP_FULLROW_ACT 1   // also the SiLU / ReLU epilogues (0: permlane-swapped 64-B pieces there; A/B)
 #endif
 #define WST_VMCNT(N) asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory")
 
@@ -107,10 +107,10 @@ constexpr int wsp_half() { return (ACT == ACT_SILU ? 20 : ACT == ACT_RELU ? 4 : 
 // of the 4 packed columns into the wave's 16 x 64 staging tile, the re-seed; an odd group then
 // reads the tile back as full 128-B rows (2 x ds_read_b128: rows 0-7, 8-15) and the next (even)
 // group stores them first thing (its step opened with lgkmcnt(0)).  2H + 4 ops either way.
-// Used where it measured faster (one-process A/B, tools/gemm_bench.py): QKV 285 -> 251 us,
-// out-proj / pw2 91 -> 89 us; the SiLU (FFN w1, N = 2048) and ReLU (front-end pw, N = 512)
-// epilogues measured 2-6% slower with it (WSP_FULLROW_ACT=1), so they keep the swapped 64-B pieces
-// (the same ReLU epilogue at N = 2048 gains 12%: the wider the layer, the more the store shape counts).
+// Used everywhere: one-process A/B (tools/gemm_bench.py) QKV 285 -> 251 us, out-proj / pw2 91 -> 89 us.
+// On random-data microbenchmarks (power-limited clocks) the SiLU / ReLU epilogues measured 2-6% slower
+// with it, but in the bench step (real activations, 2.3 GHz) FFN w1 9.1 -> 8.3 ms/step and the
+// front-end pointwise GEMMs 5.2 -> 4.8 ms/step (3 interleaved runs each), so it is on there too.
 template <int EPI, int ACT>
 constexpr bool wsp_fullrow() {
   return WSP_FULLROW && (EPI == EPI_QKV || (EPI == EPI_STORE && (ACT == ACT_NONE || WSP_FULLROW_ACT)));
