@@ -31,6 +31,9 @@
 
 namespace cfm {
 
+#ifndef G256_FULLROW
+#define G256_FULLROW 1   // EPI_STORE epilogue through LDS as full 128-B row stores (A/B: 0 = 64-B pieces)
+#endif
 // DIAG: 0 = normal; 1 = skip MFMAs (DMA + epilogue only); 2 = skip DMA inside the loop (MFMA on stale LDS);
 // 3 = skip the epilogue (no bias/activation/stores)
 template <int EPI, int ACT, int DIAG = 0>
@@ -135,7 +138,16 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_256_kernel(const bf16* __res
         // ================= LOAD segment: (epilogue of the previous tile), fragments of (s, ss), DMA issue
         if (ss == 0 && kt == 0) {
           if (epi_t >= 0) {
-            if constexpr (DIAG != 3) tile_epilogue<EPI, ACT>(acc, tile_m(epi_t), tile_n(epi_t), wm, wn, fr, g, M, ep);
+            if constexpr (DIAG != 3) {
+              if constexpr (EPI == EPI_STORE && G256_FULLROW)
+                // staging in A slot (s + 2) % 3: A(s - 1) there was read by both groups' last LOAD
+                // segments, and A(s + 2) is issued only in the ss = 1 LOAD segment, after the barrier
+                // that ends this segment for both groups
+                wave_epilogue_fullrow<ACT>(acc, tile_m(epi_t) * 256 + wm * 128, tile_n(epi_t) * 256 + wn * 64, fr, g,
+                                           lane, M, ep, lds_base + (unsigned)(((s + 2) % 3) * 32768 + wid * 2304));
+              else
+                tile_epilogue<EPI, ACT>(acc, tile_m(epi_t), tile_n(epi_t), wm, wn, fr, g, M, ep);
+            }
             epi_t = -1;
           }
           seed_bias(acc, ep.bias, tile_n(t), wn, g);
@@ -187,7 +199,16 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_256_kernel(const bf16* __res
     }
   }
   // last tile's epilogue (no MFMA partner left), then rebalance the barrier count
-  if (epi_t >= 0 && DIAG != 3) tile_epilogue<EPI, ACT>(acc, tile_m(epi_t), tile_n(epi_t), wm, wn, fr, g, M, ep);
+  if (epi_t >= 0 && DIAG != 3) {
+    if constexpr (EPI == EPI_STORE && G256_FULLROW) {
+      // every DMA has landed and been read; the other group only runs MFMAs from here on
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      wave_epilogue_fullrow<ACT>(acc, tile_m(epi_t) * 256 + wm * 128, tile_n(epi_t) * 256 + wn * 64, fr, g, lane, M,
+                                 ep, lds_base + (unsigned)(((s + 2) % 3) * 32768 + wid * 2304));
+    } else {
+      tile_epilogue<EPI, ACT>(acc, tile_m(epi_t), tile_n(epi_t), wm, wn, fr, g, M, ep);
+    }
+  }
   if (grp == 0) asm volatile("s_barrier" ::: "memory");
 }
 

@@ -136,6 +136,40 @@ CFM_DEV void wave_epilogue(f32x4 (&acc)[4][MB], int m0, int nw, int g, int M, co
   }
 }
 
+// EPI_STORE through an LDS staging tile (per wave 16 rows x 144 B): each m-block's four 4-column
+// pieces per lane are written with ds_write_b64, read back as full 128-B row pieces (8 rows per
+// read) and stored as whole lines, instead of 16-row x 64-B pieces after permlane swaps.
+template <int ACT>
+CFM_DEV void wave_epilogue_fullrow(f32x4 (&acc)[4][8], int row0, int nw, int fr, int g, int lane, int M,
+                                   const EpiArgs& ep, unsigned stg) {
+  constexpr int PITCH = 144;
+  bf16* base = reinterpret_cast<bf16*>(ep.out) + (size_t)ep.row_off * ep.ldo + nw;
+  const unsigned wr = stg + (unsigned)(fr * PITCH + 8 * g);
+  const unsigned rd = stg + (unsigned)((lane >> 3) * PITCH + 16 * (lane & 7));
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const f32x4 v = act4<ACT>(acc[i][j]);
+      asm volatile("ds_write_b64 %0, %1 offset:%2" ::"v"(wr), "v"((u32x2_t){pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3])}),
+                   "i"(32 * i) : "memory");
+    }
+    u32x4 r[2];
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+      asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r[b]) : "v"(rd), "i"(8 * PITCH * b) : "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      const int m = row0 + 16 * j + (lane >> 3) + 8 * b;
+      if (m >= M) continue;
+      u32x4* p = reinterpret_cast<u32x4*>(base + (size_t)m * ep.ldo + 8 * (lane & 7));
+      if (ep.store_mode == 2) __builtin_nontemporal_store(r[b], p);
+      else *p = r[b];
+    }
+  }
+}
+
 template <int EPI, int ACT, bool NOST = false>
 CFM_DEV void tile_epilogue(f32x4 (&acc)[4][8], int tm, int tn, int wm, int wn, int fr, int g, int M,
                            const EpiArgs& ep) {
