@@ -244,6 +244,9 @@ CFM_DEV unsigned pack_bf16x2_a(float a, float b) {
   return __builtin_bit_cast(unsigned, (b2){(bf16)a, (bf16)b});
 }
 CFM_DEV int sw128(int row, int ch) { return row * 128 + ((ch ^ ((row >> 1) & 7)) << 4); }
+#ifndef ATTN_STORE16
+#define ATTN_STORE16 1   // ring kernel output as 16-B stores after permlane swaps (A/B: 0 = 8-B stores)
+#endif
 
 __global__ __launch_bounds__(512, 1) void chunk_attention_ring_kernel(
     const bf16* __restrict__ Q, const bf16* __restrict__ KV, int kv_rows, const bf16* __restrict__ P, int p_rows,
@@ -537,12 +540,26 @@ __global__ __launch_bounds__(512, 1) void chunk_attention_ring_kernel(
       const bool live = qi < q_valid && l > 0.f;
       const float inv = live ? 1.f / l : 0.f;
       bf16* op = out + (size_t)(q_row0 + qi) * d + h * 64;
+#if ATTN_STORE16
+      // dim pairs (16 nt .. +15, 16 (nt+1) ..): one permlane16 swap per packed dword leaves lane g with
+      // 8 contiguous dims, so each query row leaves as two 64-B pieces (2 x 16-B stores per lane)
+#pragma unroll
+      for (int pr = 0; pr < 2; ++pr) {
+        const unsigned x0 = pack_bf16x2_a(O[2 * pr][0] * inv, O[2 * pr][1] * inv), x1 = pack_bf16x2_a(O[2 * pr][2] * inv, O[2 * pr][3] * inv);
+        const unsigned y0 = pack_bf16x2_a(O[2 * pr + 1][0] * inv, O[2 * pr + 1][1] * inv),
+                       y1 = pack_bf16x2_a(O[2 * pr + 1][2] * inv, O[2 * pr + 1][3] * inv);
+        const auto r0 = __builtin_amdgcn_permlane16_swap(x0, y0, false, false);
+        const auto r1 = __builtin_amdgcn_permlane16_swap(x1, y1, false, false);
+        *reinterpret_cast<u32x4*>(op + 32 * pr + 16 * (g & 1) + 8 * (g >> 1)) = (u32x4){r0[0], r1[0], r0[1], r1[1]};
+      }
+#else
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt) {
         typedef bf16 bf16x4 __attribute__((ext_vector_type(4)));
         *reinterpret_cast<bf16x4*>(op + 16 * nt + 4 * g) =
             (bf16x4){(bf16)(O[nt][0] * inv), (bf16)(O[nt][1] * inv), (bf16)(O[nt][2] * inv), (bf16)(O[nt][3] * inv)};
       }
+#endif
     }
     // ---- the prefetched rows replace the first 2C rows of this pair's windows (no longer needed)
     __syncthreads();
