@@ -839,16 +839,29 @@ __global__ __launch_bounds__(512, 1) void full_attention_bf16_kernel(
     }
   }
   const int qi = i0 + fr;
-  if (qi >= nq) return;
   const bool live = qi < q_valid && l > 0.f;
   const float inv = live ? 1.f / l : 0.f;
   bf16* op = out + ((size_t)q_row0 + qi) * d + h * 64;
+#if ATTN_STORE16
+  // as the ring kernel: 16-B stores after permlane16 swaps (every lane takes part in the swaps)
+#pragma unroll
+  for (int pr = 0; pr < 2; ++pr) {
+    const unsigned x0 = pack_bf16x2_a(O[2 * pr][0] * inv, O[2 * pr][1] * inv), x1 = pack_bf16x2_a(O[2 * pr][2] * inv, O[2 * pr][3] * inv);
+    const unsigned y0 = pack_bf16x2_a(O[2 * pr + 1][0] * inv, O[2 * pr + 1][1] * inv),
+                   y1 = pack_bf16x2_a(O[2 * pr + 1][2] * inv, O[2 * pr + 1][3] * inv);
+    const auto r0 = __builtin_amdgcn_permlane16_swap(x0, y0, false, false);
+    const auto r1 = __builtin_amdgcn_permlane16_swap(x1, y1, false, false);
+    if (qi < nq) *reinterpret_cast<u32x4*>(op + 32 * pr + 16 * (g & 1) + 8 * (g >> 1)) = (u32x4){r0[0], r1[0], r0[1], r1[1]};
+  }
+#else
+  if (qi >= nq) return;
 #pragma unroll
   for (int nt = 0; nt < 4; ++nt) {
     typedef bf16 bf16x4 __attribute__((ext_vector_type(4)));
     *reinterpret_cast<bf16x4*>(op + 16 * nt + 4 * g) =
         (bf16x4){(bf16)(O[nt][0] * inv), (bf16)(O[nt][1] * inv), (bf16)(O[nt][2] * inv), (bf16)(O[nt][3] * inv)};
   }
+#endif
 }
 
 // -1 when not eligible (T' > 384, dk != 64): the caller uses chunk_attention_kernel.  `nd` = the
