@@ -183,6 +183,52 @@ def committed_mfma_busy(cls: str = "ffn_w1_gemm"):
         return None, None, None
 
 
+def class_rooflines(prof, n_chunks: int, cfg, dtype: str, profiled: bool):
+    """Per kernel class of one profiled step: ms, launches and the roofline fraction -- MFMA classes
+    against the dense peak from their algorithmic FLOPs (SURVEY 8(d) per-chunk terms), HBM classes
+    against 8 TB/s from the committed PMC bytes per launch (only on the profiled workload)."""
+    d, ff, nb, Cc = cfg.d_model, cfg.ffn_dim, cfg.num_blocks, C
+    rows = n_chunks * Cc
+    W = L + Cc + R
+    flops = {
+        "ffn_w1_gemm": 2.0 * rows * ff * d * 2 * nb, "ffn_w2_gemm": 2.0 * rows * ff * d * 2 * nb,
+        "qkv_gemm": 2.0 * rows * 3 * d * d * nb, "out_proj_gemm": 2.0 * rows * d * d * nb,
+        "pw1_glu_gemm": 2.0 * rows * 2 * d * d * nb, "pw2_gemm": 2.0 * rows * d * d * nb,
+        "chunk_attention": 2.0 * n_chunks * Cc * d * (W + (L + 2 * Cc + R - 1) + W) * nb,
+        "frontend_pw_gemm": 2.0 * n_chunks * (d * d * (2 * Cc + 1) * 19 + d * d * Cc * 9 + Cc * 9 * d * d),
+    }
+    hbm = {"layernorm": ("layernorm", "layernorm2"), "frontend_dw2": ("frontend_dw2",),
+           "conv_dw_ln_silu": ("conv_dw_ln_silu",), "frontend_conv0_dw": ("frontend_conv0_dw",)}
+    traffic = {}
+    if profiled:
+        import glob
+        files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_traffic.json")))
+        if files:
+            try:
+                traffic = json.load(open(files[-1]))["kernels"]
+            except (OSError, ValueError, KeyError):
+                traffic = {}
+    out = {}
+    for cls, (ms, n) in prof.items():
+        if not n:
+            continue
+        ent = {"ms_per_step": round(ms, 3), "launches": n}
+        if cls in flops:
+            ach = flops[cls] / (ms / 1e3) / 1e12
+            ent.update(bound="mfma", achieved_tflops=round(ach, 1), frac=round(ach / PEAK_TFLOPS[dtype], 3))
+        elif cls in hbm and traffic:
+            # PMC bytes per launch x launches of each kernel of the class (LN: ln_kernel and ln2_kernel)
+            tot = sum(e["hbm_bytes_per_launch"] * e["dispatches"] for k in hbm[cls] for e in traffic.get(k, []))
+            disp = sum(e["dispatches"] for k in hbm[cls] for e in traffic.get(k, []))
+            if disp:
+                per_step = tot / disp * n
+                ach = per_step / (ms / 1e3) / 1e9
+                ent.update(bound="hbm", achieved_gbs=round(ach, 1), frac=round(ach / 8000.0, 3),
+                           pmc_bytes_per_step=round(per_step))
+        out[cls] = ent
+    return out
+
+
 def apply_opts(enc, opts):
     for kv in opts:
         k, v = kv.split("=")
@@ -406,14 +452,16 @@ def main():
         dist.all_reduce(te, op=dist.ReduceOp.MAX)
     e2e_ms = float(te.item()) / args.steps * 1e3
 
-    breakdown = None
+    breakdown = by_class = None
     if not args.no_breakdown:
         enc.set_option("profile_reset", 1)
         enc.set_option("profile", (1 << len(_lib.PROFILE_CLASSES)) - 1)
         step()
         torch.cuda.synchronize()
         enc.set_option("profile", 0)
-        breakdown = {k: round(v[0], 3) for k, v in _lib.profile_read(enc._h).items() if v[1]}
+        prof_all = _lib.profile_read(enc._h)
+        breakdown = {k: round(v[0], 3) for k, v in prof_all.items() if v[1]}
+        by_class = class_rooflines(prof_all, n_chunks, cfg, args.dtype, profiled)
 
     if rank == 0:
         res = {
@@ -468,6 +516,7 @@ def main():
                                 (" + ids all_gather_into_tensor and per-utterance reassembly" if world > 1 else "")),
             "allgather_logp_bf16_ms": round(gather_lp_ms, 3) if gather_lp_ms is not None else None,
             "breakdown_ms": breakdown,
+            "roofline_by_class": by_class,
         }
         if world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(lens_all)
