@@ -38,7 +38,7 @@ enum { SITE_QKV = 1, SITE_OPROJ = 2, SITE_PW2 = 4, SITE_FFN2 = 8, SITE_FFN1 = 16
 struct Tuning {
   int gemm_diag = 0, gemm_wst = 1, store_mode = 0, col_group = 0;
   int attn_reuse = 1;            // ring attention: band subtile carried between key tiles
-  int conv_dot2 = 1;             // conv module: bf16 dot2 kernel (0: per-tap f32 kernel)
+  int conv_dot2 = 2;             // conv module: bf16 dot2 kernel in half-chunk blocks (1: one block per chunk, 0: per-tap f32)
   int conv_dma = 1;              // conv module: LDS-DMA window staging (0: register staging)
   int dw2_seg = 4;               // front-end dw2: row segments per walk
   int attn128_var = 1;           // head_dim 128 attention kernel variant (A/B)

@@ -188,15 +188,18 @@ CFM_DEV unsigned pk_bf16(float lo, float hi) {
   return __builtin_bit_cast(unsigned, (bf16x2_t){(__bf16)lo, (__bf16)hi});
 }
 // the compute half of the dot2 kernels: wave w's RW output rows from the staged window `win`
+// (`w` indexes RW-row groups of the chunk; the staged window starts at window row win_row0)
 template <int VPL>
 CFM_DEV void conv_dot2_rows(const bf16* __restrict__ win, int nout, int out_row0, const float* __restrict__ wdw,
                             const float* __restrict__ bdw, const float* __restrict__ lnw,
-                            const float* __restrict__ lnb, float eps, bf16* __restrict__ out, int w, int lane) {
+                            const float* __restrict__ lnb, float eps, bf16* __restrict__ out, int w, int lane,
+                            int win_row0 = 0) {
   constexpr int d = VPL * 64, NW = VPL / 2;
   constexpr int RW = 8;
   typedef bf16 bvec __attribute__((ext_vector_type(VPL)));
   const int i0 = w * RW;
   if (i0 >= nout) return;
+  win -= (size_t)win_row0 * d;   // rows below win_row0 are never read
   const int c0 = lane * VPL;
   // tap-pair weights: wp[p][e] = (w[2p][c0 + e], w[2p + 1][c0 + e]) as bf16x2, w[15] = 0
   unsigned wp[8][VPL];
@@ -326,12 +329,66 @@ __global__ __launch_bounds__(512) void conv_dw_ln_silu_dot2_kernel(const bf16* _
 }
 
 
+// Half-chunk blocks: the dot2 kernel needs 243 VGPRs (2 waves per SIMD), so one 8-wave block holds
+// a whole CU and every chunk's window DMA waits with no other work on the CU.  Here a 4-wave block
+// takes 32 output rows of a chunk (window rows 32h .. 32h + 46, 47 KiB), two blocks share a CU and
+// one block's window DMA overlaps the other's arithmetic; the 14 overlap rows are read twice.
+template <int VPL, int QR>
+__global__ __launch_bounds__(QR * 8) void conv_dw_ln_silu_dot2h_kernel(const bf16* __restrict__ glu,
+                                                                    const int32_t* __restrict__ desc,
+                                                                    const float* __restrict__ wdw,
+                                                                    const float* __restrict__ bdw,
+                                                                    const float* __restrict__ lnw,
+                                                                    const float* __restrict__ lnb, float eps,
+                                                                    bf16* __restrict__ out) {
+  constexpr int d = VPL * 64, NWV = QR / 8;
+  constexpr int HJ = QR + 15;   // window rows of the block (+ the zero row of the w[15] = 0 tap)
+  __shared__ __attribute__((aligned(16))) bf16 win[HJ * d];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int half = blockIdx.y;
+  const int32_t* D = desc + (size_t)blockIdx.x * CD_INTS;
+  const int out_row0 = D[CD_OUT_ROW0], nout = D[CD_NOUT], src0 = D[CD_SRC_ROW0];
+  if (QR * half >= nout) return;
+  const int nj = nout + 14;
+  const int jlo = max(D[CD_J_LO], 0), jhi = min(D[CD_J_HI], nj);
+  const int r0 = QR * half;
+  if (VPL == 8) {
+    for (int jj = __builtin_amdgcn_readfirstlane(w); jj < HJ; jj += NWV) {
+      const int j = r0 + jj;
+      if (j >= jlo && j < jhi)
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(glu + (size_t)(src0 + j) * d + lane * 8),
+                                         (__attribute__((address_space(3))) void*)(win + jj * d), 16, 0, 0);
+      else
+        *reinterpret_cast<u32x4*>(win + jj * d + lane * 8) = (u32x4){0u, 0u, 0u, 0u};
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  } else {
+    constexpr int V8 = d / 8;
+    for (int idx = tid; idx < HJ * V8; idx += QR * 8) {
+      const int jj = idx / V8, v = idx % V8, j = r0 + jj;
+      u32x4 val = (u32x4){0u, 0u, 0u, 0u};
+      if (j >= jlo && j < jhi) val = *reinterpret_cast<const u32x4*>(glu + (size_t)(src0 + j) * d + v * 8);
+      *reinterpret_cast<u32x4*>(win + jj * d + v * 8) = val;
+    }
+  }
+  __syncthreads();
+  conv_dot2_rows<VPL>(win, nout, out_row0, wdw, bdw, lnw, lnb, eps, out, NWV * half + w, lane, r0);
+}
+
 template <typename T>
 int conv_dw_ln_silu(const T* glu, const int32_t* desc, int nblk, int d, const float* wdw_t, const float* bdw,
                     const float* lnw, const float* lnb, float eps, T* out, hipStream_t st, int dot2, int dma) {
   if (nblk <= 0) return 0;
   // dot2 = 0: the per-tap f32 kernel; dma = 0: stage the window through registers (A/B, model options)
   if constexpr (std::is_same<T, bf16>::value) {
+    if (dot2 >= 2 && d == 512) {   // half-chunk blocks (conv_dot2 = 2), quarter-chunk blocks (3)
+      if (dot2 == 3)
+        hipLaunchKernelGGL((conv_dw_ln_silu_dot2h_kernel<8, 16>), dim3(nblk, 4), dim3(128), 0, st, glu, desc, wdw_t, bdw, lnw, lnb, eps, out);
+      else
+        hipLaunchKernelGGL((conv_dw_ln_silu_dot2h_kernel<8, 32>), dim3(nblk, 2), dim3(256), 0, st, glu, desc, wdw_t, bdw, lnw, lnb, eps, out);
+      CFM_CHECK_LAUNCH();
+      return 0;
+    }
     if (dot2) {
       if (d == 128) hipLaunchKernelGGL((conv_dw_ln_silu_dot2_kernel<2>), dim3(nblk), dim3(512), 0, st, glu, desc, wdw_t, bdw, lnw, lnb, eps, out, dma);
       else if (d == 256) hipLaunchKernelGGL((conv_dw_ln_silu_dot2_kernel<4>), dim3(nblk), dim3(512), 0, st, glu, desc, wdw_t, bdw, lnw, lnb, eps, out, dma);
