@@ -1,0 +1,42 @@
+"""Timing of the RNN-T greedy consumer (cfm_rnnt_greedy) on synthetic encoder rows: B utterances of
+T frames each (B = 1: endless_decode's single long utterance; B > 1: batch_decode), seeded
+synthetic predictor / joint weights.  Prints frames/s and emissions per frame.
+
+    python tools/rnnt_bench.py --frames 500 --batch 1
+"""
+import argparse
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from chunkformer_amd.transducer import RNNTConfig, RNNTGreedy, synthetic_transducer_state_dict  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--frames", type=int, default=45000)
+    ap.add_argument("--batch", type=int, default=1)
+    a = ap.parse_args()
+    c = RNNTConfig()
+    g = RNNTGreedy(c, synthetic_transducer_state_dict(c, 0), device="cuda")
+    gen = torch.Generator(device="cuda").manual_seed(3)
+    B, T = a.batch, a.frames
+    enc = torch.randn(B * T, c.enc_dim, generator=gen, device="cuda")
+    starts = [b * T for b in range(B)]
+    lens = [T] * B
+    g.greedy_packed(enc[: min(B * T, 2000)], [0], [min(T, 2000)])   # warm-up
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    out = g.greedy_packed(enc, starts, lens)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    emis = int((out != c.blank).sum().item()) if out.dtype != torch.bool else 0
+    print(f"B={B} T={T}: {dt * 1e3:.1f} ms, {B * T / dt:.0f} frames/s, {emis / (B * T):.3f} emissions per frame, "
+          f"{dt * 1e3 / max(emis / B, 1):.3f} ms per emission per utterance")
+
+
+if __name__ == "__main__":
+    main()
