@@ -9,7 +9,7 @@ typedef __bf16 bf16;
 
 namespace cfm {
 
-enum { EPI_STORE = 0, EPI_STORE_F32 = 1, EPI_RESID = 2, EPI_QKV = 3, EPI_GLU = 4 };
+enum { EPI_STORE = 0, EPI_STORE_F32 = 1, EPI_RESID = 2, EPI_QKV = 3, EPI_GLU = 4, EPI_DW2 = 5 };
 enum { ACT_NONE = 0, ACT_RELU = 1, ACT_SILU = 2 };
 
 struct EpiArgs {
@@ -30,7 +30,15 @@ struct EpiArgs {
   int diag = 0;                  // timing diagnostics of the bf16 kernels ("gemm_diag"; 0 = normal)
   int wst = 1;                   // K = 512 weight-stationary kernel ("gemm_wst")
   int small_tiles = 0;           // force the 128 x 128 kernel (cfm_op_gemm A/B)
+  // DW2 (front-end pw1 + ReLU + dw2, K = N = 512 weight-stationary only): dw2 taps tap-major [9][N]
+  // f32, bias [N]; the pw1 rows are (window, t2 < t2n, f2 < 19); out = dw2 rows (window, t3 < t3n, f3 < 9)
+  const float* dw_w = nullptr;
+  const float* dw_b = nullptr;
+  int t2n = 0, t3n = 0;
 };
+
+int gemm_bf16_wst(int epi, int act, const bf16* A, int lda, const bf16* W, int ldw, int M, int N, int K,
+                  const EpiArgs& ep, hipStream_t st);
 
 enum { SITE_QKV = 1, SITE_OPROJ = 2, SITE_PW2 = 4, SITE_FFN2 = 8, SITE_FFN1 = 16, SITE_PW1 = 32, SITE_FE = 64 };
 
@@ -41,6 +49,7 @@ struct Tuning {
   int conv_dot2 = 2;             // conv module: bf16 dot2 kernel in half-chunk blocks (1: one block per chunk, 0: per-tap f32)
   int conv_dma = 1;              // conv module: LDS-DMA window staging (0: register staging)
   int dw2_seg = 4;               // front-end dw2: row segments per walk
+  int fe_fuse_dw2 = 0;           // front-end: pw1 + ReLU + dw2 in one weight-stationary GEMM (bf16)
   int attn128_var = 1;           // head_dim 128 attention kernel variant (A/B)
   // GEMM sites whose bf16 outputs are stored non-temporally ("nt_sites" bit mask, SITE_* below).
   // Default: FFN w2 (its y goes straight to the LayerNorm; bench A/B 52.2 -> 51.4 ms/step); nt on

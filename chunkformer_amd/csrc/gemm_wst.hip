@@ -42,6 +42,24 @@ constexpr int WST_NSLOT = 16;
 #endif
 constexpr int WST_DEPTH = WST_NSLOT - WSP_BARP;   // steps in flight ahead of the one being read
 static_assert(WSP_BARP == 1 || WSP_BARP == 2 || WSP_BARP == 4, "barrier period");
+// DW2 (front-end pw1 + ReLU + dw2): an 8-slot A ring leaves LDS for the pw1 output ring
+template <int EPI> constexpr int wst_nslot() { return EPI == EPI_DW2 ? 8 : WST_NSLOT; }
+template <int EPI> constexpr int wst_depth() { return wst_nslot<EPI>() - WSP_BARP; }
+// dw2 phase: positions per lane, tap-loop unroll, timing diagnostics (1 = no stores, 2 = no phase)
+#ifndef DW2_PPL
+#define DW2_PPL 1
+#endif
+#ifndef DW2_VUNROLL
+#define DW2_VUNROLL 1
+#endif
+#ifndef DW2_DIAG
+#define DW2_DIAG 0
+#endif
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+constexpr int DW2_RP = 528;                 // pw1 ring row pitch (256 bf16 + 16 B): conflict-free ds_write_b64
+constexpr int DW2_RING = 128 * DW2_RP;      // two 64-row tiles
+constexpr int DW2_WB = (9 + 1) * 256 * 4;   // dw2 taps [9][256] + bias [256], f32
+template <int N> CFM_DEV void wst_vmcnt() { asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory"); }
 }  // namespace
 
 #ifndef WSP_LGKM
@@ -115,9 +133,11 @@ template <int EPI, int ACT>
 constexpr bool wsp_fullrow() {
   return WSP_FULLROW && (EPI == EPI_QKV || (EPI == EPI_STORE && (ACT == ACT_NONE || WSP_FULLROW_ACT)));
 }
+// DW2 groups: per half q the activation ops, 2 packs, the ds_write_b64 into the pw1 ring, the re-seed
 template <int EPI, int ACT>
 constexpr int wsp_nops(int s) {
-  return EPI == EPI_GLU ? ((s & 1) ? 27 : 24) : wsp_fullrow<EPI, ACT>() ? 2 * wsp_half<ACT>() + 6 : 2 * wsp_half<ACT>() + 5;
+  return EPI == EPI_DW2 ? 2 * (wsp_half<ACT>() + 2)
+         : EPI == EPI_GLU ? ((s & 1) ? 27 : 24) : wsp_fullrow<EPI, ACT>() ? 2 * wsp_half<ACT>() + 6 : 2 * wsp_half<ACT>() + 5;
 }
 constexpr int wsp_lo(int i, int n) { return (i * n + 31) / 32; }   // first op of gap i
 constexpr int wsp_gap(int o, int n) {                                  // gap that carries op o
@@ -134,8 +154,8 @@ constexpr int wsp_late_seeds(int s) {
   // full-row: even groups open with the 2 deferred stores (seeds at 2 + H, 2H + 3); odd groups
   // end with the 2 row reads and then both seeds (2H + 2, 2H + 3)
   const bool fr = wsp_fullrow<EPI, ACT>();
-  const int o0 = EPI == EPI_GLU ? 22 : fr ? ((s & 1) ? 2 * H + 2 : H + 2) : H - 1;
-  const int o1 = EPI == EPI_GLU ? 23 : fr ? 2 * H + 3 : 2 * H - 1;
+  const int o0 = EPI == EPI_DW2 ? H : EPI == EPI_GLU ? 22 : fr ? ((s & 1) ? 2 * H + 2 : H + 2) : H - 1;
+  const int o1 = EPI == EPI_DW2 ? 2 * H + 1 : EPI == EPI_GLU ? 23 : fr ? 2 * H + 3 : 2 * H - 1;
   return (wsp_gap(o0, n) >= 14) + (wsp_gap(o1, n) >= 14);
 }
 }  // namespace
@@ -147,7 +167,9 @@ __global__ __launch_bounds__(256, 1) void gemm_wsp_kernel(const bf16* __restrict
   // A ring + the block's 256 bias values (the re-seed reads them straight into the accumulators)
   // + per wave a 16-row x 64-column bf16 output staging tile (144-B rows) for full-row stores
   constexpr int STG_PITCH = 144, STG_BYTES = 16 * STG_PITCH;
-  __shared__ __attribute__((aligned(16))) char smem[WST_NSLOT * WST_SLOT + 1024 + 4 * STG_BYTES];
+  constexpr int NS = wst_nslot<EPI>(), DP = wst_depth<EPI>();
+  constexpr int TAIL = EPI == EPI_DW2 ? DW2_RING + DW2_WB + 4 * 256 : 4 * STG_BYTES;
+  __shared__ __attribute__((aligned(16))) char smem[NS * WST_SLOT + 1024 + TAIL];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int fr = lane & 15, g = lane >> 4;
@@ -161,6 +183,10 @@ __global__ __launch_bounds__(256, 1) void gemm_wsp_kernel(const bf16* __restrict
   const int r0 = xr0 + (int)((long long)sub * (xr1 - xr0) / cpx);
   const int r1 = xr0 + (int)((long long)(sub + 1) * (xr1 - xr0) / cpx);
   if (r0 >= r1) return;
+  // DW2: a dw2 output needs the pw1 rows up to 40 before its last row, so the block also computes the
+  // tile before its range (halo; its outputs belong to the previous block) and emits the outputs whose
+  // last row lies in [64 r0, 64 r1)
+  const int r0c = (EPI == EPI_DW2 && r0 > 0) ? r0 - 1 : r0;
 
   // ---- A stream: buffer LDS-DMA, descriptor = the 64-row tile (rows past M read as 0, so the
   // pieces issued past the block's end need no clamp), lane offset (row, swizzled 16-B chunk)
@@ -185,8 +211,8 @@ __global__ __launch_bounds__(256, 1) void gemm_wsp_kernel(const bf16* __restrict
         ks * WST_KS * 2, 0, 0);   // K slice in soffset: the immediate offset would move the LDS side too
   };
   {
-    const __amdgpu_buffer_rsrc_t d0 = tile_rsrc(r0), d1 = tile_rsrc(r0 + 1);
-    sfor<0, WST_DEPTH>([&](auto Pc) {
+    const __amdgpu_buffer_rsrc_t d0 = tile_rsrc(r0c), d1 = tile_rsrc(r0c + 1);
+    sfor<0, DP>([&](auto Pc) {
       constexpr int P = decltype(Pc)::value;
       issue_piece(P < WST_NK ? d0 : d1, std::integral_constant<int, 0>{}, std::integral_constant<int, P % WST_NK>{}, Pc);
       issue_piece(P < WST_NK ? d0 : d1, std::integral_constant<int, 1>{}, std::integral_constant<int, P % WST_NK>{}, Pc);
@@ -201,8 +227,15 @@ __global__ __launch_bounds__(256, 1) void gemm_wsp_kernel(const bf16* __restrict
 #pragma unroll
     for (int kk = 0; kk < 16; ++kk) wf[nb][kk] = *reinterpret_cast<const bf16x8*>(wp + 32 * kk);
   }
+  if constexpr (EPI == EPI_DW2) {
+    float* dwl = reinterpret_cast<float*>(smem + NS * WST_SLOT + 1024 + DW2_RING);
+    for (int idx = tid; idx < 10 * 256; idx += 256) {
+      const int e = idx >> 8, j = idx & 255;
+      dwl[idx] = e < 9 ? ep.dw_w[(size_t)e * N + ct * 256 + j] : ep.dw_b[ct * 256 + j];
+    }
+  }
   if (tid < 64)
-    reinterpret_cast<f32x4*>(smem + WST_NSLOT * WST_SLOT)[tid] =
+    reinterpret_cast<f32x4*>(smem + NS * WST_SLOT)[tid] =
         ep.bias ? *reinterpret_cast<const f32x4*>(ep.bias + ct * 256 + 4 * tid) : (f32x4){0.f, 0.f, 0.f, 0.f};
   // output of the wave's two 32-column spans: wave-uniform base + row stride, lane offset
   // (row fr, 8 columns after the permlane swap)
@@ -253,12 +286,17 @@ __global__ __launch_bounds__(256, 1) void gemm_wsp_kernel(const bf16* __restrict
   }
 
   // lane's bias f32x4 of n-block nb at bias_lds + 64 nb
-  const unsigned bias_lds = lds_base + WST_NSLOT * WST_SLOT + (unsigned)(wv * 64 + 4 * g) * 4;
+  const unsigned bias_lds = lds_base + NS * WST_SLOT + (unsigned)(wv * 64 + 4 * g) * 4;
   // staging tile: write (row fr, columns 32p + 16q + 4g ..), read (row lane >> 3 (+ 8), chunk lane & 7)
-  const unsigned stg = lds_base + WST_NSLOT * WST_SLOT + 1024 + (unsigned)wv * STG_BYTES;
+  const unsigned stg = lds_base + NS * WST_SLOT + 1024 + (unsigned)wv * STG_BYTES;
   const unsigned stg_w = stg + (unsigned)(fr * STG_PITCH + 8 * g);
   const unsigned stg_r = stg + (unsigned)((lane >> 3) * STG_PITCH + 16 * (lane & 7));
   u32x4 rowv[2] = {(u32x4){0u, 0u, 0u, 0u}, (u32x4){0u, 0u, 0u, 0u}};   // full rows read back, stored next group
+  // DW2: pw1 ring (2 tiles x 64 rows x 256 columns, pitch DW2_RP), the block's dw2 taps + bias (f32),
+  // a 64-entry rank table per wave
+  const unsigned ring_base = lds_base + NS * WST_SLOT + 1024;
+  const unsigned dww = ring_base + DW2_RING;
+  const unsigned ring_w = ring_base + (unsigned)(fr * DW2_RP + 128 * wv + 8 * g);
   f32x4 acc[2][4][4];
   bf16x8 afr[2][4][2];
 #pragma unroll
@@ -297,7 +335,8 @@ __global__ __launch_bounds__(256, 1) void gemm_wsp_kernel(const bf16* __restrict
                                                   rows * old[p] * 2, 0x00020000);
     return sd;
   };
-  auto epi_op = [&](auto Sc, auto Oc, f32x4(&a)[4][4], const StoreD& sd, const StoreD& sdp, auto RSc) {
+  auto epi_op = [&](auto Sc, auto Oc, f32x4(&a)[4][4], const StoreD& sd, const StoreD& sdp, auto RSc, auto SLc) {
+    (void)ring_w;
     (void)stg_w;   // named outside the if-constexpr branches: clang's implicit capture in generic lambdas
     (void)stg_r;
     (void)voffF;
@@ -337,7 +376,28 @@ __global__ __launch_bounds__(256, 1) void gemm_wsp_kernel(const bf16* __restrict
       else et[i] = yf(i) * et[i];
       pin(et[i]);
     };
-    if constexpr (EPI == EPI_GLU) {
+    if constexpr (EPI == EPI_DW2) {
+      // per half q (n-block 2p + q): the activation ops, 2 packs, ONE ds_write_b64 of the 4 columns into
+      // the pw1 ring (row 64 * slot + 16 jj + fr of the drained tile), the re-seed
+      constexpr int p = S & 1, jj = S >> 1, SL = decltype(SLc)::value;
+      constexpr int H = wsp_half<ACT>() + 2;   // ops per half
+      constexpr int q = O / H, o = O % H;
+      auto val = [&](int i) -> float { return a[2 * p + q][jj][i]; };
+      if constexpr (o == H - 1) {
+        seed(std::integral_constant<int, 2 * p + q>{}, jj);
+      } else if constexpr (o < H - 4) {
+        et[o] = fmaxf(val(o), 0.f);
+        pin(et[o]);
+      } else if constexpr (o < H - 2) {
+        constexpr int k = o - (H - 4);
+        epk[2 * q + k] = pack_bf16x2(et[2 * k], et[2 * k + 1]);
+        pin(epk[2 * q + k]);
+      } else {
+        typedef unsigned u32x2_w __attribute__((ext_vector_type(2)));
+        asm volatile("ds_write_b64 %0, %1 offset:%2" ::"v"(ring_w), "v"((u32x2_w){epk[2 * q], epk[2 * q + 1]}),
+                     "i"(SL * 64 * DW2_RP + jj * 16 * DW2_RP + 64 * p + 32 * q) : "memory");
+      }
+    } else if constexpr (EPI == EPI_GLU) {
       // ops 0-19 gate chain, 20-21 packs, 22-23 re-seeds (both accumulators are dead after op 19),
       // then on odd S the 2 swaps and the store
       constexpr int jj = S >> 1, h = S & 1;
@@ -438,11 +498,11 @@ __global__ __launch_bounds__(256, 1) void gemm_wsp_kernel(const bf16* __restrict
   // rows below lim; sdp: the previously drained tile, whose last rows the full-row path stores here)
   auto tile = [&](auto BUFc, int rt, const StoreD& sd, const StoreD& sdp) {
     constexpr int BUF = decltype(BUFc)::value;
-    const __amdgpu_buffer_rsrc_t dA1 = tile_rsrc(rt + 1), dA2 = tile_rsrc(rt + 2);
+    const __amdgpu_buffer_rsrc_t dA0 = tile_rsrc(rt), dA1 = tile_rsrc(rt + 1), dA2 = tile_rsrc(rt + 2);
     sfor<0, WST_NK>([&](auto KSc) {
       constexpr int KS = decltype(KSc)::value;
-      constexpr int slot_n = (8 * BUF + KS + 1) % WST_NSLOT;          // next step's slot (read)
-      constexpr int slot_d = (8 * BUF + KS + WST_DEPTH) % WST_NSLOT;  // step y + DEPTH's slot (DMA)
+      constexpr int slot_n = (8 * BUF + KS + 1) % NS;     // next step's slot (read)
+      constexpr int slot_d = (8 * BUF + KS + DP) % NS;    // step y + DEPTH's slot (DMA)
       constexpr int n_ops = wsp_nops<EPI, ACT>(KS);
       // step y+1 landed (2 pieces per step, issued unconditionally -- past the block's end they
       // land in dead slots -- so exactly 28 loads are younger-or-equal here) and, after the
@@ -451,11 +511,7 @@ __global__ __launch_bounds__(256, 1) void gemm_wsp_kernel(const bf16* __restrict
       // every WSP_BARP-th step: steps y+1 .. y+WSP_BARP landed (the younger DMA steps y+WSP_BARP+1 ..
       // y+DEPTH-1 may be in flight, 2 pieces each), then one barrier for all of them
       if constexpr (KS % WSP_BARP == 0) {
-        if constexpr (DIAG != 2 && DIAG != 4) {
-          if constexpr (WSP_BARP == 1) WST_VMCNT(26);
-          else if constexpr (WSP_BARP == 2) WST_VMCNT(22);
-          else WST_VMCNT(14);
-        }
+        if constexpr (DIAG != 2 && DIAG != 4) wst_vmcnt<2 * (DP - 1 - WSP_BARP)>();
         if constexpr (DIAG != 10) asm volatile("s_barrier" ::: "memory");
       }
       bf16x8(&cur)[4][2] = afr[KS & 1];
@@ -468,11 +524,14 @@ __global__ __launch_bounds__(256, 1) void gemm_wsp_kernel(const bf16* __restrict
           constexpr int rmb = (i >> 1) & 3, rkh = i >> 3;
           lds_read_into<(slot_n & 7) * WST_SLOT + rmb * 2048>(nxt[rmb][rkh], rdb[slot_n >> 3][rkh]);
         }
-        if constexpr ((i == 6 || i == 22) && DIAG != 4)
-          issue_piece(KS < WSP_BARP ? dA1 : dA2, std::integral_constant<int, i == 22 ? 1 : 0>{},
-                      std::integral_constant<int, (KS + WST_DEPTH) % WST_NK>{},
-                      std::integral_constant<int, slot_d>{});
-        sfor<wsp_lo(i, n_ops), wsp_lo(i + 1, n_ops)>([&](auto Oc) { epi_op(KSc, Oc, acc[1 - BUF], sd, sdp, std::true_type{}); });
+        if constexpr ((i == 6 || i == 22) && DIAG != 4) {
+          constexpr int toff = (KS + DP) / WST_NK;   // tile of step y + DEPTH: this one, the next or the one after
+          issue_piece(toff == 0 ? dA0 : toff == 1 ? dA1 : dA2, std::integral_constant<int, i == 22 ? 1 : 0>{},
+                      std::integral_constant<int, (KS + DP) % WST_NK>{}, std::integral_constant<int, slot_d>{});
+        }
+        sfor<wsp_lo(i, n_ops), wsp_lo(i + 1, n_ops)>([&](auto Oc) {
+          epi_op(KSc, Oc, acc[1 - BUF], sd, sdp, std::true_type{}, std::integral_constant<int, 1 - BUF>{});
+        });
         __builtin_amdgcn_sched_barrier(0);
       });
       constexpr int late = wsp_late_seeds<EPI, ACT>(KS);
@@ -489,7 +548,7 @@ __global__ __launch_bounds__(256, 1) void gemm_wsp_kernel(const bf16* __restrict
     asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");   // last MFMA writes -> VALU reads
     sfor<0, 8>([&](auto Sc) {
       constexpr int S = decltype(Sc)::value;
-      sfor<0, wsp_nops<EPI, ACT>(S)>([&](auto Oc) { epi_op(Sc, Oc, a, sd, sdp, std::false_type{}); });
+      sfor<0, wsp_nops<EPI, ACT>(S)>([&](auto Oc) { epi_op(Sc, Oc, a, sd, sdp, std::false_type{}, std::integral_constant<int, 1>{}); });
     });
     return sd;
   };
@@ -504,11 +563,102 @@ __global__ __launch_bounds__(256, 1) void gemm_wsp_kernel(const bf16* __restrict
     }
   };
 
+  // DW2: the dw2 outputs whose last pw1 row lies in tile rtp (drained into ring slot `slot`; tile
+  // rtp - 1 sits in the other slot).  Wave-local: a wave reads only its own 64 ring columns.  Lane =
+  // (position k of 8 in flight, 8 channels); the same f32 taps and FMA order as fe_dw2_kernel.
+  auto dw2_phase = [&](int rtp, int slot) {
+    (void)dww;
+    if constexpr (EPI == EPI_DW2 && DW2_DIAG != 2) {
+      const int wrows = ep.t2n * 19;
+      const int R = rtp * WST_MT + lane;
+      bool last = false;
+      if (R < M) {
+        const int w_ = R / wrows, rem = R - w_ * wrows, t2 = rem / 19, f2 = rem - t2 * 19;
+        last = t2 >= 2 && !(t2 & 1) && f2 >= 2 && !(f2 & 1);
+      }
+      const unsigned long long mask = __builtin_amdgcn_ballot_w64(last);
+      const int n = __builtin_popcountll(mask);
+      const unsigned tab = dww + DW2_WB + (unsigned)wv * 256;
+      if (last) {
+        const int rank = __builtin_amdgcn_mbcnt_hi((unsigned)(mask >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)mask, 0u));
+        asm volatile("ds_write_b32 %0, %1" ::"v"(tab + 4u * rank), "v"(lane) : "memory");
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      const int cl = wv * 64 + 8 * (lane & 7);   // the lane's 8 channels within the block's 256
+      const float* dwl = reinterpret_cast<const float*>(smem + NS * WST_SLOT + 1024 + DW2_RING);
+      const char* ring = smem + NS * WST_SLOT + 1024 + 128 * wv + 16 * (lane & 7);
+      // DW2_PPL positions per lane (k, k + 8, ..): each tap's 8 f32 weights are read from LDS once for
+      // all of them; packed f32 FMAs (v_pk_fma_f32: per-element fma, the same rounding as fmaf)
+      constexpr int P = DW2_PPL;
+      for (int base = 0; base < n; base += 8 * P) {
+        const int k0 = base + (lane >> 3);
+        if (k0 >= n) continue;
+        int Rl[P];
+#pragma unroll
+        for (int u = 0; u < P; ++u) {
+          const int ku = min(k0 + 8 * u, n - 1);
+          int rr;
+          asm volatile("ds_read_b32 %0, %1" : "=v"(rr) : "v"(tab + 4u * ku) : "memory");
+          Rl[u] = rr;
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        f32x2 a[P][4];
+        {
+          const f32x4 b0 = *reinterpret_cast<const f32x4*>(dwl + 9 * 256 + cl);
+          const f32x4 b1 = *reinterpret_cast<const f32x4*>(dwl + 9 * 256 + cl + 4);
+#pragma unroll
+          for (int u = 0; u < P; ++u) {
+            a[u][0] = (f32x2){b0[0], b0[1]};
+            a[u][1] = (f32x2){b0[2], b0[3]};
+            a[u][2] = (f32x2){b1[0], b1[1]};
+            a[u][3] = (f32x2){b1[2], b1[3]};
+          }
+        }
+        // ring row of pw1 row `row` (tile t sits in slot (t - r0c) & 1): (row - 64 r0c) mod 128
+        int rb[P];
+#pragma unroll
+        for (int u = 0; u < P; ++u) rb[u] = Rl[u] + rtp * WST_MT - WST_MT * r0c + 128;
+#pragma unroll DW2_VUNROLL
+        for (int v = 0; v < 3; ++v)
+#pragma unroll
+          for (int i = 0; i < 3; ++i) {
+            const int off = (2 - i) * 19 + (2 - v);
+            const f32x4 w0 = *reinterpret_cast<const f32x4*>(dwl + (3 * i + v) * 256 + cl);
+            const f32x4 w1 = *reinterpret_cast<const f32x4*>(dwl + (3 * i + v) * 256 + cl + 4);
+            const f32x2 wq[4] = {(f32x2){w0[0], w0[1]}, (f32x2){w0[2], w0[3]}, (f32x2){w1[0], w1[1]}, (f32x2){w1[2], w1[3]}};
+#pragma unroll
+            for (int u = 0; u < P; ++u) {
+              const u32x4 x = *reinterpret_cast<const u32x4*>(ring + ((rb[u] - off) & 127) * DW2_RP);
+#pragma unroll
+              for (int h = 0; h < 4; ++h) {
+                const f32x2 xv = {__builtin_bit_cast(float, x[h] << 16), __builtin_bit_cast(float, x[h] & 0xffff0000u)};
+                a[u][h] = __builtin_elementwise_fma(wq[h], xv, a[u][h]);
+              }
+            }
+          }
+#pragma unroll
+        for (int u = 0; u < P; ++u) {
+          if (k0 + 8 * u >= n) break;
+          const int R = rtp * WST_MT + Rl[u];
+          const int w_ = R / wrows, rem = R - w_ * wrows, t2 = rem / 19, f2 = rem - t2 * 19;
+          const int t3 = (t2 - 2) >> 1, f3 = (f2 - 2) >> 1;
+          bf16x8 o8;
+#pragma unroll
+          for (int h = 0; h < 4; ++h) {
+            o8[2 * h] = (bf16)a[u][h][0];
+            o8[2 * h + 1] = (bf16)a[u][h][1];
+          }
+          if constexpr (DW2_DIAG != 1)
+            *reinterpret_cast<bf16x8*>(reinterpret_cast<bf16*>(ep.out) + ((size_t)(w_ * ep.t3n + t3) * 9 + f3) * ep.ldo +
+                                       ct * 256 + cl) = o8;
+        }
+      }
+    }
+  };
+
   // prologue: weights in AGPRs (s_nop: AGPR writes -> MFMA reads), step 0 landed, its fragments read
   asm volatile("s_nop 7" ::: "memory");
-  if constexpr (WSP_BARP == 1) WST_VMCNT(28);   // step 0 landed: DEPTH - 1 younger steps in flight
-  else if constexpr (WSP_BARP == 2) WST_VMCNT(26);
-  else WST_VMCNT(22);
+  wst_vmcnt<2 * (DP - 1)>();   // step 0 landed: DEPTH - 1 younger steps in flight
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // + the bias in LDS
 #pragma unroll
   for (int nb = 0; nb < 4; ++nb)
@@ -525,20 +675,26 @@ __global__ __launch_bounds__(256, 1) void gemm_wsp_kernel(const bf16* __restrict
 
   // tiles in pairs (acc[0], acc[1]); an odd count runs one dummy tile past the block's range whose
   // results are never stored (lim = 0 in the drain), which keeps one straight loop body
-  const int npair = (r1 - r0 + 1) >> 1;
+  const int npair = (r1 - r0c + 1) >> 1;
   // the first tile's gaps drain a fake previous tile: rows of a REAL tile (never negative, so the
   // store descriptors' row bases stay inside the output) with lim = 0, i.e. zero-record stores
-  StoreD sd_prev = store_rsrc(r0, 0);
+  StoreD sd_prev = store_rsrc(r0c, 0);
   for (int it = 0; it < npair; ++it) {
-    const int rt = r0 + 2 * it;
+    const int rt = r0c + 2 * it;
     const StoreD sd0 = store_rsrc(it > 0 ? rt - 1 : rt, it > 0 ? M : 0);
     tile(std::integral_constant<int, 0>{}, rt, sd0, sd_prev);
+    if (EPI == EPI_DW2 && it > 0 && rt - 1 >= r0) dw2_phase(rt - 1, 1);   // drained into ring slot 1
     const StoreD sd1 = store_rsrc(rt, M);
     tile(std::integral_constant<int, 1>{}, rt + 1, sd1, sd0);
+    if (EPI == EPI_DW2 && rt >= r0 && rt < r1) dw2_phase(rt, 0);
     sd_prev = sd1;
   }
-  if (((r1 - r0) & 1) == 0) flush_rows(drain(acc[1], r1 - 1, sd_prev));
-  else flush_rows(sd_prev);   // odd count: the last tile call drained the last real tile
+  if (((r1 - r0c) & 1) == 0) {
+    flush_rows(drain(acc[1], r1 - 1, sd_prev));
+    if (EPI == EPI_DW2 && r1 - 1 >= r0) dw2_phase(r1 - 1, 1);
+  } else {
+    flush_rows(sd_prev);   // odd count: the last tile call drained the last real tile
+  }
   // the pieces issued past the end land (and the drain's seed reads return) before the
   // workgroup's LDS is released
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
@@ -593,7 +749,7 @@ int gemm_bf16_wst(int epi, int act, const bf16* A, int lda, const bf16* W, int l
   // 128 otherwise (measured at endless_decode's 12.7k-row segments: FFN w1 45 -> 41 us, QKV 36 ->
   // 30 us; GLU 20 -> 24 us, so it keeps the 256 x 256 kernel there); ep.wst == 2: any M (A/B)
   const int min_tiles = epi == EPI_GLU ? 512 : 128;
-  if (ep.wst < 2 && (M + WST_MT - 1) / WST_MT < min_tiles) return -1;
+  if (ep.wst < 2 && epi != EPI_DW2 && (M + WST_MT - 1) / WST_MT < min_tiles) return -1;
   if (N / 256 > 32) return -1;
   switch (epi) {
     case EPI_STORE:
@@ -604,6 +760,9 @@ int gemm_bf16_wst(int epi, int act, const bf16* A, int lda, const bf16* W, int l
     case EPI_GLU:
       if (ep.bias == nullptr) return -1;
       return launch_wst<EPI_GLU, ACT_NONE>(A, lda, W, ldw, M, N, ep, st);
+    case EPI_DW2:   // front-end pw1 + ReLU + dw2 (N = 512, dw2 taps / bias / geometry in ep)
+      if (act != ACT_RELU || N != 512 || !ep.dw_w || !ep.dw_b || ep.t2n < 3 || ep.ldo % 8) return -1;
+      return launch_wst<EPI_DW2, ACT_RELU>(A, lda, W, ldw, M, N, ep, st);
   }
   return -1;
 }

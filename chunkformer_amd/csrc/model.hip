@@ -285,10 +285,22 @@ struct ModelT : public cfm_model {
       PROF(PC_FE_CONV, frontend_conv0_dw<T>(feats, meta + (size_t)g0 * PLAN_REC, PLAN_REC, ng, Wn, fe.cm, fe.ci, fe.w0, fe.b0,
                                 fe.w1, fe.b1, fe.wpack, d, w.feA, st));
       EpiArgs e1 = E(SITE_FE); e1.bias = fe.b_pw1; e1.out = w.feB; e1.ldo = d;
-      PROF(PC_FE_GEMM, gemm<T>(EPI_STORE, ACT_RELU, w.feA, d, (const T*)fe.pw1, d, ng * T2 * 19, d, d, e1, st));
-      PROF(PC_FE_DW2, frontend_dw2<T>(w.feB, ng, T2, d, fe.w2, fe.b2, w.feA, st, tune.dw2_seg));
+      T* dw2_rows = w.feA;   // the pw2 GEMM's input
+      if constexpr (std::is_same<T, bf16>::value) {
+        if (tune.fe_fuse_dw2) {   // pw1 + ReLU + dw2 in one kernel: dw2 rows straight into feB
+          EpiArgs ef = e1; ef.dw_w = fe.w2; ef.dw_b = fe.b2; ef.t2n = T2; ef.t3n = T3;
+          int r = -1;
+          PROF(PC_FE_GEMM, (r = gemm_bf16_wst(EPI_DW2, ACT_RELU, w.feA, d, (const bf16*)fe.pw1, d, ng * T2 * 19, d, d, ef, st),
+                            r == -1 ? 0 : r));
+          if (r != -1) dw2_rows = w.feB;
+        }
+      }
+      if (dw2_rows == w.feA) {
+        PROF(PC_FE_GEMM, gemm<T>(EPI_STORE, ACT_RELU, w.feA, d, (const T*)fe.pw1, d, ng * T2 * 19, d, d, e1, st));
+        PROF(PC_FE_DW2, frontend_dw2<T>(w.feB, ng, T2, d, fe.w2, fe.b2, w.feA, st, tune.dw2_seg));
+      }
       EpiArgs e2 = E(SITE_FE); e2.bias = fe.b_pw2; e2.out = w.feC + (size_t)g0 * T3 * 9 * d; e2.ldo = d;
-      PROF(PC_FE_GEMM, gemm<T>(EPI_STORE, ACT_RELU, w.feA, d, (const T*)fe.pw2, d, ng * T3 * 9, d, d, e2, st));
+      PROF(PC_FE_GEMM, gemm<T>(EPI_STORE, ACT_RELU, dw2_rows, d, (const T*)fe.pw2, d, ng * T3 * 9, d, d, e2, st));
     }
     { EpiArgs e3 = E(); e3.bias = fe.b_out; e3.out = w.x; e3.ldo = d; e3.row_off = 0; e3.alpha = std::sqrt((float)d);
       PROF(PC_FE_GEMM, gemm<T>(EPI_STORE_F32, ACT_NONE, w.feC, 9 * d, (const T*)fe.wout, 9 * d, nwin * T3, d, 9 * d, e3, st)); }
@@ -681,6 +693,7 @@ cfm_status cfm_model_set_option(cfm_model* m, const char* key, int64_t value) {
         {"gemm_diag", &m->tune.gemm_diag}, {"gemm_wst", &m->tune.gemm_wst},   {"store_mode", &m->tune.store_mode},
         {"col_group", &m->tune.col_group}, {"attn_reuse", &m->tune.attn_reuse}, {"conv_dot2", &m->tune.conv_dot2},
         {"conv_dma", &m->tune.conv_dma},   {"dw2_seg", &m->tune.dw2_seg},   {"nt_sites", &m->tune.nt_sites},
+        {"fe_fuse_dw2", &m->tune.fe_fuse_dw2},
         {"attn128_var", &m->tune.attn128_var}};
     for (auto& k : knobs)
       if (!std::strcmp(key, k.first)) { *k.second = (int)value; return CFM_OK; }

@@ -138,6 +138,34 @@ def test_stream_split_bit_identical(large, dtype, minutes, parts):
         enc.stream_split, enc.split_min_chunks = saved
 
 
+@pytest.mark.parametrize("minutes,group", [(240, 0), (1, 2)])
+def test_frontend_fused_dw2_bit_identical(large, minutes, group):
+    """bf16 front-end option fe_fuse_dw2: pw1 + ReLU + dw2 in one weight-stationary GEMM (the dw2
+    taps applied to the pw1 tile ring in LDS, gemm_wst.hip EPI_DW2) must give the rows of the
+    pw1 GEMM + fe_dw2_kernel pair bit for bit -- same bf16 pw1 values, same f32 taps and FMA order.
+    (1 minute, 2 windows per group: group offsets > 0 and blocks with a halo tile at range start.)"""
+    g, _, models = large
+    enc = models["bf16"]
+    xs, _ = _embedded_batch(g, minutes, enc.device)
+    lens = torch.tensor([x.shape[0] for x in xs], dtype=torch.int32)
+    try:
+        enc.set_option("gemm_wst", 2)   # small groups: the unfused pw1 on the same kernel at any M
+        enc.set_option("fe_group_windows", group)
+        enc.set_option("fe_fuse_dw2", 0)
+        ref = enc.forward_parallel_chunk(xs, lens, 64, 128, 128)[0]
+        enc.set_option("fe_fuse_dw2", 1)
+        out = enc.forward_parallel_chunk(xs, lens, 64, 128, 128)[0]
+        torch.cuda.synchronize()
+        o2, r2 = out.reshape(-1, out.shape[-1]), ref.reshape(-1, ref.shape[-1])
+        bad = (o2 != r2).any(dim=1).nonzero().flatten()
+        assert bad.numel() == 0, (f"{bad.numel()} of {o2.shape[0]} rows differ, first {bad[:8].tolist()}, "
+                                  f"max abs {(o2.float() - r2.float()).abs().max().item():.3e}")
+    finally:
+        enc.set_option("fe_fuse_dw2", 0)
+        enc.set_option("fe_group_windows", 0)
+        enc.set_option("gemm_wst", 1)
+
+
 def test_frontend_window_groups_forced(large):
     """Cap the front-end at 2 windows per group (per-model option): the 30 s utterance's 6
     windows then run in 3 groups whose offsets into the intermediate buffers are > 0."""
