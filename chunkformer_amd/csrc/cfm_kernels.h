@@ -49,7 +49,8 @@ struct Tuning {
   int conv_dot2 = 2;             // conv module: bf16 dot2 kernel in half-chunk blocks (1: one block per chunk, 0: per-tap f32)
   int conv_dma = 1;              // conv module: LDS-DMA window staging (0: register staging)
   int dw2_seg = 4;               // front-end dw2: row segments per walk
-  int fe_fuse_dw2 = 0;           // front-end: pw1 + ReLU + dw2 in one weight-stationary GEMM (bf16)
+  int fe_fuse_dw2 = 1;           // front-end: pw1 + ReLU + dw2 in one weight-stationary GEMM (bf16; bench A/B
+                                 // 50.85 -> 50.15 ms/step, 3 interleaved pairs; 0 = pw1 GEMM + fe_dw2_kernel)
   int attn128_var = 1;           // head_dim 128 attention kernel variant (A/B)
   // GEMM sites whose bf16 outputs are stored non-temporally ("nt_sites" bit mask, SITE_* below).
   // Default: FFN w2 (its y goes straight to the LayerNorm; bench A/B 52.2 -> 51.4 ms/step); nt on

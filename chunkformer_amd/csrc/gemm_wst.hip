@@ -44,7 +44,11 @@ constexpr int WST_DEPTH = WST_NSLOT - WSP_BARP;   // steps in flight ahead of th
 static_assert(WSP_BARP == 1 || WSP_BARP == 2 || WSP_BARP == 4, "barrier period");
 // DW2 (front-end pw1 + ReLU + dw2): an 8-slot A ring leaves LDS for the pw1 output ring
 template <int EPI> constexpr int wst_nslot() { return EPI == EPI_DW2 ? 8 : WST_NSLOT; }
-template <int EPI> constexpr int wst_depth() { return wst_nslot<EPI>() - WSP_BARP; }
+#ifndef DW2_BARP
+#define DW2_BARP 2   // DW2's barrier period (its 8-slot ring keeps DEPTH - 1 - BARP steps in flight past the wait)
+#endif
+template <int EPI> constexpr int wst_barp() { return EPI == EPI_DW2 ? DW2_BARP : WSP_BARP; }
+template <int EPI> constexpr int wst_depth() { return wst_nslot<EPI>() - wst_barp<EPI>(); }
 // dw2 phase: positions per lane, tap-loop unroll, timing diagnostics (1 = no stores, 2 = no phase)
 #ifndef DW2_PPL
 #define DW2_PPL 1
@@ -510,8 +514,8 @@ __global__ __launch_bounds__(256, 1) void gemm_wsp_kernel(const bf16* __restrict
       // the DMA below refills
       // every WSP_BARP-th step: steps y+1 .. y+WSP_BARP landed (the younger DMA steps y+WSP_BARP+1 ..
       // y+DEPTH-1 may be in flight, 2 pieces each), then one barrier for all of them
-      if constexpr (KS % WSP_BARP == 0) {
-        if constexpr (DIAG != 2 && DIAG != 4) wst_vmcnt<2 * (DP - 1 - WSP_BARP)>();
+      if constexpr (KS % wst_barp<EPI>() == 0) {
+        if constexpr (DIAG != 2 && DIAG != 4) wst_vmcnt<2 * (DP - 1 - wst_barp<EPI>())>();
         if constexpr (DIAG != 10) asm volatile("s_barrier" ::: "memory");
       }
       bf16x8(&cur)[4][2] = afr[KS & 1];

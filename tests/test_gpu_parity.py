@@ -153,8 +153,10 @@ def test_large_12L(cfm, large, dtype):
     ids = ids.cpu().numpy()
     margin = g["top2"][..., 0] - g["top2"][..., 1]
     if dtype == "fp32":
-        np.testing.assert_allclose(o, g["out"], atol=FP32_ATOL * 5, rtol=0)
-        sure = margin > 1e-3
+        # max-abs <= 1e-4 (measured 4.9e-6 on the box, tools/large12_err.py), ids equal
+        # wherever the reference's top-2 margin is >= 1e-4
+        np.testing.assert_allclose(o, g["out"], atol=FP32_ATOL, rtol=0)
+        sure = margin > 1e-4
         np.testing.assert_array_equal(ids[sure], g["ids"][sure])
     else:
         assert _rel_l2(o, g["out"]) <= BF16_RELL2

@@ -161,7 +161,7 @@ def test_frontend_fused_dw2_bit_identical(large, minutes, group):
         assert bad.numel() == 0, (f"{bad.numel()} of {o2.shape[0]} rows differ, first {bad[:8].tolist()}, "
                                   f"max abs {(o2.float() - r2.float()).abs().max().item():.3e}")
     finally:
-        enc.set_option("fe_fuse_dw2", 0)
+        enc.set_option("fe_fuse_dw2", 1)   # the default
         enc.set_option("fe_group_windows", 0)
         enc.set_option("gemm_wst", 1)
 
