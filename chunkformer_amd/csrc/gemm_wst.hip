@@ -59,6 +59,13 @@ template <int EPI> constexpr int wst_depth() { return wst_nslot<EPI>() - wst_bar
 #ifndef DW2_DIAG
 #define DW2_DIAG 0
 #endif
+#ifndef DW2_NT
+#define DW2_NT 0     // dw2 output stores non-temporal (A/B)
+#endif
+#ifndef DW2_DEFER
+#define DW2_DEFER 0  // dw2 outputs staged in LDS and stored at the start of the next phase (A/B)
+#endif
+constexpr int DW2_STG = 3 * (64 * 16 + 64 * 4);   // per wave: 3 passes x (64 lanes x 16 B + a u32 offset)
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 constexpr int DW2_RP = 528;                 // pw1 ring row pitch (256 bf16 + 16 B): conflict-free ds_write_b64
 constexpr int DW2_RING = 128 * DW2_RP;      // two 64-row tiles
@@ -172,7 +179,7 @@ __global__ __launch_bounds__(256, 1) void gemm_wsp_kernel(const bf16* __restrict
   // + per wave a 16-row x 64-column bf16 output staging tile (144-B rows) for full-row stores
   constexpr int STG_PITCH = 144, STG_BYTES = 16 * STG_PITCH;
   constexpr int NS = wst_nslot<EPI>(), DP = wst_depth<EPI>();
-  constexpr int TAIL = EPI == EPI_DW2 ? DW2_RING + DW2_WB + 4 * 256 : 4 * STG_BYTES;
+  constexpr int TAIL = EPI == EPI_DW2 ? DW2_RING + DW2_WB + 4 * 256 + (DW2_DEFER ? 4 * DW2_STG : 0) : 4 * STG_BYTES;
   __shared__ __attribute__((aligned(16))) char smem[NS * WST_SLOT + 1024 + TAIL];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -570,8 +577,31 @@ __global__ __launch_bounds__(256, 1) void gemm_wsp_kernel(const bf16* __restrict
   // DW2: the dw2 outputs whose last pw1 row lies in tile rtp (drained into ring slot `slot`; tile
   // rtp - 1 sits in the other slot).  Wave-local: a wave reads only its own 64 ring columns.  Lane =
   // (position k of 8 in flight, 8 channels); the same f32 taps and FMA order as fe_dw2_kernel.
+  // DW2_DEFER: the previous phase's outputs (npend passes) leave from the LDS staging area here, so
+  // their store acknowledgements overlap this phase's arithmetic instead of the next DMA waits
+  const unsigned dstg = dww + DW2_WB + 4 * 256 + (unsigned)wv * DW2_STG;
+  int npend = 0;
+  auto dw2_flush = [&]() {
+    if constexpr (EPI == EPI_DW2 && DW2_DEFER) {
+      for (int p = 0; p < npend; ++p) {
+        u32x4 v;
+        unsigned off;
+        asm volatile("ds_read_b128 %0, %1 offset:0" : "=v"(v) : "v"(dstg + (unsigned)p * 1280 + 16u * lane) : "memory");
+        asm volatile("ds_read_b32 %0, %1 offset:1024" : "=v"(off) : "v"(dstg + (unsigned)p * 1280 + 4u * lane) : "memory");
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (off != 0xffffffffu) {
+          u32x4* dst = reinterpret_cast<u32x4*>(reinterpret_cast<bf16*>(ep.out) + off);
+          if constexpr (DW2_NT) __builtin_nontemporal_store(v, dst);
+          else *dst = v;
+        }
+      }
+      npend = 0;
+    }
+  };
   auto dw2_phase = [&](int rtp, int slot) {
     (void)dww;
+    (void)dstg;
+    dw2_flush();
     if constexpr (EPI == EPI_DW2 && DW2_DIAG != 2) {
       const int wrows = ep.t2n * 19;
       const int R = rtp * WST_MT + lane;
@@ -594,8 +624,11 @@ __global__ __launch_bounds__(256, 1) void gemm_wsp_kernel(const bf16* __restrict
       // DW2_PPL positions per lane (k, k + 8, ..): each tap's 8 f32 weights are read from LDS once for
       // all of them; packed f32 FMAs (v_pk_fma_f32: per-element fma, the same rounding as fmaf)
       constexpr int P = DW2_PPL;
+      const bool defer = DW2_DEFER && P == 1 && n <= 24;
       for (int base = 0; base < n; base += 8 * P) {
         const int k0 = base + (lane >> 3);
+        if (defer)   // marker first: lanes without a position store nothing at the flush
+          asm volatile("ds_write_b32 %0, %1 offset:1024" ::"v"(dstg + (unsigned)(base >> 3) * 1280 + 4u * lane), "v"(0xffffffffu) : "memory");
         if (k0 >= n) continue;
         int Rl[P];
 #pragma unroll
@@ -652,11 +685,23 @@ __global__ __launch_bounds__(256, 1) void gemm_wsp_kernel(const bf16* __restrict
             o8[2 * h] = (bf16)a[u][h][0];
             o8[2 * h + 1] = (bf16)a[u][h][1];
           }
-          if constexpr (DW2_DIAG != 1)
-            *reinterpret_cast<bf16x8*>(reinterpret_cast<bf16*>(ep.out) + ((size_t)(w_ * ep.t3n + t3) * 9 + f3) * ep.ldo +
-                                       ct * 256 + cl) = o8;
+          bf16x8* dst = reinterpret_cast<bf16x8*>(reinterpret_cast<bf16*>(ep.out) + ((size_t)(w_ * ep.t3n + t3) * 9 + f3) * ep.ldo +
+                                                  ct * 256 + cl);
+          if constexpr (DW2_DIAG != 1) {
+            if (defer) {
+              const unsigned sb = dstg + (unsigned)(base >> 3) * 1280;
+              asm volatile("ds_write_b128 %0, %1 offset:0" ::"v"(sb + 16u * lane), "v"(__builtin_bit_cast(u32x4, o8)) : "memory");
+              asm volatile("ds_write_b32 %0, %1 offset:1024" ::"v"(sb + 4u * lane),
+                           "v"((unsigned)(((size_t)(w_ * ep.t3n + t3) * 9 + f3) * ep.ldo + ct * 256 + cl)) : "memory");
+            } else if constexpr (DW2_NT) {
+              __builtin_nontemporal_store(o8, dst);
+            } else {
+              *dst = o8;
+            }
+          }
         }
       }
+      if (defer) npend = (n + 7) >> 3;
     }
   };
 
@@ -699,6 +744,7 @@ __global__ __launch_bounds__(256, 1) void gemm_wsp_kernel(const bf16* __restrict
   } else {
     flush_rows(sd_prev);   // odd count: the last tile call drained the last real tile
   }
+  dw2_flush();
   // the pieces issued past the end land (and the drain's seed reads return) before the
   // workgroup's LDS is released
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
