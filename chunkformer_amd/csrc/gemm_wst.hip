@@ -62,6 +62,9 @@ template <int EPI> constexpr int wst_depth() { return wst_nslot<EPI>() - wst_bar
 #ifndef DW2_NT
 #define DW2_NT 0     // dw2 output stores non-temporal (A/B)
 #endif
+#ifndef DW2_PIPE
+#define DW2_PIPE 0   // dw2 taps software-pipelined two deep (explicit LDS reads and waits)
+#endif
 #ifndef DW2_DEFER
 #define DW2_DEFER 0  // dw2 outputs staged in LDS and stored at the start of the next phase (A/B)
 #endif
@@ -631,18 +634,28 @@ __global__ __launch_bounds__(256, 1) void gemm_wsp_kernel(const bf16* __restrict
           asm volatile("ds_write_b32 %0, %1 offset:1024" ::"v"(dstg + (unsigned)(base >> 3) * 1280 + 4u * lane), "v"(0xffffffffu) : "memory");
         if (k0 >= n) continue;
         int Rl[P];
+        f32x4 b0, b1;
+        if constexpr (DW2_PIPE >= 2 && P == 1) {
+          // the rank and the bias seeds in one LDS round trip
+          const unsigned bl = dww + 4u * (unsigned)(9 * 256 + cl);
+          asm volatile("ds_read_b32 %0, %1" : "=v"(Rl[0]) : "v"(tab + 4u * min(k0, n - 1)) : "memory");
+          asm volatile("ds_read_b128 %0, %1" : "=v"(b0) : "v"(bl) : "memory");
+          asm volatile("ds_read_b128 %0, %1 offset:16" : "=v"(b1) : "v"(bl) : "memory");
+          asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(Rl[0]), "+v"(b0), "+v"(b1)::"memory");
+        } else {
 #pragma unroll
-        for (int u = 0; u < P; ++u) {
-          const int ku = min(k0 + 8 * u, n - 1);
-          int rr;
-          asm volatile("ds_read_b32 %0, %1" : "=v"(rr) : "v"(tab + 4u * ku) : "memory");
-          Rl[u] = rr;
+          for (int u = 0; u < P; ++u) {
+            const int ku = min(k0 + 8 * u, n - 1);
+            int rr;
+            asm volatile("ds_read_b32 %0, %1" : "=v"(rr) : "v"(tab + 4u * ku) : "memory");
+            Rl[u] = rr;
+          }
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          b0 = *reinterpret_cast<const f32x4*>(dwl + 9 * 256 + cl);
+          b1 = *reinterpret_cast<const f32x4*>(dwl + 9 * 256 + cl + 4);
         }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         f32x2 a[P][4];
         {
-          const f32x4 b0 = *reinterpret_cast<const f32x4*>(dwl + 9 * 256 + cl);
-          const f32x4 b1 = *reinterpret_cast<const f32x4*>(dwl + 9 * 256 + cl + 4);
 #pragma unroll
           for (int u = 0; u < P; ++u) {
             a[u][0] = (f32x2){b0[0], b0[1]};
@@ -655,6 +668,44 @@ __global__ __launch_bounds__(256, 1) void gemm_wsp_kernel(const bf16* __restrict
         int rb[P];
 #pragma unroll
         for (int u = 0; u < P; ++u) rb[u] = Rl[u] + rtp * WST_MT - WST_MT * r0c + 128;
+        if constexpr (DW2_PIPE && P == 1) {
+          // the 9 taps (t = 3v + i, the order below) software-pipelined two deep: tap t + 2's ring row and
+          // weights are read while tap t computes (the compiler issued each tap's reads only after the
+          // previous tap's FMAs: one LDS round trip per tap with one wave per SIMD)
+          const unsigned rl = ring_base + 128u * (unsigned)wv + 16u * (unsigned)(lane & 7);
+          const unsigned wl = dww + 4u * (unsigned)cl;
+          u32x4 xs[2];
+          f32x4 ws[2][2];
+          // the bias seeds landed before the first asm read (the compiler's own lgkmcnt wait for them
+          // would otherwise come after those reads and drain them)
+          asm volatile("" : "+v"(a[0][0]), "+v"(a[0][1]), "+v"(a[0][2]), "+v"(a[0][3]));
+          auto issue = [&xs, &ws, &rb, rl, wl](auto Tc) {
+            constexpr int t = decltype(Tc)::value, v = t / 3, i = t % 3, sl = t & 1;
+            constexpr int off = (2 - i) * 19 + (2 - v);
+            const unsigned xa = rl + (unsigned)(((rb[0] - off) & 127) * DW2_RP);
+            asm volatile("ds_read_b128 %0, %1" : "=v"(xs[sl]) : "v"(xa) : "memory");
+            asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(ws[sl][0]) : "v"(wl), "i"((3 * i + v) * 1024) : "memory");
+            asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(ws[sl][1]) : "v"(wl), "i"((3 * i + v) * 1024 + 16) : "memory");
+          };
+          issue(std::integral_constant<int, 0>{});
+          issue(std::integral_constant<int, 1>{});
+          sfor<0, 9>([&xs, &ws, &a, &issue](auto Tc) {
+            constexpr int t = decltype(Tc)::value, sl = t & 1;
+            if constexpr (t < 8)
+              asm volatile("s_waitcnt lgkmcnt(3)" : "+v"(xs[sl]), "+v"(ws[sl][0]), "+v"(ws[sl][1])::"memory");
+            else
+              asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(xs[sl]), "+v"(ws[sl][0]), "+v"(ws[sl][1])::"memory");
+            const f32x4 w0 = ws[sl][0], w1 = ws[sl][1];
+            const u32x4 x = xs[sl];
+            const f32x2 wq[4] = {(f32x2){w0[0], w0[1]}, (f32x2){w0[2], w0[3]}, (f32x2){w1[0], w1[1]}, (f32x2){w1[2], w1[3]}};
+#pragma unroll
+            for (int h = 0; h < 4; ++h) {
+              const f32x2 xv = {__builtin_bit_cast(float, x[h] << 16), __builtin_bit_cast(float, x[h] & 0xffff0000u)};
+              a[0][h] = __builtin_elementwise_fma(wq[h], xv, a[0][h]);
+            }
+            if constexpr (t + 2 < 9) issue(std::integral_constant<int, t + 2>{});
+          });
+        } else
 #pragma unroll DW2_VUNROLL
         for (int v = 0; v < 3; ++v)
 #pragma unroll
