@@ -76,7 +76,11 @@ void cfm_model_destroy(cfm_model* m);
  *                   stream (bit i = class i of cfm_profile_read); 0 = off
  *   "profile_reset" clear the accumulated profile
  *   "ring_attention" 1 (default) = bf16 masked batch uses the sliding-ring attention kernel,
- *                   0 = the generic per-block kernel (A/B testing) */
+ *                   0 = the generic per-block kernel (A/B testing)
+ *   "fe_fuse_dw2"   1 (default) = bf16 front-end pw1 + ReLU + dw2 in one weight-stationary GEMM,
+ *                   0 = pw1 GEMM + the separate dw2 kernel (bit-identical; A/B testing)
+ * (all per-model kernel options: struct Tuning in chunkformer_amd/csrc/cfm_kernels.h, keyed in
+ *  cfm_model_set_option, chunkformer_amd/csrc/model.hip) */
 cfm_status cfm_model_set_option(cfm_model* m, const char* key, int64_t value);
 /* Per kernel class: name, accumulated milliseconds and launch count of the
  * event-bracketed launches since the last reset.  Host-synchronising (waits for
