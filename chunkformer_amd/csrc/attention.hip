@@ -252,7 +252,7 @@ __global__ __launch_bounds__(512, 1) void chunk_attention_ring_kernel(
     const bf16* __restrict__ Q, const bf16* __restrict__ KV, int kv_rows, const bf16* __restrict__ P, int p_rows,
     const float* __restrict__ pos_u, const float* __restrict__ pos_v, const int32_t* __restrict__ desc, int n_chunks,
     int H, int C, int W, bf16* __restrict__ out, int diag, int nch, int p_ld) {
-  const bool reuse_band = diag != 5;   // diag 5: recompute band subtile 0 of every tile (A/B)
+  const bool reuse_band = (diag & 15) != 5;   // diag 5: recompute band subtile 0 of every tile (A/B)
   __shared__ __attribute__((aligned(16))) char smem[RING_LDS];
   char* kr = smem;
   char* pl = smem + KR_BYTES;
@@ -334,7 +334,7 @@ __global__ __launch_bounds__(512, 1) void chunk_attention_ring_kernel(
   for (int cp = c0; cp < c1; cp += 2) {
     const int kvp = kvb + (cp - c0) * C;
     const int c = cp + half;
-    const bool active = c < c1 && i0 < C && diag != 1;
+    const bool active = c < c1 && i0 < C && (diag & 15) != 1;
     qraw[0] = qnext[0];
     qraw[1] = qnext[1];
     const int key_lo = klo_n, key_hi = khi_n;
@@ -445,10 +445,13 @@ __global__ __launch_bounds__(512, 1) void chunk_attention_ring_kernel(
             const f32x4 a = band[2 * hh + pt];
             // rel_shift by the reshape trick: row fr is written at pitch 49 (+1) and read back at
             // pitch 48, so query fr's band for key jj starts 16 - fr elements later: the reads
-            // are aligned 8-B vectors (4 keys), the writes 2-B aligned (LDS takes unaligned b64)
+            // are aligned 8-B vectors (4 keys), the writes 2-B aligned, as four ds_write_b16
             const unsigned waddr = scr_base + 2u * (unsigned)(fr * SCR_PITCH + 1 + 16 * pt + 4 * g);
             const unsigned lo = pack_bf16x2_a(a[0], a[1]), hi = pack_bf16x2_a(a[2], a[3]);
-            asm volatile("ds_write_b64 %0, %1" ::"v"(waddr), "v"((u32x2_a){lo, hi}) : "memory");
+            if (diag & 16)   // A/B: one unaligned ds_write_b64 (replayed by the LDS)
+              asm volatile("ds_write_b64 %0, %1" ::"v"(waddr), "v"((u32x2_a){lo, hi}) : "memory");
+            else
+              lds_store_4bf16_a2(waddr, lo, hi);
           }
           // band of (query fr, key j0+32hh+16st2+4g+rr) = scratch[fr][16st2 + 4g + rr + 15 - fr]
           typedef bf16 bf16x4 __attribute__((ext_vector_type(4)));
@@ -512,7 +515,7 @@ __global__ __launch_bounds__(512, 1) void chunk_attention_ring_kernel(
 #pragma unroll
       for (int t = 0; t < 5; ++t) {
         const int j0 = jb + 64 * t;
-        if (j0 >= key_hi || diag == 3) continue;
+        if (j0 >= key_hi || (diag & 15) == 3) continue;
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
           bf16x8 pb;
@@ -585,7 +588,7 @@ int chunk_attention_masked_bf16(const bf16* q, const bf16* kv, int kv_rows, cons
     (void)hipGetDevice(&dev);
     if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0) n_cu = 256;
   }
-  if (!reuse && diag == 0) diag = 5;   // "attn_reuse" 0: recompute the shared band subtile (A/B)
+  if (!reuse && (diag & 15) == 0) diag |= 5;   // "attn_reuse" 0: recompute the shared band subtile (A/B)
   int nch = (int)(((long long)n_chunks * H + n_cu - 1) / n_cu);
   nch = max(NCH, (nch + 1) & ~1);
   const dim3 grid((n_chunks + nch - 1) / nch, H);
@@ -751,8 +754,7 @@ __global__ __launch_bounds__(512, 1) void full_attention_bf16_kernel(
         for (int pt = 0; pt < 3; ++pt) {
           const f32x4 a = band[2 * hh + pt];
           const unsigned waddr = scr_base + 2u * (unsigned)(fr * SCR_PITCH + 1 + 16 * pt + 4 * g);
-          const unsigned lo = pack_bf16x2_a(a[0], a[1]), hi = pack_bf16x2_a(a[2], a[3]);
-          asm volatile("ds_write_b64 %0, %1" ::"v"(waddr), "v"((u32x2_a){lo, hi}) : "memory");
+          lds_store_4bf16_a2(waddr, pack_bf16x2_a(a[0], a[1]), pack_bf16x2_a(a[2], a[3]));
         }
         typedef bf16 bf16x4 __attribute__((ext_vector_type(4)));
         bf16x4 bdv4[2];

@@ -189,8 +189,11 @@ __global__ __launch_bounds__(512, 1) void chunk_attention_a128_kernel(
         const int i = 16 * qs + fr;
         const int col = 48 * w + 16 * rs + 4 * g + i - 59;
         if (col >= 1 && col <= W + 3) {   // groups that reach a read column j + 4, j in [0, W)
-          const unsigned addr = bb_lds + 2u * (unsigned)(i * A8_BAND_PITCH + col);
-          asm volatile("ds_write_b64 %0, %1" ::"v"(addr), "v"((u32x2_){pk2(a[0], a[1]), pk2(a[2], a[3])}) : "memory");
+          const unsigned addr = bb_lds + 2u * (unsigned)(i * A8_BAND_PITCH + col);   // 2-B aligned
+          if constexpr (VAR == 3)   // A/B: one unaligned ds_write_b64 (replayed by the LDS)
+            asm volatile("ds_write_b64 %0, %1" ::"v"(addr), "v"((u32x2_){pk2(a[0], a[1]), pk2(a[2], a[3])}) : "memory");
+          else
+            lds_store_4bf16_a2(addr, pk2(a[0], a[1]), pk2(a[2], a[3]));
         }
       }
       __builtin_amdgcn_sched_barrier(0);
@@ -346,6 +349,7 @@ int chunk_attention_masked_a128(const bf16* q, const bf16* kv, int kv_rows, cons
     default:
       switch (var) {   // 10-13: timing-only diagnostics (no band / score / P.V MFMAs, no V^T loads)
         case 0: A128(5, 0); break;
+        case 3: A128(5, 3); break;
         case 10: A128(5, 10); break;
         case 11: A128(5, 11); break;
         case 12: A128(5, 12); break;

@@ -106,13 +106,13 @@ def test_golden_utterances_inside_bench_batch(large, dtype, minutes):
         else:
             # bf16 moves the log-probs by ~1e-2 (random weights: many near-tied frames), so an id may
             # flip where the reference's own top-2 margin is that small; beyond BF16_MARGIN every id
-            # must agree, and overall agreement stays >= 98%
+            # must agree, and agreement stays >= 99% (measured 99.74% / 100% / 100%)
             m = margin[gstart[k]: gstart[k + 1]]
             flips = m[i != ei]
             print(f"bf16 golden utt {k}: rel-L2 {_rel_l2(o, exp):.2e}, CTC argmax agreement {(i == ei).mean():.4f}, "
                   f"{flips.size} flips, largest flipped margin {flips.max() if flips.size else 0:.2e}")
             assert _rel_l2(o, exp) <= BF16_RELL2, f"utt {k}: {_rel_l2(o, exp)}"
-            assert (i == ei).mean() >= 0.98
+            assert (i == ei).mean() >= 0.99
             np.testing.assert_array_equal(i[m > BF16_MARGIN], ei[m > BF16_MARGIN])
 
 
