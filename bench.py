@@ -51,7 +51,7 @@ sys.path.insert(0, ROOT)
 
 from chunkformer_amd import _lib  # noqa: E402
 from chunkformer_amd.config import LARGE  # noqa: E402
-from chunkformer_amd.distributed import (chunks_of, gather_ids, gather_logp, init_from_env,  # noqa: E402
+from chunkformer_amd.distributed import (_assemble, chunks_of, gather_ids, gather_logp, init_from_env,  # noqa: E402
                                          plan_shards, rank_rows)
 from chunkformer_amd.encoder import ChunkFormerEncoder  # noqa: E402
 from chunkformer_amd.weights import synthetic_state_dict  # noqa: E402
@@ -280,8 +280,9 @@ def main():
                          "attention, B=256)")
     ap.add_argument("--hours", type=float, default=16.0, help="endless: audio hours")
     ap.add_argument("--endless-mode", default="pipeline", choices=["pipeline", "graph"],
-                    help="endless: two segments in flight on two streams (pipeline) or one captured HIP graph "
-                         "replayed per middle segment (graph); both are bit-identical to the eager loop")
+                    help="endless: --pipeline-depth segments in flight on as many streams (pipeline) or one "
+                         "captured HIP graph replayed per middle segment (graph); both are bit-identical to the "
+                         "eager loop")
     ap.add_argument("--pipeline-depth", type=int, default=3, help="endless pipeline: segments in flight")
     ap.add_argument("--tbd", type=int, default=7200,
                     help="endless: total_batch_duration (s); a memory budget that does not change results "
@@ -429,6 +430,20 @@ def main():
             gather_lp_ms = (time.perf_counter() - tg) * 1e3
             del logp
     del out, enc_out, ids
+    # the gather's per-utterance reassembly at configs[2]'s world 8, timed on this GPU alone: one
+    # index_select of the gathered [8, max_rows] ids with the plan's cached index, then views
+    assemble_ms = None
+    if sharded and rank == 0:
+        sh8 = plan_shards(lens_all, 8, C, L, R, cfg.num_blocks)
+        buf8 = torch.zeros(8, max(1, max(sum(p.rows for p in s_) for s_ in sh8)), dtype=torch.int32, device=dev)
+        _assemble(buf8, sh8, len(lens_all), lens_all)   # builds and uploads the plan's index once
+        torch.cuda.synchronize()
+        ta = time.perf_counter()
+        for _ in range(5):
+            _assemble(buf8, sh8, len(lens_all), lens_all)
+        torch.cuda.synchronize()
+        assemble_ms = (time.perf_counter() - ta) / 5 * 1e3
+        del buf8
 
     # ---- end to end: the step + the fused CTC ids head + (N > 1) the ids all-gather with the
     # per-utterance reassembly on every rank; K steps between barriers, max over ranks
@@ -515,6 +530,7 @@ def main():
             "end_to_end_note": ("encoder step + fused CTC ids head" +
                                 (" + ids all_gather_into_tensor and per-utterance reassembly" if world > 1 else "")),
             "allgather_logp_bf16_ms": round(gather_lp_ms, 3) if gather_lp_ms is not None else None,
+            "reassembly_world8_ms": round(assemble_ms, 3) if assemble_ms is not None else None,
             "breakdown_ms": breakdown,
             "roofline_by_class": by_class,
         }
@@ -557,7 +573,8 @@ def bench_single(args):
         workload = (f"endless_decode over one {args.hours:g} h utterance (synthetic N(0,1) fbank), C=64 L=128 "
                     f"R=128, total_batch_duration={args.tbd}: {len(segs)} segments of <= {seg_len} frames "
                     f"(trunc {trunc} rows kept each), att/cnn caches carried, " +
-                    ("two segments in flight on two HIP streams (segment k+1 layer l waits for segment k layer l)"
+                    (f"{args.pipeline_depth} segments in flight on {args.pipeline_depth} HIP streams (segment k+1 "
+                     "layer l waits for segment k layer l)"
                      if args.endless_mode == "pipeline" else
                      "middle segments replayed from one captured HIP graph (front-end + 12 blocks + after_norm + "
                      "CTC argmax)"))

@@ -68,6 +68,7 @@ cfm_workspace_bytes_masked = _sig("cfm_workspace_bytes_masked", SZ, P, I32, I32,
 cfm_workspace_bytes_padded = _sig("cfm_workspace_bytes_padded", SZ, P, I32, I32, I32, I32, I32)
 cfm_encode_masked = _sig("cfm_encode_masked", I32, P, P, P, P, P, P, I32, P, P, P, P, SZ, P)
 cfm_encode_padded = _sig("cfm_encode_padded", I32, P, P, P, P, P, P, SZ, P)
+cfm_encode_masked_utts = _sig("cfm_encode_masked_utts", I32, P, P, P, P, P, P, I32, P, P, P, P, SZ, P)
 cfm_encode_masked_stages = _sig("cfm_encode_masked_stages", I32, P, P, P, P, P, P, I32, P, P, P, P, SZ, I32, I32, P)
 cfm_masks_from_plan = _sig("cfm_masks_from_plan", I32, P, P, P, P, P)
 cfm_profile_read = _sig("cfm_profile_read", I32, P, P, P, P, I32)
@@ -107,7 +108,7 @@ EXPORTED_OPS = ["cfm_op_gemm"]
 
 EXPORTED = ["cfm_version", "cfm_last_error", "cfm_model_create", "cfm_model_destroy", "cfm_model_set_option",
             "cfm_plan_masked", "cfm_plan_masked_ex", "cfm_plan_padded", "cfm_workspace_bytes_masked", "cfm_workspace_bytes_padded",
-            "cfm_encode_masked", "cfm_encode_masked_stages", "cfm_encode_padded", "cfm_masks_from_plan", "cfm_profile_read", "cfm_ctc_workspace_bytes",
+            "cfm_encode_masked", "cfm_encode_masked_utts", "cfm_encode_masked_stages", "cfm_encode_padded", "cfm_masks_from_plan", "cfm_profile_read", "cfm_ctc_workspace_bytes",
             "cfm_ctc_logprobs", "cfm_ctc_ids_workspace_bytes", "cfm_ctc_ids", "cfm_ctc_collapse",
             "cfm_plan_stream", "cfm_workspace_bytes_stream", "cfm_encode_stream",
             "cfm_fbank_create", "cfm_fbank_destroy", "cfm_fbank_num_frames", "cfm_fbank_compute",

@@ -69,5 +69,8 @@ LARGE = EncoderConfig()
 # the reference's shipped d=512 recipe family: 4 heads -> head_dim 128
 # (examples/asr/rnnt/conf/chunkformer-rnnt-large-vie.yaml:5-6)
 LARGE_4H = EncoderConfig(n_heads=4)
+# the reference's shipped small recipes (examples/asr/ctc/conf/chunkformer-ctc-small-libri-100h.yaml:5-8,
+# rnnt small, libri-960h): d=256, 4 heads (head_dim 64), ff 2048, 12 blocks, bpe1024 vocabulary
+SMALL256 = EncoderConfig(d_model=256, n_heads=4, ffn_dim=2048, num_blocks=12, vocab=1024)
 # small config used for the committed golden fixtures (tests/golden)
 SMALL = EncoderConfig(d_model=128, n_heads=2, ffn_dim=256, num_blocks=2, vocab=48)

@@ -582,12 +582,7 @@ int chunk_attention_masked_bf16(const bf16* q, const bf16* kv, int kv_rows, cons
   if (C <= 0 || C > 64 || (C % 16) || (W & 1) || W > 320 || W + C > RING || p_rows > RING || n_chunks <= 0) return -1;
   // one block per CU (LDS-bound), each sweeping a long run of chunks of one head: one prologue
   // (P rows + first window) per block instead of one per 8 chunks
-  static int n_cu = 0;
-  if (!n_cu) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0) n_cu = 256;
-  }
+  const int n_cu = cu_count();
   if (!reuse && (diag & 15) == 0) diag |= 5;   // "attn_reuse" 0: recompute the shared band subtile (A/B)
   int nch = (int)(((long long)n_chunks * H + n_cu - 1) / n_cu);
   nch = max(NCH, (nch + 1) & ~1);

@@ -327,12 +327,7 @@ int chunk_attention_masked_a128(const bf16* q, const bf16* kv, int kv_rows, cons
                                 int p_rows, int p_ld, const float* pos_u, const float* pos_v, const int32_t* desc,
                                 int n_chunks, int H, int C, int W, bf16* out, hipStream_t st, int var) {
   if (!attention_a128_eligible(C, W, p_rows, 128) || n_chunks <= 0) return -1;
-  static int n_cu = 0;
-  if (!n_cu) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0) n_cu = 256;
-  }
+  const int n_cu = cu_count();
   // one block per CU sweeping consecutive chunks of one head (one K-ring prologue per block)
   int nch = (int)(((long long)n_chunks * H + n_cu - 1) / n_cu);
   nch = std::max(4, nch);

@@ -9,6 +9,10 @@ typedef __bf16 bf16;
 
 namespace cfm {
 
+// compute units of the current device (launch sizing of the persistent kernels), cached per
+// device id: correct for a process that drives several GPUs, safe to call from several threads
+int cu_count();
+
 enum { EPI_STORE = 0, EPI_STORE_F32 = 1, EPI_RESID = 2, EPI_QKV = 3, EPI_GLU = 4, EPI_DW2 = 5 };
 enum { ACT_NONE = 0, ACT_RELU = 1, ACT_SILU = 2 };
 
@@ -126,9 +130,12 @@ int conv_dw_ln_silu(const T* glu, const int32_t* desc, int nblk, int d, const fl
                     const float* bdw, const float* lnw, const float* lnb, float eps, T* out, hipStream_t st,
                     int dot2 = 1, int dma = 1);
 
-// front-end (frontend.hip): meta rows give (src_row, nvalid) per window at PM_SRC_ROW / PM_NVALID
+// front-end (frontend.hip): meta rows give (src_row, nvalid) per window at PM_SRC_ROW / PM_NVALID;
+// with `tab` (device array of per-utterance row pointers) window c of utterance u starts at
+// tab[u] + c * step rows instead (PM_UTT / PM_CHUNK)
 template <typename T>
-int frontend_conv0_dw(const float* feats, const int32_t* meta, int meta_stride, int nwin, int W,
+int frontend_conv0_dw(const float* feats, const float* const* tab, int step, const int32_t* meta, int meta_stride,
+                      int nwin, int W,
                       const float* cmvn_mean, const float* cmvn_istd, const float* w0, const float* b0,
                       const float* w1, const float* b1, const float* wpack, int d, T* out, hipStream_t st);
 // per-channel [w0 taps 0..8 | w1 taps 0..8 | b0 | b1 | pad 2] (FE_WPACK floats) for the bf16 MFMA front-end

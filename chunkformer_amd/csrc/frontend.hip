@@ -27,8 +27,17 @@ constexpr int FE_IN_ROWS = 2 * FE_T1_ROWS + 1;  // input rows per block
 constexpr int FE_F0 = 80, FE_F1 = 39, FE_F2 = 19, FE_F3 = 9;
 constexpr int FE_CG = 16;                     // channels per LDS pass
 
+// First feature row of a window: packed mode (feats = the utterances concatenated, plan row
+// PM_SRC_ROW) or table mode (tab[utt] = that utterance's own [T, 80] rows, window c at row c * step),
+// so forward_parallel_chunk's caller-owned tensors are read in place, with no concatenation copy.
+__device__ __forceinline__ const float* window_rows(const float* feats, const float* const* tab, int step,
+                                                   const int32_t* m) {
+  return tab ? tab[m[PM_UTT]] + (size_t)m[PM_CHUNK] * step * FE_F0 : feats + (size_t)m[PM_SRC_ROW] * FE_F0;
+}
+
 template <typename T>
-__global__ __launch_bounds__(256) void fe_conv0_dw_kernel(const float* __restrict__ feats, const int32_t* __restrict__ meta,
+__global__ __launch_bounds__(256) void fe_conv0_dw_kernel(const float* __restrict__ feats, const float* const* __restrict__ tab,
+                                                          int step, const int32_t* __restrict__ meta,
                                                           int meta_stride, int W, int T2, const float* __restrict__ cm,
                                                           const float* __restrict__ ci, const float* __restrict__ w0,
                                                           const float* __restrict__ b0, const float* __restrict__ w1,
@@ -40,12 +49,12 @@ __global__ __launch_bounds__(256) void fe_conv0_dw_kernel(const float* __restric
   const int t2_0 = blockIdx.x * FE_T2_TILE;
   const int nt2 = min(FE_T2_TILE, T2 - t2_0);
   const int T1 = (W - 3) / 2 + 1;
-  const int src = meta[(size_t)win * meta_stride + PM_SRC_ROW];
+  const float* xsrc = window_rows(feats, tab, step, meta + (size_t)win * meta_stride);
   const int nvalid = meta[(size_t)win * meta_stride + PM_NVALID];
   const int r0 = 4 * t2_0;   // first input row
   for (int idx = tid; idx < FE_IN_ROWS * FE_F0; idx += 256) {
     const int r = idx / FE_F0, f = idx - r * FE_F0, gr = r0 + r;
-    float v = (gr < nvalid && gr < W) ? feats[(size_t)(src + gr) * FE_F0 + f] : 0.f;
+    float v = (gr < nvalid && gr < W) ? xsrc[(size_t)gr * FE_F0 + f] : 0.f;
     if (cm) v = (v - cm[f]) * ci[f];
     xin[idx] = v;
   }
@@ -108,6 +117,7 @@ constexpr int FE_POS_BLOCK = 128;                     // dw1 positions per block
 constexpr int FE_XROWS = 4 * ((FE_POS_BLOCK - 1) / FE_F2 + 2) + 3;   // staged input rows (>= 4*span + 7)
 
 __global__ __launch_bounds__(256, 3) void fe_conv0_dw_mfma_kernel(const float* __restrict__ feats,
+                                                               const float* const* __restrict__ tab, int step,
                                                                const int32_t* __restrict__ meta, int meta_stride,
                                                                int W, int T2, const float* __restrict__ cm,
                                                                const float* __restrict__ ci,
@@ -123,11 +133,11 @@ __global__ __launch_bounds__(256, 3) void fe_conv0_dw_mfma_kernel(const float* _
   const int P = T2 * FE_F2;
   const int p0 = blockIdx.x * FE_POS_BLOCK;
   const int r0 = 4 * (p0 / FE_F2);   // first staged input row
-  const int src = meta[(size_t)win * meta_stride + PM_SRC_ROW];
+  const float* xsrc = window_rows(feats, tab, step, meta + (size_t)win * meta_stride);
   const int nvalid = min(meta[(size_t)win * meta_stride + PM_NVALID], W);
   for (int idx = tid; idx < FE_XROWS * FE_F0; idx += 256) {
     const int r = idx / FE_F0, f = idx - r * FE_F0, gr = r0 + r;
-    float v = gr < nvalid ? feats[(size_t)(src + gr) * FE_F0 + f] : 0.f;
+    float v = gr < nvalid ? xsrc[(size_t)gr * FE_F0 + f] : 0.f;
     if (cm) v = (v - cm[f]) * ci[f];   // CMVN after padding, like cmvn.py:32-43 on the padded window
     xin[idx] = v;
   }
@@ -291,7 +301,8 @@ __global__ __launch_bounds__(256) void fe_dw2_kernel(const T* __restrict__ in, i
 }
 
 template <typename T>
-int frontend_conv0_dw(const float* feats, const int32_t* meta, int meta_stride, int nwin, int W,
+int frontend_conv0_dw(const float* feats, const float* const* tab, int step, const int32_t* meta, int meta_stride,
+                      int nwin, int W,
                       const float* cmvn_mean, const float* cmvn_istd, const float* w0, const float* b0,
                       const float* w1, const float* b1, const float* wpack, int d, T* out, hipStream_t st) {
   if (nwin <= 0) return 0;
@@ -302,9 +313,10 @@ int frontend_conv0_dw(const float* feats, const int32_t* meta, int meta_stride, 
     // one window's dw1 output is addressed by 32-bit byte offsets (buffer stores)
     if (d % 64 || (size_t)T2 * FE_F2 * d * sizeof(bf16) >= ((size_t)1 << 31)) return (int)hipErrorInvalidValue;
     hipLaunchKernelGGL(fe_conv0_dw_mfma_kernel, dim3((T2 * FE_F2 + FE_POS_BLOCK - 1) / FE_POS_BLOCK, nwin), dim3(256),
-                       0, st, feats, meta, meta_stride, W, T2, cmvn_mean, cmvn_istd, wpack, d, out);
+                       0, st, feats, tab, step, meta, meta_stride, W, T2, cmvn_mean, cmvn_istd, wpack, d, out);
   } else {
-    hipLaunchKernelGGL((fe_conv0_dw_kernel<T>), grid, dim3(256), 0, st, feats, meta, meta_stride, W, T2, cmvn_mean,
+    hipLaunchKernelGGL((fe_conv0_dw_kernel<T>), grid, dim3(256), 0, st, feats, tab, step, meta, meta_stride, W, T2,
+                       cmvn_mean,
                        cmvn_istd, w0, b0, w1, b1, d, out);
   }
   CFM_CHECK_LAUNCH();
@@ -325,9 +337,11 @@ int frontend_dw2(const T* in, int nwin, int T2, int d, const float* w, const flo
   return 0;
 }
 
-template int frontend_conv0_dw<float>(const float*, const int32_t*, int, int, int, const float*, const float*,
+template int frontend_conv0_dw<float>(const float*, const float* const*, int, const int32_t*, int, int, int, const float*,
+                                      const float*,
                                       const float*, const float*, const float*, const float*, const float*, int, float*, hipStream_t);
-template int frontend_conv0_dw<bf16>(const float*, const int32_t*, int, int, int, const float*, const float*,
+template int frontend_conv0_dw<bf16>(const float*, const float* const*, int, const int32_t*, int, int, int, const float*,
+                                     const float*,
                                      const float*, const float*, const float*, const float*, const float*, int, bf16*, hipStream_t);
 template int frontend_dw2<float>(const float*, int, int, int, const float*, const float*, float*, hipStream_t, int);
 template int frontend_dw2<bf16>(const bf16*, int, int, int, const float*, const float*, bf16*, hipStream_t, int);

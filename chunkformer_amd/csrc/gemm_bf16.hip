@@ -216,13 +216,7 @@ template <int EPI, int ACT>
 static int launch256(const bf16* A, int lda, const bf16* W, int ldw, int M, int N, int K, const EpiArgs& ep,
                      hipStream_t st) {
   const int tiles = ((M + 255) / 256) * (N / 256);
-  static int n_cu = 0;
-  if (!n_cu) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0) n_cu = 256;
-    n_cu = (n_cu + 7) / 8 * 8;
-  }
+  const int n_cu = (cu_count() + 7) / 8 * 8;
   const int grid = tiles <= n_cu ? tiles : n_cu;   // persistent: one 512-thread block per CU
   // ep.diag (timing diagnostics, model option "gemm_diag"): 1 no MFMA, 2 no DMA in the loop, 3 no
   // epilogue, 5 / 6 wave-group priorities

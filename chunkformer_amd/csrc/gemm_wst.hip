@@ -805,13 +805,7 @@ __global__ __launch_bounds__(256, 1) void gemm_wsp_kernel(const bf16* __restrict
 template <int EPI, int ACT>
 static int launch_wst(const bf16* A, int lda, const bf16* W, int ldw, int M, int N, const EpiArgs& ep,
                       hipStream_t st) {
-  static int n_cu = 0;
-  if (!n_cu) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0) n_cu = 256;
-    n_cu = n_cu / 8 * 8;
-  }
+  const int n_cu = cu_count() / 8 * 8;
   // buffer descriptors are built per 64-row tile on 64-bit bases (offsets inside one tile stay
   // below 64 rows x ld), so outputs past 2 GiB (a 980-minute batch's FFN hidden: 3 GB) stay here
 #define WSP_LAUNCH(D) hipLaunchKernelGGL((gemm_wsp_kernel<EPI, ACT, D>), dim3(n_cu), dim3(256), 0, st, A, lda, W, ldw, M, N, ep)

@@ -1,8 +1,23 @@
 // Small kernels: relative PE table, cache carry, mask materialisation, CTC log-softmax.
+#include <atomic>
 #include "cfm_common.h"
 #include "cfm_kernels.h"
 
 namespace cfm {
+
+int cu_count() {
+  static std::atomic<int> cache[64];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0) dev = 0;
+  if (dev >= 64) dev = 63;
+  int n = cache[dev].load(std::memory_order_relaxed);
+  if (n <= 0) {
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    cache[dev].store(n, std::memory_order_relaxed);
+  }
+  return n;
+}
+
 
 // Relative PE rows (embedding.py:119-142 / 144-174): row k <-> distance p = anchor - k,
 // [2i] = sin(p * div_i), [2i+1] = cos(p * div_i), div_i = exp(2i * -(ln 1e4 / d)); f32 math.

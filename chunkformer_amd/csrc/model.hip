@@ -159,7 +159,8 @@ struct cfm_model {
   // over consecutive stage ranges with the same workspace give the same result.
   virtual cfm_status encode(const float* feats, const int32_t* plan_dev, const int32_t* plan_hdr, const float* aci,
                             const float* cci, int trunc, float* aco, float* cco, float* out, void* ws, size_t wsb,
-                            hipStream_t st, int cache_b = 1, int stage_lo = -1, int stage_hi = 1 << 30) const = 0;
+                            hipStream_t st, int cache_b = 1, int stage_lo = -1, int stage_hi = 1 << 30,
+                            const float* const* feats_tab = nullptr) const = 0;
   virtual cfm_status ctc(const float* enc, int rows, float* logp, int32_t* ids, void* ws, size_t wsb,
                          hipStream_t st) const = 0;
   virtual size_t ws_bytes(const int32_t* hdr) const = 0;
@@ -250,7 +251,8 @@ struct ModelT : public cfm_model {
 
   cfm_status encode(const float* feats, const int32_t* plan_dev, const int32_t* hh, const float* aci, const float* cci,
                     int trunc, float* aco, float* cco, float* out, void* ws, size_t wsb,
-                    hipStream_t st, int cache_b, int stage_lo, int stage_hi) const override {
+                    hipStream_t st, int cache_b, int stage_lo, int stage_hi,
+                    const float* const* feats_tab) const override {
     const int d = cfg.d_model, ff = cfg.ffn_dim, H = cfg.n_heads, dk = d / H;
     const float eps = cfg.norm_eps;
     const int rows = hh[PH_ROWS], C = hh[PH_C], L = hh[PH_L];
@@ -282,12 +284,15 @@ struct ModelT : public cfm_model {
     const int G = fe_group(hh);
     for (int g0 = 0; g0 < nwin; g0 += G) {
       const int ng = std::min(G, nwin - g0);
-      PROF(PC_FE_CONV, frontend_conv0_dw<T>(feats, meta + (size_t)g0 * PLAN_REC, PLAN_REC, ng, Wn, fe.cm, fe.ci, fe.w0, fe.b0,
+      PROF(PC_FE_CONV, frontend_conv0_dw<T>(feats, feats_tab, 8 * C, meta + (size_t)g0 * PLAN_REC, PLAN_REC, ng, Wn,
+                                fe.cm, fe.ci, fe.w0, fe.b0,
                                 fe.w1, fe.b1, fe.wpack, d, w.feA, st));
       EpiArgs e1 = E(SITE_FE); e1.bias = fe.b_pw1; e1.out = w.feB; e1.ldo = d;
       T* dw2_rows = w.feA;   // the pw2 GEMM's input
       if constexpr (std::is_same<T, bf16>::value) {
-        if (tune.fe_fuse_dw2) {   // pw1 + ReLU + dw2 in one kernel: dw2 rows straight into feB
+        // pw1 + ReLU + dw2 in one weight-stationary kernel (so "gemm_wst" 0 turns it off too): dw2 rows
+        // straight into feB
+        if (tune.fe_fuse_dw2 && tune.gemm_wst) {
           EpiArgs ef = e1; ef.dw_w = fe.w2; ef.dw_b = fe.b2; ef.t2n = T2; ef.t3n = T3;
           int r = -1;
           PROF(PC_FE_GEMM, (r = gemm_bf16_wst(EPI_DW2, ACT_RELU, w.feA, d, (const bf16*)fe.pw1, d, ng * T2 * 19, d, d, ef, st),
@@ -737,6 +742,17 @@ cfm_status cfm_encode_masked(const cfm_model* m, const float* feats, const int32
   if ((aci == nullptr) != (cci == nullptr)) return set_error(CFM_ERR_VALUE, "att_cache and cnn_cache must be given together");
   HIPC(hipSetDevice(m->device));
   return m->encode(feats, plan_dev, h, aci, cci, trunc, aco, cco, out, ws, wsb, (hipStream_t)stream);
+}
+
+cfm_status cfm_encode_masked_utts(const cfm_model* m, const float* const* utt_feats, const int32_t* h,
+                                  const int32_t* plan_dev, const float* aci, const float* cci, int32_t trunc, float* aco,
+                                  float* cco, float* out, void* ws, size_t wsb, cfm_stream stream) {
+  if (!m || !utt_feats || !h || !plan_dev || !out) return set_error(CFM_ERR_VALUE, "null argument");
+  if (h[PH_KIND] != 1) return set_error(CFM_ERR_VALUE, "not a masked-batch plan");
+  if ((aci == nullptr) != (cci == nullptr)) return set_error(CFM_ERR_VALUE, "att_cache and cnn_cache must be given together");
+  HIPC(hipSetDevice(m->device));
+  return m->encode(nullptr, plan_dev, h, aci, cci, trunc, aco, cco, out, ws, wsb, (hipStream_t)stream, 1, -1, 1 << 30,
+                   utt_feats);
 }
 
 cfm_status cfm_encode_masked_stages(const cfm_model* m, const float* feats, const int32_t* h, const int32_t* plan_dev,

@@ -30,6 +30,7 @@ import math
 from dataclasses import dataclass
 from typing import Dict, List, Optional, Sequence, Tuple
 
+import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -184,26 +185,48 @@ def run_pieces(encoder, xs: Sequence[torch.Tensor], shard: Sequence[Piece], C: i
     lens = torch.tensor([p.frames for p in shard], dtype=torch.int32)
     out, _, n_chunks, _, _, _ = encoder.forward_parallel_chunk(feats, lens, C, L, R)
     flat = out.reshape(-1, out.shape[-1])
-    starts, o = [], 0
-    for nc in n_chunks:
-        starts.append(o)
-        o += nc * C
-    idx = torch.cat([torch.arange(s + p.skip, s + p.skip + p.rows) for s, p in zip(starts, shard)])
-    kept = flat.index_select(0, idx.to(flat.device))
+    starts = np.cumsum([0] + [nc * C for nc in n_chunks])
+    idx = np.concatenate([np.arange(s + p.skip, s + p.skip + p.rows) for s, p in zip(starts, shard)])
+    kept = flat.index_select(0, torch.from_numpy(idx).to(flat.device))
     logp, ids = encoder.ctc_log_softmax(kept, want_logp=want_logp, want_ids=want_ids) if (want_ids or want_logp) \
         else (None, None)
     return kept, ids, logp
 
 
-def _assemble(buf: torch.Tensor, shards: List[List[Piece]], n_utt: int, lens: Sequence[int]) -> List[torch.Tensor]:
-    """buf [world, max_rows, ...] -> per-utterance tensors [out_len(T_u), ...]."""
-    res = [buf.new_zeros((out_len(lens[u]),) + tuple(buf.shape[2:])) for u in range(n_utt)]
+def assemble_index(shards: List[List[Piece]], lens: Sequence[int], mx: int) -> Tuple[np.ndarray, List[int]]:
+    """Source row, in the gathered [world * mx] buffer, of every output row of the batch (the
+    utterances' rows concatenated in utterance order), and the per-utterance row counts.  Every row
+    of every utterance is kept by exactly one piece of a plan_shards plan."""
+    out_lens = [out_len(t) for t in lens]
+    starts = np.cumsum([0] + out_lens)
+    idx = np.full(int(starts[-1]), -1, np.int64)
     for r, shard in enumerate(shards):
-        o = 0
+        o = r * mx
         for p in shard:
-            res[p.utt][p.row0: p.row0 + p.rows] = buf[r, o: o + p.rows]
+            d0 = int(starts[p.utt]) + p.row0
+            idx[d0: d0 + p.rows] = np.arange(o, o + p.rows)
             o += p.rows
-    return res
+    if (idx < 0).any():
+        raise ValueError("the shard plan does not keep every output row")
+    return idx, out_lens
+
+
+_INDEX_CACHE: Dict[tuple, Tuple[torch.Tensor, List[int]]] = {}
+
+
+def _assemble(buf: torch.Tensor, shards: List[List[Piece]], n_utt: int, lens: Sequence[int]) -> List[torch.Tensor]:
+    """buf [world, max_rows, ...] -> per-utterance tensors [out_len(T_u), ...]: ONE index_select
+    over the gathered rows with an index built once per plan (kept on buf's device), then views."""
+    key = (tuple(tuple(s) for s in shards), tuple(int(t) for t in lens[:n_utt]), buf.shape[1], str(buf.device))
+    hit = _INDEX_CACHE.get(key)
+    if hit is None:
+        idx, out_lens = assemble_index(shards, lens[:n_utt], buf.shape[1])
+        if len(_INDEX_CACHE) >= 8:
+            _INDEX_CACHE.clear()
+        hit = _INDEX_CACHE[key] = (torch.from_numpy(idx).to(buf.device), out_lens)
+    idx, out_lens = hit
+    flat = buf.reshape((-1,) + tuple(buf.shape[2:])).index_select(0, idx)
+    return list(flat.split(out_lens))
 
 
 def _comm_device(t: torch.Tensor, group) -> torch.device:

@@ -3,7 +3,7 @@
 Same method names, argument meaning, return tuples and error types as the
 reference; every tensor op of the hot path runs in libcfm.so (HIP, gfx950):
 
-  forward_parallel_chunk  encoder.py:503-681   -> cfm_plan_masked + cfm_encode_masked
+  forward_parallel_chunk  encoder.py:503-681   -> cfm_plan_masked + cfm_encode_masked_utts
   forward_encoder         encoder.py:220-274   -> cfm_plan_padded + cfm_encode_padded
   forward                 encoder.py:461-501   (eval branch: negative sizes -> 0/0/0)
   forward_chunk           encoder.py:310-385   -> cfm_plan_stream + cfm_encode_stream (realtime path)
@@ -126,9 +126,9 @@ class ChunkFormerEncoder:
                                                     mask_lens=None if lens == mask_lens else mask_lens)
         N = sum(n_chunks)
         d = self.cfg.d_model
-        feats = torch.cat([x.to(dev, torch.float32).reshape(-1, self.cfg.input_dim) for x in xs], 0).contiguous()
-        if feats.shape[0] == 0:
-            feats = torch.zeros(1, self.cfg.input_dim, device=dev)
+        # the utterances are read where they are (cfm_encode_masked_utts: a device table of B row
+        # pointers), not concatenated first; only inputs that are not already f32 on this device are copied
+        utts = [x.to(dev, torch.float32).reshape(-1, self.cfg.input_dim).contiguous() for x in xs]
         out = torch.empty(N * C, d, dtype=torch.float32, device=dev)
         has_cache = att_cache.size(0) > 0
         aci = cci = aco = cco = None
@@ -144,13 +144,21 @@ class ChunkFormerEncoder:
             cco = torch.empty_like(cci)
         parts = min(self.stream_split, B)
         if not has_cache and parts > 1 and N >= self.split_min_chunks:
+            feats = torch.cat(utts, 0)
             self._encode_masked_split(feats, lens, offs, mask_lens, n_chunks, parts, C, L, R, out)
         else:
             plan_dev = self._upload(plan)
             ws_bytes = _lib.cfm_workspace_bytes_masked(self._h, N, C, L, R)
             ws = self._workspace(ws_bytes)
-            self._last_plan = (plan, plan_dev)   # keep the uploaded plan alive until the stream consumed it
-            self._encode_masked_raw(feats, plan, plan_dev, aci, cci, int(truncated_context_size), aco, cco, out, ws)
+            # an empty utterance still needs a readable row pointer (its windows read no rows)
+            tab = self._upload(torch.tensor([u.data_ptr() if u.numel() else out.data_ptr() for u in utts],
+                                            dtype=torch.int64))
+            # the uploaded plan, pointer table and utterance tensors stay alive until the stream consumed them
+            self._last_plan = (plan, plan_dev, tab, utts)
+            _lib.check(_lib.cfm_encode_masked_utts(self._h, tab.data_ptr(), plan.data_ptr(), plan_dev.data_ptr(),
+                                                   _lib.ptr(aci), _lib.ptr(cci), int(truncated_context_size),
+                                                   _lib.ptr(aco), _lib.ptr(cco), out.data_ptr(), ws.data_ptr(),
+                                                   ws_bytes, self._stream()))
         xs_lens = torch.tensor(out_lens, dtype=torch.int32, device=xs_origin_lens.device)
         offset += xs_lens.to(offset.device)
         if has_cache:

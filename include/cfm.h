@@ -135,6 +135,15 @@ cfm_status cfm_encode_masked(const cfm_model* m, const float* feats_dev, const i
                              float* att_cache_out, float* cnn_cache_out, float* out_dev, void* workspace,
                              size_t workspace_bytes, cfm_stream stream);
 
+/* cfm_encode_masked reading each utterance's fbank where the caller holds it: utt_feats_dev is a
+ * DEVICE array of B pointers, utterance b's [x.size(0), 80] f32 rows (the reference's list `xs`,
+ * encoder.py:553-564), in the order of the plan's lengths.  Same result as cfm_encode_masked on the
+ * concatenation, without the concatenation copy (torch.cat at encoder.py:606). */
+cfm_status cfm_encode_masked_utts(const cfm_model* m, const float* const* utt_feats_dev, const int32_t* plan_host,
+                                  const int32_t* plan_dev, const float* att_cache_in, const float* cnn_cache_in,
+                                  int32_t truncated_context_size, float* att_cache_out, float* cnn_cache_out,
+                                  float* out_dev, void* workspace, size_t workspace_bytes, cfm_stream stream);
+
 /* cfm_encode_masked in stages, for pipelining consecutive endless_decode segments (segment k + 1's
  * layer l needs only segment k's layer-l caches): stage -1 = the front-end, relative positions and the
  * first LayerNorm; stage l = encoder layer l (the last one ends with after_norm into out_dev).  Calls

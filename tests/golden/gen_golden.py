@@ -33,7 +33,7 @@ from chunkformer.modules.cmvn import GlobalCMVN  # noqa: E402
 from chunkformer.modules.ctc import CTC  # noqa: E402
 from chunkformer.modules.encoder import ChunkFormerEncoder  # noqa: E402
 
-from chunkformer_amd.config import LARGE, LARGE_4H, SMALL, EncoderConfig  # noqa: E402
+from chunkformer_amd.config import LARGE, LARGE_4H, SMALL, SMALL256, EncoderConfig  # noqa: E402
 from chunkformer_amd.weights import synthetic_features, synthetic_state_dict, synthetic_vocab  # noqa: E402
 
 torch.set_num_threads(8)
@@ -381,6 +381,32 @@ def gen_endless_tbd(path, cfg=SMALL, seed=1):
                         ids=ids.numpy().astype(np.int32), att=ac.numpy(), cnn=cc.numpy())
 
 
+def gen_small256(path, seed=2):
+    """The reference's shipped small recipes (examples/asr/ctc/conf/chunkformer-ctc-small-libri-100h.yaml:5-8,
+    likewise the rnnt-small and libri-960h recipes): d=256, 4 heads (head_dim 64), ff 2048, 12 blocks,
+    bpe1024 vocabulary.  (a) masked batch at the decoding default C=64 L=R=128 with CTC ids and top-2
+    margins; (b) the padded chunked path (encode()) on the same utterances; (c) a masked batch with
+    C=128 L=R=128 (one of the recipe's dynamic_chunk_sizes, > 64 queries per chunk)."""
+    cfg = SMALL256
+    enc, ctc, sd = build_reference(cfg, seed)
+    lens = [3000, 1234, 600]
+    xs = feats(lens, 8)
+    with torch.no_grad():
+        r = enc.forward_parallel_chunk(xs, torch.tensor(lens), 64, 128, 128)
+        logp = ctc.log_softmax(r[0])
+        xp = torch.zeros(len(lens), max(lens), 80)
+        for i, t in enumerate(xs):
+            xp[i, : t.shape[0]] = t
+        y, masks = enc.forward_encoder(xp, torch.tensor(lens), 64, 128, 128)
+        r2 = enc.forward_parallel_chunk(xs, torch.tensor(lens), 128, 128, 128)
+    top2 = torch.topk(logp, 2, dim=-1).values
+    np.savez_compressed(path, sd_digest=sd_digest(sd), seed=np.array(seed), lens=np.array(lens, np.int32),
+                        feat_seed=np.array(8), out=r[0].numpy(), outlens=r[1].numpy(),
+                        nchunks=np.array(r[2], np.int32), ids=logp.argmax(-1).numpy().astype(np.int32),
+                        top2=top2.numpy(), pc_out=y.numpy(), pc_mask=masks.numpy(),
+                        c128_out=r2[0].numpy(), c128_nchunks=np.array(r2[2], np.int32), c128_outlens=r2[1].numpy())
+
+
 def gen_rows_neq(path, cfg=SMALL, seed=1):
     """forward_parallel_chunk with x.size(0) != xs_origin_lens (encoder.py:556-596, 673): the rows are
     padded and unfolded from x.size(0) while the masks and output lengths follow xs_origin_lens; the
@@ -388,11 +414,19 @@ def gen_rows_neq(path, cfg=SMALL, seed=1):
     enc, _, sd = build_reference(cfg, seed)
     rows, lens, C, L, R = [700, 237, 1100, 300], [690, 230, 1100, 271], 16, 32, 32
     xs = feats(rows, 55)
+    # (gt) the other direction, xs_origin_lens > x.size(0) with equal chunk counts (690 rows, lens 695;
+    # 240 rows, lens 245): the masks reach past the real rows, which the reference fills with zeros
+    gt_rows, gt_lens = [690, 240, 500], [695, 245, 500]
+    gt_xs = feats(gt_rows, 56)
     with torch.no_grad():
         r = enc.forward_parallel_chunk(xs, torch.tensor(lens), C, L, R)
+        r2 = enc.forward_parallel_chunk(gt_xs, torch.tensor(gt_lens), C, L, R)
     np.savez_compressed(path, sd_digest=sd_digest(sd), seed=np.array(seed), feat_seed=np.array(55),
                         rows=np.array(rows, np.int32), lens=np.array(lens, np.int32), clr=np.array([C, L, R], np.int32),
-                        out=r[0].numpy(), outlens=r[1].numpy(), nchunks=np.array(r[2], np.int32))
+                        out=r[0].numpy(), outlens=r[1].numpy(), nchunks=np.array(r[2], np.int32),
+                        gt_feat_seed=np.array(56), gt_rows=np.array(gt_rows, np.int32),
+                        gt_lens=np.array(gt_lens, np.int32), gt_out=r2[0].numpy(), gt_outlens=r2[1].numpy(),
+                        gt_nchunks=np.array(r2[2], np.int32))
 
 
 ENDLESS_RNNT_FRAMES = 480
@@ -448,9 +482,49 @@ def gen_rnnt(path, seed=3, n_steps=64):
                         margin_batch=np.array(m_b), margin_endless=np.array(m_e))
 
 
+SPARSE_BLANK_BIAS = 7.0   # with enc_scale 8: 80% of the frames decide blank first
+SPARSE_ENC_SCALE = 8.0
+
+
+def gen_rnnt_sparse(path, seed=3, n_steps=64, blank_bias=SPARSE_BLANK_BIAS, enc_scale=SPARSE_ENC_SCALE):
+    """As gen_rnnt's endless half (optimized_search, B=1, the first ENDLESS_RNNT_FRAMES rows of
+    large_endless.npz) with a larger blank bias and a frame-dependent joint (enc_ffn x8), so that
+    blank dominates: 80% of the frames decide blank at their first step, in runs (the regime where
+    the kernel's 8-frame blank-block skip decides most frames); decisions at n_steps 64 and 3."""
+    from chunkformer.transducer.joint import TransducerJoint
+    from chunkformer.transducer.predictor import RNNPredictor
+    from chunkformer.transducer.search.greedy_search import optimized_search
+
+    from chunkformer_amd.transducer import RNNTConfig, synthetic_transducer_state_dict
+    c = RNNTConfig()
+    sd = synthetic_transducer_state_dict(c, seed, blank_bias=blank_bias, enc_scale=enc_scale)
+    pred = RNNPredictor(c.vocab, c.embed_size, c.pred_out, 0.1, c.hidden, c.num_layers, True, "lstm", 0.1).eval()
+    joint = TransducerJoint(c.vocab, c.enc_dim, c.pred_out, c.join_dim, True, False, "add", "tanh").eval()
+    pred.load_state_dict({k[len("predictor."):]: v for k, v in sd.items() if k.startswith("predictor.")}, strict=True)
+    joint.load_state_dict({k[len("joint."):]: v for k, v in sd.items() if k.startswith("joint.")}, strict=True)
+    model = types.SimpleNamespace(predictor=pred, joint=joint, blank=0)
+    ge = np.load(os.path.join(HERE, "large_endless.npz"))
+    enc_e = torch.from_numpy(ge["out"][:ENDLESS_RNNT_FRAMES]).unsqueeze(0)
+    with torch.no_grad():
+        out_e = optimized_search(model, enc_e, torch.tensor([enc_e.shape[1]]), n_steps)
+        out_3 = optimized_search(model, enc_e, torch.tensor([enc_e.shape[1]]), 3)
+    from oracle import rnnt_ref
+    _, m_e = rnnt_ref.optimized_search(sd, c.num_layers, c.hidden, enc_e, [enc_e.shape[1]], n_steps)
+    _, m_3 = rnnt_ref.optimized_search(sd, c.num_layers, c.hidden, enc_e, [enc_e.shape[1]], 3)
+    m_e = min(m_e, m_3)
+    d = out_e.reshape(1, -1, n_steps)
+    first = d[..., 0]
+    print(f"rnnt sparse: frames {first.numel()}, blank-first {float((first == 0).float().mean()):.3f}, "
+          f"tokens {int((d != 0).sum())}, max steps/frame {int((d != 0).sum(-1).max())}, min margin {m_e:.2e}")
+    np.savez_compressed(path, seed=np.array(seed), n_steps=np.array(n_steps), vocab=np.array(c.vocab),
+                        blank_bias=np.array(blank_bias), enc_scale=np.array(enc_scale), endless_out=out_e.numpy().astype(np.int32),
+                        endless_out_steps3=out_3.numpy().astype(np.int32),
+                        margin_endless=np.array(m_e))
+
+
 if __name__ == "__main__":
     which = sys.argv[1:] or ["masks", "small", "large", "large_4h", "large_endless", "large_full", "text", "stream",
-                             "endless_tbd", "rnnt", "rows_neq"]
+                             "endless_tbd", "rnnt", "rows_neq", "small256", "rnnt_sparse"]
     if "masks" in which:
         gen_masks(os.path.join(HERE, "masks.npz"))
     if "small" in which:
@@ -473,4 +547,8 @@ if __name__ == "__main__":
         gen_rows_neq(os.path.join(HERE, "rows_neq.npz"))
     if "rnnt" in which:
         gen_rnnt(os.path.join(HERE, "rnnt.npz"))
+    if "small256" in which:
+        gen_small256(os.path.join(HERE, "small256.npz"))
+    if "rnnt_sparse" in which:
+        gen_rnnt_sparse(os.path.join(HERE, "rnnt_sparse.npz"))
     print("ok", which)

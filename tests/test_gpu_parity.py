@@ -217,7 +217,7 @@ def test_masked_batch_rejects_length_mismatch(cfm, small_models):
 
 @pytest.mark.parametrize("dtype", ["fp32", "bf16"])
 def test_rows_differ_from_origin_lens(golden_dir, dtype):
-    """forward_parallel_chunk with utterances longer than xs_origin_lens (the reference unfolds
+    """forward_parallel_chunk with x.size(0) != xs_origin_lens in both directions (the reference unfolds
     x.size(0) rows and bounds masks / output lengths by xs_origin_lens) against the reference."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
@@ -227,13 +227,16 @@ def test_rows_differ_from_origin_lens(golden_dir, dtype):
     g = np.load(os.path.join(golden_dir, "rows_neq.npz"))
     C, L, R = (int(v) for v in g["clr"])
     enc = ChunkFormerEncoder(SMALL, synthetic_state_dict(SMALL, int(g["seed"])), dtype=dtype)
-    xs = synthetic_features(g["rows"].tolist(), int(g["feat_seed"]))
-    off = torch.zeros(len(xs), dtype=torch.long)
-    out, olens, nch, _, _, off2 = enc.forward_parallel_chunk(xs, torch.tensor(g["lens"]), C, L, R, offset=off)
-    assert nch == g["nchunks"].tolist() and olens.tolist() == g["outlens"].tolist()
-    assert off2.tolist() == g["outlens"].tolist()
-    if dtype == "fp32":
-        np.testing.assert_allclose(out.cpu().numpy(), g["out"], atol=1e-4, rtol=0)
-    else:
-        o = out.cpu().numpy().astype(np.float64)
-        assert np.linalg.norm(o - g["out"]) / np.linalg.norm(g["out"]) <= 2e-2
+    # "": rows > xs_origin_lens; "gt_": xs_origin_lens > rows (the masks reach past the real rows)
+    for pre in ("", "gt_"):
+        xs = synthetic_features(g[pre + "rows"].tolist(), int(g[pre + "feat_seed"]))
+        off = torch.zeros(len(xs), dtype=torch.long)
+        out, olens, nch, _, _, off2 = enc.forward_parallel_chunk(xs, torch.tensor(g[pre + "lens"]), C, L, R,
+                                                                 offset=off)
+        assert nch == g[pre + "nchunks"].tolist() and olens.tolist() == g[pre + "outlens"].tolist()
+        assert off2.tolist() == g[pre + "outlens"].tolist()
+        if dtype == "fp32":
+            np.testing.assert_allclose(out.cpu().numpy(), g[pre + "out"], atol=1e-4, rtol=0, err_msg=pre)
+        else:
+            o = out.cpu().numpy().astype(np.float64)
+            assert np.linalg.norm(o - g[pre + "out"]) / np.linalg.norm(g[pre + "out"]) <= 2e-2, pre

@@ -56,6 +56,23 @@ def test_endless_b1_matches_reference(rnnt, golden_dir):
     np.testing.assert_array_equal(out.cpu().numpy(), g["endless_out"])
 
 
+@pytest.mark.parametrize("key,n_steps", [("endless_out", 64), ("endless_out_steps3", 3)])
+def test_sparse_emission_matches_reference(golden_dir, key, n_steps):
+    """rnnt_sparse.npz: a blank-dominated joint (80% of the frames decide blank first, in runs), B=1
+    over the endless encoder rows: the regime of the kernel's 8-frame blank-block skip."""
+    from chunkformer_amd.transducer import RNNTConfig, RNNTGreedy, synthetic_transducer_state_dict
+    g = np.load(os.path.join(golden_dir, "rnnt_sparse.npz"))
+    c = RNNTConfig(vocab=int(g["vocab"]))
+    sd = synthetic_transducer_state_dict(c, int(g["seed"]), blank_bias=float(g["blank_bias"]),
+                                         enc_scale=float(g["enc_scale"]))
+    dec = RNNTGreedy(c, sd, "cuda")
+    ge = np.load(os.path.join(golden_dir, "large_endless.npz"))
+    T = g[key].shape[1] // n_steps
+    enc = torch.from_numpy(ge["out"][:T]).unsqueeze(0).cuda()
+    out = dec.optimized_search(enc, torch.tensor([T]), n_steps)
+    np.testing.assert_array_equal(out.cpu().numpy(), g[key])
+
+
 @pytest.mark.parametrize("n_steps", [1, 3])
 def test_small_cap_and_ragged_vs_oracle(rnnt, n_steps):
     """n_steps 1 / 3 (the cap reached often), ragged packed utterances incl. empty and one frame."""

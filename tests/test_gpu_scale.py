@@ -307,26 +307,95 @@ def test_wide_windows_fall_back_correctly(C, L, R):
             assert _rel_l2(out, r_out) <= BF16_RELL2
 
 
-def test_head_dim_128_kernel_vs_generic():
-    """The head_dim 128 masked-batch kernel (attention128.hip) against the generic per-block kernel
-    (model option ring_attention = 0) on the 4-head d=512 model, 12 layers, a batch with utterance
-    starts / ends (masked key ranges), a 1-chunk utterance and a T < 15 one."""
+@pytest.fixture(scope="module")
+def model_4h():
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     from chunkformer_amd.config import LARGE_4H
     from chunkformer_amd.encoder import ChunkFormerEncoder
-    from chunkformer_amd.weights import synthetic_features, synthetic_state_dict
-    enc = ChunkFormerEncoder(LARGE_4H, synthetic_state_dict(LARGE_4H, 0), dtype="bf16")
-    lens = [30_000, 519, 3000, 7, 12_345, 1100, 64_000]
-    xs = synthetic_features(lens, 17)
+    from chunkformer_amd.weights import synthetic_state_dict
+    return ChunkFormerEncoder(LARGE_4H, synthetic_state_dict(LARGE_4H, 0), dtype="bf16")
+
+
+def _fast_vs_generic(enc, lens, seed, C, L, R):
+    from chunkformer_amd.weights import synthetic_features
+    xs = synthetic_features(lens, seed)
     tl = torch.tensor(lens, dtype=torch.int32)
-    fast = enc.forward_parallel_chunk(xs, tl, 64, 128, 128)[0].cpu().numpy()
+    fast = enc.forward_parallel_chunk(xs, tl, C, L, R)[0].cpu().numpy()
     enc.set_option("ring_attention", 0)
     try:
-        gen = enc.forward_parallel_chunk(xs, tl, 64, 128, 128)[0].cpu().numpy()
+        gen = enc.forward_parallel_chunk(xs, tl, C, L, R)[0].cpu().numpy()
     finally:
         enc.set_option("ring_attention", 1)
     assert np.isfinite(fast).all()
-    rel = _rel_l2(fast, gen)
-    print(f"head_dim 128 kernel vs generic: rel-L2 {rel:.2e}")
+    return _rel_l2(fast, gen)
+
+
+# every key-tile count the head_dim-128 kernel is built for (W = L + 64 + R = 64 .. 320, NT = 1 .. 5)
+@pytest.mark.parametrize("C,L,R", [(64, 0, 0), (64, 64, 0), (64, 64, 64), (64, 96, 96), (64, 128, 128)])
+def test_head_dim_128_kernel_vs_generic(model_4h, C, L, R):
+    """The head_dim 128 masked-batch kernel (attention128.hip) against the generic per-block kernel
+    (model option ring_attention = 0) on the 4-head d=512 model, 12 layers, a batch with utterance
+    starts / ends (masked key ranges), a 1-chunk utterance and a T < 15 one."""
+    rel = _fast_vs_generic(model_4h, [30_000, 519, 3000, 7, 12_345, 1100, 64_000], 17, C, L, R)
+    print(f"head_dim 128 kernel vs generic (C={C} L={L} R={R}): rel-L2 {rel:.2e}")
     assert rel <= 5e-3
+
+
+@pytest.mark.parametrize("C,L,R", [(64, 128, 128), (64, 64, 64), (64, 0, 0), (32, 64, 32), (48, 16, 32),
+                                   (16, 32, 32), (64, 128, 0)])
+def test_ring_kernel_shapes_vs_generic(large, C, L, R):
+    """The dk = 64 ring kernel against the generic kernel on chunkformer-large (12 layers, 8 heads)
+    over the chunk / context shapes it accepts (C % 16 == 0, W <= 320), utterance edges included."""
+    _, _, models = large
+    rel = _fast_vs_generic(models["bf16"], [20_000, 519, 3000, 7, 1100, 9000], 19, C, L, R)
+    print(f"ring kernel vs generic (C={C} L={L} R={R}): rel-L2 {rel:.2e}")
+    assert rel <= 5e-3
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_small256_recipe_shape(dtype):
+    """The reference's shipped small recipes (d=256, 4 heads, ff 2048, 12 blocks, bpe1024;
+    examples/asr/ctc/conf/chunkformer-ctc-small-libri-100h.yaml:5-8) against small256.npz: masked
+    batch at C=64 L=R=128 (+ CTC ids), the padded chunked path, and a C=128 masked batch."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from chunkformer_amd.config import SMALL256
+    from chunkformer_amd.encoder import ChunkFormerEncoder
+    from chunkformer_amd.weights import synthetic_features, synthetic_state_dict
+    from conftest import GOLDEN
+    g = np.load(os.path.join(GOLDEN, "small256.npz"))
+    enc = ChunkFormerEncoder(SMALL256, synthetic_state_dict(SMALL256, int(g["seed"])), dtype=dtype)
+    lens = g["lens"].tolist()
+    xs = synthetic_features(lens, int(g["feat_seed"]))
+    tl = torch.tensor(lens, dtype=torch.int32)
+    out, olens, nch, _, _, _ = enc.forward_parallel_chunk(xs, tl, 64, 128, 128)
+    assert nch == g["nchunks"].tolist() and olens.tolist() == g["outlens"].tolist()
+    _, ids = enc.ctc_log_softmax(out, want_logp=False)
+    ids = ids.cpu().numpy()
+    xp = torch.zeros(len(lens), max(lens), 80)
+    for i, t in enumerate(xs):
+        xp[i, : t.shape[0]] = t
+    y, masks = enc.forward_encoder(xp, torch.tensor(lens), 64, 128, 128)
+    np.testing.assert_array_equal(masks.cpu().numpy(), g["pc_mask"])
+    out2, olens2, nch2, _, _, _ = enc.forward_parallel_chunk(xs, tl, 128, 128, 128)
+    assert nch2 == g["c128_nchunks"].tolist() and olens2.tolist() == g["c128_outlens"].tolist()
+    margin = g["top2"][..., 0] - g["top2"][..., 1]
+    pairs = ((out, g["out"]), (y, g["pc_out"]), (out2, g["c128_out"]))
+    if dtype == "fp32":
+        for a, b in pairs:
+            np.testing.assert_allclose(a.float().cpu().numpy(), b, atol=1e-4, rtol=0)
+        sure = margin > 1e-3
+        np.testing.assert_array_equal(ids[sure], g["ids"][sure])
+    else:
+        for a, b in pairs:
+            assert _rel_l2(a.float().cpu().numpy(), b) <= BF16_RELL2
+        # this random-weight V=1024 head is flat: 10% of the frames have a reference top-2 margin
+        # below 1e-2 (chunkformer-large: 3%), the size of bf16's log-prob noise, so the 99% bar is
+        # taken over the frames whose margin exceeds it (overall agreement printed; measured 98.4%)
+        agree = (ids == g["ids"]).mean()
+        clear = margin >= 1e-2
+        print(f"small256 bf16: CTC argmax agreement {agree:.4f} overall, "
+              f"{(ids == g['ids'])[clear].mean():.4f} where the margin >= 1e-2")
+        assert (ids == g["ids"])[clear].mean() >= 0.99
+        np.testing.assert_array_equal(ids[margin > BF16_MARGIN], g["ids"][margin > BF16_MARGIN])

@@ -119,6 +119,45 @@ def test_large_4h_matches_reference(golden_dir):
     np.testing.assert_allclose(y.numpy(), g["pc_out"], atol=1e-4, rtol=0)
 
 
+def test_small256_matches_reference(golden_dir):
+    """The shipped small recipes' shape (d=256, 4 heads, ff 2048, 12 blocks): masked batch at
+    C=64 L=R=128 with CTC ids, the padded chunked path, and a C=128 masked batch."""
+    from chunkformer_amd.config import SMALL256
+    g = _load(golden_dir, "small256.npz")
+    sd = synthetic_state_dict(SMALL256, int(g["seed"]))
+    np.testing.assert_allclose(np.array([float(v.double().sum()) for v in sd.values()]), g["sd_digest"], rtol=0, atol=0)
+    lens = g["lens"].tolist()
+    xs = synthetic_features(lens, int(g["feat_seed"]))
+    out, olens, nch, _, _, _ = ref.forward_parallel_chunk(sd, SMALL256, xs, lens, 64, 128, 128)
+    assert nch == g["nchunks"].tolist() and olens.tolist() == g["outlens"].tolist()
+    np.testing.assert_allclose(out.numpy(), g["out"], atol=1e-4, rtol=0)
+    logp = ref.ctc_log_softmax(sd, out).numpy()
+    margin = g["top2"][..., 0] - g["top2"][..., 1]
+    sure = margin > 1e-4
+    np.testing.assert_array_equal(logp.argmax(-1)[sure], g["ids"][sure])
+    xp = torch.zeros(len(lens), max(lens), 80)
+    for i, t in enumerate(xs):
+        xp[i, : t.shape[0]] = t
+    y, masks = ref.forward_encoder(sd, SMALL256, xp, lens, 64, 128, 128)
+    np.testing.assert_array_equal(masks.numpy(), g["pc_mask"])
+    np.testing.assert_allclose(y.numpy(), g["pc_out"], atol=1e-4, rtol=0)
+    out2, olens2, nch2, _, _, _ = ref.forward_parallel_chunk(sd, SMALL256, xs, lens, 128, 128, 128)
+    assert nch2 == g["c128_nchunks"].tolist() and olens2.tolist() == g["c128_outlens"].tolist()
+    np.testing.assert_allclose(out2.numpy(), g["c128_out"], atol=1e-4, rtol=0)
+
+
+def test_rows_neq_both_directions_match_reference(golden_dir):
+    """x.size(0) != xs_origin_lens with equal chunk counts, rows > lens and rows < lens."""
+    g = _load(golden_dir, "rows_neq.npz")
+    sd = synthetic_state_dict(SMALL, int(g["seed"]))
+    C, L, R = (int(v) for v in g["clr"])
+    for pre in ("", "gt_"):
+        xs = synthetic_features(g[pre + "rows"].tolist(), int(g[pre + "feat_seed"]))
+        out, olens, nch, _, _, _ = ref.forward_parallel_chunk(sd, SMALL, xs, g[pre + "lens"].tolist(), C, L, R)
+        assert nch == g[pre + "nchunks"].tolist() and olens.tolist() == g[pre + "outlens"].tolist()
+        np.testing.assert_allclose(out.numpy(), g[pre + "out"], atol=2e-5, rtol=0, err_msg=pre)
+
+
 def oracle_endless(sd, cfg, x, C, L, R, tbd):
     """endless_decode's segment loop (chunkformer_model.py:344-435) driven on the oracle, with the
     host segment schedule of chunkformer_amd.model.endless_segments."""

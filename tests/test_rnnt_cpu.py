@@ -49,6 +49,23 @@ def test_oracle_matches_reference_endless_prefix(rnnt, golden_dir):
     np.testing.assert_array_equal(o.numpy(), g["endless_out"].reshape(-1, n)[:PREFIX])
 
 
+def test_oracle_matches_reference_sparse_emission(golden_dir):
+    """rnnt_sparse.npz: blank dominates (80% of the frames decide blank first, in runs)."""
+    g = np.load(os.path.join(golden_dir, "rnnt_sparse.npz"))
+    c = RNNTConfig(vocab=int(g["vocab"]))
+    sd = synthetic_transducer_state_dict(c, int(g["seed"]), blank_bias=float(g["blank_bias"]),
+                                         enc_scale=float(g["enc_scale"]))
+    ge = np.load(os.path.join(golden_dir, "large_endless.npz"))
+    n = int(g["n_steps"])
+    T = g["endless_out"].shape[1] // n
+    enc = torch.from_numpy(ge["out"][:T])
+    first = g["endless_out"].reshape(-1, n)[:, 0]
+    assert 0.7 <= (first == 0).mean() < 1.0
+    for key, steps in (("endless_out", n), ("endless_out_steps3", 3)):
+        o, _ = rnnt_ref.greedy_one(sd, c.num_layers, c.hidden, enc[:3 * PREFIX], steps)
+        np.testing.assert_array_equal(o.numpy(), g[key].reshape(-1, steps)[:3 * PREFIX], err_msg=key)
+
+
 def test_golden_exercises_every_branch(rnnt):
     """The fixture covers blank frames, frames with a few tokens ended by a blank, and frames that
     reach the n_steps cap; the batch hypotheses are the non-blank decisions in order."""
