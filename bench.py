@@ -279,10 +279,11 @@ def main():
                          "configs[3] (16 h endless_decode, graph-replayed segments); full = configs[4] (full "
                          "attention, B=256)")
     ap.add_argument("--hours", type=float, default=16.0, help="endless: audio hours")
-    ap.add_argument("--endless-mode", default="pipeline", choices=["pipeline", "graph"],
-                    help="endless: --pipeline-depth segments in flight on as many streams (pipeline) or one "
-                         "captured HIP graph replayed per middle segment (graph); both are bit-identical to the "
-                         "eager loop")
+    ap.add_argument("--endless-mode", default="graphpipe", choices=["graphpipe", "pipeline", "graph"],
+                    help="endless: --pipeline-depth segments in flight whose steady-state ticks replay captured "
+                         "HIP graphs (graphpipe), the same pipeline launched eagerly (pipeline), or one segment "
+                         "at a time replaying one captured graph per middle segment (graph); all bit-identical "
+                         "to the eager loop")
     ap.add_argument("--pipeline-depth", type=int, default=3, help="endless pipeline: segments in flight")
     ap.add_argument("--tbd", type=int, default=7200,
                     help="endless: total_batch_duration (s); a memory budget that does not change results "
@@ -562,7 +563,8 @@ def bench_single(args):
 
         def step():
             return model.endless_decode(x, C, L, R, total_batch_duration=args.tbd, return_timestamps=False,
-                                        pipeline=args.endless_mode == "pipeline", pipeline_depth=args.pipeline_depth)
+                                        pipeline=args.endless_mode in ("pipeline", "graphpipe"),
+                                        cuda_graph=args.endless_mode != "pipeline", pipeline_depth=args.pipeline_depth)
         from chunkformer_amd.model import endless_segments
         trunc, segs = endless_segments(T, C, L, R, args.tbd, LARGE.num_blocks, LARGE.kernel_size)
         seg_len = max(b - a for a, b, _, _ in segs)
@@ -573,11 +575,13 @@ def bench_single(args):
         workload = (f"endless_decode over one {args.hours:g} h utterance (synthetic N(0,1) fbank), C=64 L=128 "
                     f"R=128, total_batch_duration={args.tbd}: {len(segs)} segments of <= {seg_len} frames "
                     f"(trunc {trunc} rows kept each), att/cnn caches carried, " +
-                    (f"{args.pipeline_depth} segments in flight on {args.pipeline_depth} HIP streams (segment k+1 "
-                     "layer l waits for segment k layer l)"
-                     if args.endless_mode == "pipeline" else
-                     "middle segments replayed from one captured HIP graph (front-end + 12 blocks + after_norm + "
-                     "CTC argmax)"))
+                    {"graphpipe": f"{args.pipeline_depth} segments in flight (stage slots of a software pipeline "
+                                  "on as many HIP streams, each steady-state tick one replay of a captured HIP "
+                                  "graph; segment k+1's layer l after segment k's layer l)",
+                     "pipeline": f"{args.pipeline_depth} segments in flight on {args.pipeline_depth} HIP streams "
+                                 "(segment k+1 layer l waits for segment k layer l), launched eagerly",
+                     "graph": "middle segments replayed one at a time from one captured HIP graph (front-end + "
+                              "12 blocks + after_norm + CTC argmax)"}[args.endless_mode])
         extra = {"segments": len(segs), "segment_frames": seg_len, "truncated_context_size": trunc,
                  "endless_mode": args.endless_mode, "pipeline_depth": args.pipeline_depth}
     else:

@@ -13,6 +13,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 typedef __bf16 bf16;
 typedef bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -21,6 +23,15 @@ typedef float f32x8 __attribute__((ext_vector_type(8)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 #define CFM_DEV __device__ __forceinline__
+
+// compile-time loop: f(std::integral_constant<int, i>) for i = B .. E-1
+template <int B, int E, class F>
+CFM_DEV void sfor(F&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    sfor<B + 1, E>(f);
+  }
+}
 
 template <typename T> struct Frag;
 template <> struct Frag<float> { typedef f32x8 type; };

@@ -123,13 +123,6 @@ CFM_DEV void lds_read_into(bf16x8& v, unsigned addr) {
 }
 
 namespace {
-template <int B, int E, class F>
-CFM_DEV void sfor(F&& f) {
-  if constexpr (B < E) {
-    f(std::integral_constant<int, B>{});
-    sfor<B + 1, E>(f);
-  }
-}
 // micro-ops of epilogue group s (0..7).  STORE/QKV: two halves (one 16-column n-block each) of
 // [activation ops on 4 values, 2 packs], then 2 permlane swaps, 1 store, 2 re-seeds.
 // GLU: group s = (m-block s/2, channel half s%1): 20 sigmoid-gate ops + 2 packs (+ swaps and the

@@ -370,7 +370,10 @@ struct ModelT : public cfm_model {
         hipEvent_t pb_;
         prof_begin(PC_ATTN, st, &pb_);
         if constexpr (sizeof(T) == 2) {
-          if (masked && use_ring_attention && dk == 64)
+          if (masked && use_ring_attention && dk == 64 && tune.attn_q32)
+            r = chunk_attention_masked_q32(w.q, w.kv, kv_rows, w.P + (size_t)l * d, p_rows, p_ld, Lw.pu, Lw.pv, attd,
+                                           natt, H, C, hh[PH_L] + C + hh[PH_R], w.ao, st);
+          if (r == -1 && masked && use_ring_attention && dk == 64)
             r = chunk_attention_masked_bf16(w.q, w.kv, kv_rows, w.P + (size_t)l * d, p_rows, Lw.pu, Lw.pv,
                                             attd, natt, H, C, hh[PH_L] + C + hh[PH_R], w.ao, st, attn_diag, p_ld,
                                             tune.attn_reuse);
@@ -699,7 +702,7 @@ cfm_status cfm_model_set_option(cfm_model* m, const char* key, int64_t value) {
         {"col_group", &m->tune.col_group}, {"attn_reuse", &m->tune.attn_reuse}, {"conv_dot2", &m->tune.conv_dot2},
         {"conv_dma", &m->tune.conv_dma},   {"dw2_seg", &m->tune.dw2_seg},   {"nt_sites", &m->tune.nt_sites},
         {"fe_fuse_dw2", &m->tune.fe_fuse_dw2},
-        {"attn128_var", &m->tune.attn128_var}};
+        {"attn128_var", &m->tune.attn128_var}, {"attn_q32", &m->tune.attn_q32}};
     for (auto& k : knobs)
       if (!std::strcmp(key, k.first)) { *k.second = (int)value; return CFM_OK; }
   }

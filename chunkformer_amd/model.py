@@ -35,7 +35,7 @@ import torch
 
 from .config import EncoderConfig
 from .encoder import ChunkFormerEncoder
-from .streaming import EndlessGraphRunner, EndlessPipeline
+from .streaming import EndlessGraphPipeline, EndlessGraphRunner, EndlessPipeline
 from .transducer import RNNTConfig, RNNTGreedy
 
 Features = Union[torch.Tensor, np.ndarray, str]
@@ -306,11 +306,12 @@ class ChunkFormerModel:
         identical to the reference's argmax over the concatenation).
         Returns text (with char_dict) or ids [1, T', 1] like the reference; with
         `return_encoder_out` also the concatenated encoder output [1, T', d] (fp32).
-        `cuda_graph`: the full-size middle segments replay one captured HIP graph (front-end,
-        blocks with the caches carried, after_norm, CTC argmax); see streaming.py.  `pipeline`
-        (default: on from 3 segments up): `pipeline_depth` segments in flight on as many streams
-        instead, segment k + 1's layer l waiting only for segment k's layer l (EndlessPipeline).  Every mode gives
-        the same result as the eager loop (same kernels, same plans)."""
+        `pipeline` (default: on from 3 segments up): `pipeline_depth` segments in flight on as many
+        streams, segment k + 1's layer l waiting only for segment k's layer l; with `cuda_graph` the
+        pipeline's steady-state ticks replay captured HIP graphs (EndlessGraphPipeline), without it they
+        are launched eagerly (EndlessPipeline).  pipeline=False: one segment at a time, the full-size
+        middle segments replaying one captured graph (EndlessGraphRunner) when `cuda_graph`.  Every
+        mode gives the same result as the eager loop (same kernels, same plans); see streaming.py."""
         C = chunk_size if chunk_size is not None else 64
         L = left_context_size if left_context_size is not None else 128
         R = right_context_size if right_context_size is not None else 128
@@ -327,8 +328,11 @@ class ChunkFormerModel:
         key = (C, L, R, trunc, seg_len, want_eo, bool(cuda_graph), bool(pipeline), int(pipeline_depth))
         runner = self._endless_runners.get(key)
         if runner is None:   # graphs are captured once per segment geometry and reused across calls
-            runner = (EndlessPipeline(enc, C, L, R, trunc, want_eo, pipeline_depth) if pipeline else
-                      EndlessGraphRunner(enc, C, L, R, trunc, seg_len, want_eo, use_graph=cuda_graph))
+            if pipeline:
+                runner = (EndlessGraphPipeline(enc, C, L, R, trunc, seg_len, want_eo, pipeline_depth) if cuda_graph
+                          else EndlessPipeline(enc, C, L, R, trunc, want_eo, pipeline_depth))
+            else:
+                runner = EndlessGraphRunner(enc, C, L, R, trunc, seg_len, want_eo, use_graph=cuda_graph)
             self._endless_runners = {key: runner}
         if pipeline:
             tids, teos, cur = runner.run(xs_dev, segs)

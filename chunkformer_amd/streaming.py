@@ -245,3 +245,166 @@ class EndlessPipeline:
             caller.wait_stream(s)
         self._keep = keep
         return ids_out, eo_out, len(segs) % 2
+
+
+class EndlessGraphPipeline:
+    """endless_decode's segments as a software pipeline of `depth` stage slots whose steady state is
+    replayed from HIP graphs (BASELINE configs[3]: context caches carried across graph-captured steps,
+    with several segments in flight).
+
+    The encoder stages (-1 = front-end, 0..nb-1 = layers) are cut into `depth` consecutive slots.  Tick
+    t runs slot s of segment t - s for every s: those units are independent (segment k's slot s needs
+    segment k - 1's slot s, i.e. the layer caches it carries, and its own slot s - 1, both from tick
+    t - 1), so within a tick they run on `depth` streams at once, and tick t + 1 starts after tick t.
+    A tick whose units all belong to middle segments (the same length and, once offset >= max(L, 7),
+    the same plan: streaming.py's module note) is one HIP graph replay; the graph only depends on the
+    tick's phase (segment k uses workspace / output slot k % depth and cache pair k % 2), so
+    lcm(depth, 2) graphs are captured once per segment geometry.  The first segments (offset 0), the
+    ragged last one and the pipeline's fill / drain ticks run the same stage calls eagerly.  Every unit
+    is a cfm_encode_masked_stages call with that segment's plan, caches and workspace, so the result is
+    bit-identical to the one-call-per-segment loop."""
+
+    def __init__(self, encoder, C: int, L: int, R: int, trunc: int, seg_len: int, want_out: bool, depth: int = 3):
+        if depth < 1:
+            raise ValueError(f"pipeline depth {depth} < 1")
+        self.enc = encoder
+        cfg = encoder.cfg
+        self.C, self.L, self.R, self.trunc, self.seg_len = C, L, R, trunc, seg_len
+        self.want_out = want_out
+        dev = encoder.device
+        self.dev = dev
+        nb, H, dk, d = cfg.num_blocks, cfg.n_heads, cfg.head_dim, cfg.d_model
+        stages = list(range(-1, nb))
+        depth = min(depth, len(stages))
+        self.depth = depth
+        per, extra = divmod(len(stages), depth)
+        self.slots, i = [], 0
+        for s in range(depth):   # consecutive stage ranges [lo, hi], the longer ones first
+            n = per + (1 if s < extra else 0)
+            self.slots.append((stages[i], stages[i + n - 1]))
+            i += n
+        self.att = [torch.zeros(nb, L, H, 2 * dk, device=dev) for _ in range(2)]
+        self.cnn = [torch.zeros(nb, d, cfg.conv_lorder, device=dev) for _ in range(2)]
+        self.streams = [torch.cuda.Stream(dev) for _ in range(depth)]
+        self.ws: List[Optional[torch.Tensor]] = [None] * depth
+        self.out: List[Optional[torch.Tensor]] = [None] * depth
+        self.ids: List[Optional[torch.Tensor]] = [None] * depth
+        self.ctc_ws: List[Optional[torch.Tensor]] = [None] * depth
+        self.period = depth if depth % 2 == 0 else 2 * depth
+        self.graphs: dict = {}
+        self.g_plan = None
+        self.g_feats = torch.zeros(max(seg_len, 1), cfg.input_dim, device=dev)
+        self.vocab = cfg.vocab
+        self.replayed = 0   # ticks replayed from graphs in the last run (tests / bench)
+
+    def _buf(self, lst, i, n, dtype) -> None:
+        t = lst[i]
+        if t is None or t.numel() < n:
+            lst[i] = torch.empty(n, dtype=dtype, device=self.dev)
+            self.graphs.clear()   # captured graphs hold the old buffer's address
+
+    def _unit(self, seg: dict, slot: int, st) -> None:
+        """Slot `slot`'s stage calls for one segment on stream `st` (+ the CTC head after the last)."""
+        enc = self.enc
+        k, p = seg["k"], seg["k"] % self.depth
+        c = k % 2
+        lo, hi = self.slots[slot]
+        _lib.check(_lib.cfm_encode_masked_stages(
+            enc._h, seg["feats"].data_ptr(), seg["plan"].data_ptr(), seg["plan_dev"].data_ptr(),
+            self.att[c].data_ptr(), self.cnn[c].data_ptr(), int(self.trunc), self.att[1 - c].data_ptr(),
+            self.cnn[1 - c].data_ptr(), self.out[p].data_ptr(), self.ws[p].data_ptr(), seg["wsb"], lo, hi,
+            st.cuda_stream))
+        if slot == self.depth - 1 and self.vocab > 0 and seg["rows"] > 0:
+            with torch.cuda.stream(st):
+                enc._ctc_raw(self.out[p], seg["rows"], None, self.ids[p], self.ctc_ws[p])
+
+    def _tick(self, units, graph_key=None) -> None:
+        """One tick: its units on `depth` streams (fork from / join into the caller's stream), either
+        eagerly or by replaying (capturing first) the graph of `graph_key`."""
+        caller = torch.cuda.current_stream(self.dev)
+        if graph_key is not None:
+            g = self.graphs.get(graph_key)
+            if g is None:
+                g = torch.cuda.CUDAGraph()
+                cap = self.streams[0]
+                cap.wait_stream(caller)
+                with torch.cuda.graph(g, stream=cap):
+                    self._fork_join(units, cap)
+                self.graphs[graph_key] = g
+            g.replay()
+            self.replayed += 1
+            return
+        self._fork_join(units, caller)
+
+    def _fork_join(self, units, base) -> None:
+        for i, (seg, slot) in enumerate(units):
+            st = self.streams[i]
+            if st is not base:
+                st.wait_stream(base)
+            self._unit(seg, slot, st)
+        for i in range(len(units)):
+            if self.streams[i] is not base:
+                base.wait_stream(self.streams[i])
+
+    def run(self, xs_dev: torch.Tensor, segs):
+        """Returns (per-segment CTC ids of the kept rows, per-segment kept encoder rows or None, index of
+        the cache pair holding the caches after the last segment), ready on the caller's stream."""
+        enc, C, L, R, D = self.enc, self.C, self.L, self.R, self.depth
+        d = enc.cfg.d_model
+        self.att[0].zero_()
+        self.cnn[0].zero_()
+        self.replayed = 0
+        caller = torch.cuda.current_stream(self.dev)
+        n = len(segs)
+        if n == 0:
+            return [], [], 0
+        info, offset = [], 0
+        for k, (start, stop, keep_trunc, _) in enumerate(segs):
+            n_frames = stop - start
+            plan, n_chunks, out_lens = _lib.plan_masked([n_frames], [offset], C, L, R)
+            N = n_chunks[0]
+            kept = min(out_lens[0], self.trunc) if keep_trunc else out_lens[0]
+            info.append({"k": k, "x": xs_dev[start:stop], "plan": plan, "N": N, "n": out_lens[0], "rows": kept,
+                         "wsb": int(_lib.cfm_workspace_bytes_masked(enc._h, N, C, L, R)), "len": n_frames})
+            offset += kept
+        # the graph plan: the first middle segment whose plan no longer depends on the offset
+        if self.g_plan is None:
+            for s in info:
+                if s["len"] == self.seg_len and sum(s2["rows"] for s2 in info[: s["k"]]) >= max(L, 7):
+                    self.g_plan = s["plan"]
+                    self.g_plan_dev = enc._upload(s["plan"])
+                    break
+        for s in info:
+            s["graph"] = self.g_plan is not None and s["len"] == self.seg_len and torch.equal(s["plan"], self.g_plan)
+            if s["graph"]:
+                s["plan"], s["plan_dev"], s["feats"] = self.g_plan, self.g_plan_dev, self.g_feats
+            else:
+                s["plan_dev"] = enc._upload(s["plan"])
+                s["feats"] = s["x"].contiguous()
+        max_rows = max([s["rows"] for s in info] + [1])
+        ctc_b = enc.ctc_ws_bytes(max_rows, False) if self.vocab > 0 else 0   # 0 on the fused argmax head
+        for p in range(D):   # slot buffers sized for the largest segment
+            self._buf(self.ws, p, max(s["wsb"] for s in info), torch.uint8)
+            self._buf(self.out, p, max(s["N"] for s in info) * C * d, torch.float32)
+            self._buf(self.ids, p, max_rows, torch.int32)
+            if ctc_b > 0:
+                self._buf(self.ctc_ws, p, ctc_b, torch.uint8)
+        ids_out: List[Optional[torch.Tensor]] = [None] * n
+        eo_out: List[Optional[torch.Tensor]] = [None] * n
+        for t in range(n + D - 1):
+            units = [(info[t - s], s) for s in range(D) if 0 <= t - s < n]
+            full = len(units) == D and all(u[0]["graph"] for u in units)
+            if units and units[0][1] == 0 and units[0][0]["graph"]:
+                self.g_feats[: units[0][0]["len"]].copy_(units[0][0]["x"])   # the graph's input rows
+            self._tick(units, (t % self.period) if full else None)
+            done = t - (D - 1)   # the segment whose last slot ran in this tick
+            if 0 <= done < n:
+                s = info[done]
+                p = done % D
+                eo = self.out[p][: s["N"] * C * d].view(s["N"] * C, d)[: s["rows"]]
+                if self.vocab > 0 and s["rows"] > 0:
+                    ids_out[done] = self.ids[p][: s["rows"]].clone()
+                if self.want_out:
+                    eo_out[done] = eo.clone()
+        self._keep = info
+        return ids_out, eo_out, n % 2

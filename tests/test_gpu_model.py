@@ -95,12 +95,19 @@ def test_endless_graph_replay_equals_eager(small, dtype):
     assert eo_g.shape == eo_e.shape
     assert torch.equal(eo_g, eo_e)
     assert torch.equal(ids_g, ids_e)
-    # two segments in flight on two streams (streaming.py EndlessPipeline): same rows, ids and caches
-    ids_p, eo_p = m.endless_decode(x, C, L, R, total_batch_duration=tbd, return_encoder_out=True, pipeline=True)
-    assert torch.equal(eo_p, eo_e)
-    assert torch.equal(ids_p, ids_e)
-    for a, b in zip(m.last_endless_caches, ca_e):
-        assert torch.equal(a, b)
+    # segments in flight on several streams, eagerly (EndlessPipeline) and with the pipeline's steady
+    # ticks replayed from HIP graphs (EndlessGraphPipeline, twice: captured, then reused), at depths
+    # 2, 3 (default) and 4: same rows, ids and caches
+    for graph, depth in ((False, 3), (True, 3), (True, 3), (True, 2), (True, 4)):
+        ids_p, eo_p = m.endless_decode(x, C, L, R, total_batch_duration=tbd, return_encoder_out=True, pipeline=True,
+                                       cuda_graph=graph, pipeline_depth=depth)
+        assert torch.equal(eo_p, eo_e), (graph, depth)
+        assert torch.equal(ids_p, ids_e), (graph, depth)
+        for a, b in zip(m.last_endless_caches, ca_e):
+            assert torch.equal(a, b), (graph, depth)
+        if graph:
+            runner = next(iter(m._endless_runners.values()))
+            assert runner.replayed > 0, depth   # some ticks did replay graphs
 
 
 @pytest.mark.parametrize("dtype", ["fp32", "bf16"])
