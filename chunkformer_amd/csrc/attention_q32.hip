@@ -42,6 +42,17 @@ CFM_DEV unsigned q32_pk(float a, float b) {
   return __builtin_bit_cast(unsigned, (b2){(bf16)a, (bf16)b});
 }
 // D = A (AGPR) x B + C, 16x16x32 bf16: the P fragments live in the AGPR half of the register file
+// a bf16 fragment moved into the AGPR half of the register file (MFMA A/B operands may be AGPRs):
+// keeps the query operands out of the VGPRs the scores and the P.V accumulators need
+CFM_DEV bf16x8 to_agpr(const bf16x8& v) {
+  const u32x4 x = __builtin_bit_cast(u32x4, v);
+  unsigned a0, a1, a2, a3;
+  asm("v_accvgpr_write_b32 %0, %1" : "=a"(a0) : "v"(x[0]));
+  asm("v_accvgpr_write_b32 %0, %1" : "=a"(a1) : "v"(x[1]));
+  asm("v_accvgpr_write_b32 %0, %1" : "=a"(a2) : "v"(x[2]));
+  asm("v_accvgpr_write_b32 %0, %1" : "=a"(a3) : "v"(x[3]));
+  return __builtin_bit_cast(bf16x8, (u32x4){a0, a1, a2, a3});
+}
 // (not volatile: a pure function of its operands, so hipcc may schedule it like any other instruction)
 CFM_DEV f32x4 mfma_pa(const bf16x8& a, const bf16x8& b, f32x4 c) {
   asm("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(c) : "a"(a), "v"(b));
@@ -58,12 +69,15 @@ CFM_DEV f32x4 mfma_pa0(const bf16x8& a, const bf16x8& b) {   // C = 0 (inline co
 constexpr float Q32_DEFER = 5.545177444479562f;   // 8 / log2(e)
 }  // namespace
 
-// NH = W / 32 key halves per window (2..10; W = L + 64 + R)
-template <int NH>
+// NH = W / 32 key halves per window (2..10; W = L + 64 + R); PIPE: 0 = one half after the other,
+// 1 = software-pipelined by one half
+template <int NH, int PIPE>
 __global__ __launch_bounds__(256, 1) void chunk_attention_q32_kernel(
     const bf16* __restrict__ Q, const bf16* __restrict__ KV, int kv_rows, const bf16* __restrict__ P, int p_rows,
     int p_ld, const float* __restrict__ pos_u, const float* __restrict__ pos_v, const int32_t* __restrict__ desc,
-    int n_chunks, int H, int nch, bf16* __restrict__ out) {
+    int n_chunks, int H, int nch, bf16* __restrict__ out, int diag) {
+  // diag (timing only, model option "attn_diag" >= 64): bit 0 no band MFMAs / writes, bit 1 no exp +
+  // P.V, bit 2 no score MFMAs, bit 3 no LDS-DMA of the next pair (stale rows)
   constexpr int W = 32 * NH;
   constexpr int RING = W + 192;          // ring rows: a pair's windows (W + 64) + the next pair's 128 new rows
   constexpr int NPT = 2 * NH + 2;        // P tiles per wave
@@ -171,7 +185,7 @@ __global__ __launch_bounds__(256, 1) void chunk_attention_q32_kernel(
     const bool act = c < c1;
     const int key_lo = klo_n, key_hi = khi_n;
     // ---- the next pair's 128 new rows by LDS-DMA (they replace the rows the previous pair dropped)
-    if (cp + 2 < c1) {
+    if (cp + 2 < c1 && !(diag & 8)) {
       const int x0 = (cp - c0) * 64 + W + 64;
       dma_rows(x0, x0 + (cp + 3 < c1 ? 128 : 64));
     }
@@ -207,6 +221,13 @@ __global__ __launch_bounds__(256, 1) void chunk_attention_q32_kernel(
             qv[q][s][e] = (bf16)fmaf(qf, 0.125f, (e < 4 ? v0[e] : v1[e - 4]) * 0.125f);
           }
       }
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          qu[q][s] = to_agpr(qu[q][s]);
+          qv[q][s] = to_agpr(qv[q][s]);
+        }
       // interior chunks see the whole window: the masking code exists only in the edge-chunk copy
       const bool need_mask = __builtin_amdgcn_readfirstlane(key_lo != 0 || key_hi != W) != 0;
       auto body = [&](auto MASKc) {
@@ -217,13 +238,16 @@ __global__ __launch_bounds__(256, 1) void chunk_attention_q32_kernel(
       f32x4 bnd[2][3];
       auto band = [&](auto HFc, bool carry) {
         constexpr int hf = decltype(HFc)::value;
+        if (diag & 1) return;
 #pragma unroll
         for (int q = 0; q < 2; ++q)
 #pragma unroll
           for (int pt = 0; pt < 3; ++pt) {
             if (pt == 0 && carry) { bnd[q][0] = bnd[q][2]; continue; }
             const int n = 2 * hf + pt + (q == 0 ? 1 : 0);
-            bnd[q][pt] = mfma_pa(pf[n][1], qv[q][1], mfma_pa0(pf[n][0], qv[q][0]));
+            bnd[q][pt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                pf[n][1], qv[q][1], __builtin_amdgcn_mfma_f32_16x16x32_bf16(pf[n][0], qv[q][0], (f32x4){0.f, 0.f, 0.f, 0.f}, 0, 0, 0),
+                0, 0, 0);
           }
         // skewed write (pitch 57; read back at pitch 56 by scores())
 #pragma unroll
@@ -262,40 +286,32 @@ __global__ __launch_bounds__(256, 1) void chunk_attention_q32_kernel(
         return o;
       };
       band(std::integral_constant<int, 0>{}, false);
-      HalfOps cur = load_ops(0);
-      sfor<0, NH>([&](auto HFc) {
-        constexpr int hf = decltype(HFc)::value;
-        const int kb = ring32(32 * hf);   // ring row of the half's first key
-        // V^T fragments of this half's P.V (two transposed reads per 16-dim tile: rows kb + 4g + ..,
-        // kb + 16 + 4g + ..), issued before the scores so they land meanwhile
-        bf16x8 va[4];
-        {
-          const char* vb = vr + kb * 128;
+      // V^T fragments of half hf's P.V: two transposed reads per 16-dim tile (rows kb + 4g + ..,
+      // kb + 16 + 4g + ..)
+      auto load_va = [&](int hf, bf16x8 (&va)[4]) {
+        const char* vb = vr + ring32(32 * hf) * 128;
 #pragma unroll
-          for (int dt = 0; dt < 4; ++dt) {
-            const s16x4_q lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                (__attribute__((address_space(3))) s16x4_q*)(vb + v_lane[dt]));
-            const s16x4_q hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                (__attribute__((address_space(3))) s16x4_q*)(vb + v_lane[dt] + 16 * 128));
-            const bf16x4_q l4 = __builtin_bit_cast(bf16x4_q, lo), h4 = __builtin_bit_cast(bf16x4_q, hi);
-            va[dt] = (bf16x8){l4[0], l4[1], l4[2], l4[3], h4[0], h4[1], h4[2], h4[3]};
-          }
+        for (int dt = 0; dt < 4; ++dt) {
+          const s16x4_q lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (__attribute__((address_space(3))) s16x4_q*)(vb + v_lane[dt]));
+          const s16x4_q hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (__attribute__((address_space(3))) s16x4_q*)(vb + v_lane[dt] + 16 * 128));
+          const bf16x4_q l4 = __builtin_bit_cast(bf16x4_q, lo), h4 = __builtin_bit_cast(bf16x4_q, hi);
+          va[dt] = (bf16x8){l4[0], l4[1], l4[2], l4[3], h4[0], h4[1], h4[2], h4[3]};
         }
-        // ---- scores S^T = K . (q+u)^T + skewed band (keys 32hf + 16 st2 + 4g + rr, query i0 + 16q + fr)
-        f32x4 S[2][2];
+      };
+      // scores S^T = K . (q+u)^T + skewed band (keys 32hf + 16 st2 + 4g + rr, query i0 + 16q + fr)
+      auto scores = [&](const HalfOps& o, f32x4 (&S)[2][2]) {
 #pragma unroll
         for (int q = 0; q < 2; ++q)
 #pragma unroll
           for (int st2 = 0; st2 < 2; ++st2) {
-            f32x4 a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cur.kf[st2][0], qu[q][0], cur.bc[q][st2], 0, 0, 0);
-            S[st2][q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cur.kf[st2][1], qu[q][1], a, 0, 0, 0);
+            if (diag & 4) { S[st2][q] = o.bc[q][st2] + (float)o.kf[st2][0][0]; continue; }
+            f32x4 a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(o.kf[st2][0], qu[q][0], o.bc[q][st2], 0, 0, 0);
+            S[st2][q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(o.kf[st2][1], qu[q][1], a, 0, 0, 0);
           }
-        // the next half's band, then its operands (its scratch writes follow this half's band reads
-        // and precede the next reads in program order: the LDS serves one wave in order)
-        if constexpr (hf + 1 < NH) {
-          band(std::integral_constant<int, hf + 1>{}, true);
-          cur = load_ops(hf + 1);
-        }
+      };
+      auto mask = [&](int hf, f32x4 (&S)[2][2]) {
         if constexpr (MASK) {
 #pragma unroll
           for (int q = 0; q < 2; ++q)
@@ -307,8 +323,10 @@ __global__ __launch_bounds__(256, 1) void chunk_attention_q32_kernel(
                 S[st2][q][rr] = (j < key_lo || j >= key_hi) ? -INFINITY : S[st2][q][rr];
               }
         }
-        // ---- running max over the query's 4 lanes (permlane swaps, no LDS), rescale on growth
-        float ml[2];
+      };
+      // running max over the query's 4 lanes (permlane swaps, no LDS); O rescaled when it is raised;
+      // returns m * log2(e) for the exps
+      auto softmax_max = [&](bool first, const f32x4 (&S)[2][2], float (&ml)[2]) {
         bool grew = false;
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
@@ -323,7 +341,7 @@ __global__ __launch_bounds__(256, 1) void chunk_attention_q32_kernel(
           grew |= up;
           ml[q] = up ? x : m[q];
         }
-        if (hf > 0 && __builtin_amdgcn_ballot_w64(grew)) {
+        if (!first && __builtin_amdgcn_ballot_w64(grew)) {
 #pragma unroll
           for (int q = 0; q < 2; ++q) {
             // pass-through terms at the old maximum, rescaled (0 while no key of the query was unmasked)
@@ -338,8 +356,9 @@ __global__ __launch_bounds__(256, 1) void chunk_attention_q32_kernel(
           m[q] = ml[q];
           ml[q] = (ml[q] == -INFINITY ? 0.f : ml[q]) * 1.4426950408889634f;   // fully masked so far: p = 0
         }
-        // ---- P.V: probabilities (bf16, keys in the score registers' order) as B fragments
-        bf16x8 pb[2];
+      };
+      // probabilities (bf16, keys in the score registers' order) as B fragments
+      auto probs = [&](const f32x4 (&S)[2][2], const float (&ml)[2], bf16x8 (&pb)[2]) {
 #pragma unroll
         for (int q = 0; q < 2; ++q)
 #pragma unroll
@@ -347,13 +366,73 @@ __global__ __launch_bounds__(256, 1) void chunk_attention_q32_kernel(
 #pragma unroll
             for (int rr = 0; rr < 4; ++rr)
               pb[q][4 * st2 + rr] = (bf16)__builtin_amdgcn_exp2f(fmaf(S[st2][q][rr], 1.4426950408889634f, -ml[q]));
+      };
+      auto pv = [&](const bf16x8 (&va)[4], const bf16x8 (&pb)[2]) {
 #pragma unroll
         for (int dt = 0; dt < 4; ++dt)
 #pragma unroll
           for (int q = 0; q < 2; ++q) O[q][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va[dt], pb[q], O[q][dt], 0, 0, 0);
 #pragma unroll
         for (int q = 0; q < 2; ++q) Ol[q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pb[q], Ol[q], 0, 0, 0);
-      });
+      };
+
+      HalfOps cur = load_ops(0);
+      if constexpr (PIPE == 0) {
+        // one half after the other: V^T reads, scores, the next half's band and operands, softmax, P.V
+        sfor<0, NH>([&](auto HFc) {
+          constexpr int hf = decltype(HFc)::value;
+          bf16x8 va[4];
+          load_va(hf, va);
+          f32x4 S[2][2];
+          scores(cur, S);
+          // the next half's band, then its operands (its scratch writes follow this half's band reads
+          // and precede the next reads in program order: the LDS serves one wave in order)
+          if constexpr (hf + 1 < NH) {
+            band(std::integral_constant<int, hf + 1>{}, true);
+            cur = load_ops(hf + 1);
+          }
+          mask(hf, S);
+          if (diag & 2) {   // timing only: keep the scores alive, skip the softmax and P.V
+#pragma unroll
+            for (int q = 0; q < 2; ++q) O[q][0] += S[0][q] + S[1][q] + (float)va[0][0];
+            return;
+          }
+          float ml[2];
+          softmax_max(hf == 0, S, ml);
+          bf16x8 pb[2];
+          probs(S, ml, pb);
+          pv(va, pb);
+        });
+      } else {
+        // software-pipelined by one half: iteration hf runs half hf + 1's score MFMAs beside half hf's
+        // max, then half hf's exps beside half hf + 2's band MFMAs and half hf's P.V
+        f32x4 Sn[2][2];
+        scores(cur, Sn);
+        if constexpr (NH > 1) {
+          band(std::integral_constant<int, 1>{}, true);
+          cur = load_ops(1);
+        }
+        bf16x8 va[4];
+        load_va(0, va);
+        sfor<0, NH>([&](auto HFc) {
+          constexpr int hf = decltype(HFc)::value;
+          f32x4 S[2][2];
+#pragma unroll
+          for (int q = 0; q < 2; ++q) { S[0][q] = Sn[0][q]; S[1][q] = Sn[1][q]; }
+          if constexpr (hf + 1 < NH) scores(cur, Sn);
+          mask(hf, S);
+          float ml[2];
+          softmax_max(hf == 0, S, ml);
+          bf16x8 pb[2];
+          if (!(diag & 2)) probs(S, ml, pb);
+          if constexpr (hf + 2 < NH) {
+            band(std::integral_constant<int, hf + 2>{}, true);
+            cur = load_ops(hf + 2);
+          }
+          if (!(diag & 2)) pv(va, pb);
+          if constexpr (hf + 1 < NH) load_va(hf + 1, va);
+        });
+      }
       // ---- normalise and store: lane (query fr, g) holds dims 16 dt + 4g .. +3; permlane16 swaps give
       // each lane 8 contiguous dims, so a query row leaves as 16-B pieces
 #pragma unroll
@@ -388,7 +467,7 @@ bool attention_q32_eligible(int C, int W, int p_rows) {
 
 int chunk_attention_masked_q32(const bf16* q, const bf16* kv, int kv_rows, const bf16* P, int p_rows, int p_ld,
                                const float* pos_u, const float* pos_v, const int32_t* desc, int n_chunks, int H, int C,
-                               int W, bf16* out, hipStream_t st) {
+                               int W, bf16* out, hipStream_t st, int diag, int pipe) {
   if (!attention_q32_eligible(C, W, p_rows) || n_chunks <= 0) return -1;
   if (p_ld <= 0) p_ld = H * 64;
   // one block per CU (LDS-bound), a run of consecutive chunks of one head (even: two per iteration)
@@ -396,8 +475,12 @@ int chunk_attention_masked_q32(const bf16* q, const bf16* kv, int kv_rows, const
   nch = max(4, (nch + 1) & ~1);
   const dim3 grid((n_chunks + nch - 1) / nch, H);
 #define Q32(NH_)                                                                                                     \
-  hipLaunchKernelGGL((chunk_attention_q32_kernel<NH_>), grid, dim3(256), 0, st, q, kv, kv_rows, P, p_rows, p_ld,    \
-                     pos_u, pos_v, desc, n_chunks, H, nch, out)
+  if (pipe)                                                                                                          \
+    hipLaunchKernelGGL((chunk_attention_q32_kernel<NH_, 1>), grid, dim3(256), 0, st, q, kv, kv_rows, P, p_rows,     \
+                       p_ld, pos_u, pos_v, desc, n_chunks, H, nch, out, diag);                                       \
+  else                                                                                                               \
+    hipLaunchKernelGGL((chunk_attention_q32_kernel<NH_, 0>), grid, dim3(256), 0, st, q, kv, kv_rows, P, p_rows,     \
+                       p_ld, pos_u, pos_v, desc, n_chunks, H, nch, out, diag)
   switch (W / 32) {
     case 2: Q32(2); break;
     case 3: Q32(3); break;

@@ -247,6 +247,28 @@ class EndlessPipeline:
         return ids_out, eo_out, len(segs) % 2
 
 
+def stage_slots(num_blocks: int, depth: int):
+    """The encoder stages (-1 = front-end, 0 .. num_blocks-1 = layers) cut into `depth` consecutive
+    slots [lo, hi] (the longer ones first): EndlessGraphPipeline's stage slots."""
+    stages = list(range(-1, num_blocks))
+    depth = max(1, min(depth, len(stages)))
+    per, extra = divmod(len(stages), depth)
+    slots, i = [], 0
+    for s in range(depth):
+        n = per + (1 if s < extra else 0)
+        slots.append((stages[i], stages[i + n - 1]))
+        i += n
+    return slots
+
+
+def pipeline_ticks(n_segments: int, depth: int):
+    """Tick t of the software pipeline runs slot s of segment t - s for every valid s: a list of
+    [(segment, slot), ...] per tick.  Every segment runs its slots 0 .. depth-1 in consecutive ticks,
+    and segment k's slot s runs one tick after segment k - 1's (its layer caches) and one tick after
+    its own slot s - 1."""
+    return [[(t - s, s) for s in range(depth) if 0 <= t - s < n_segments] for t in range(n_segments + depth - 1)]
+
+
 class EndlessGraphPipeline:
     """endless_decode's segments as a software pipeline of `depth` stage slots whose steady state is
     replayed from HIP graphs (BASELINE configs[3]: context caches carried across graph-captured steps,
@@ -274,15 +296,9 @@ class EndlessGraphPipeline:
         dev = encoder.device
         self.dev = dev
         nb, H, dk, d = cfg.num_blocks, cfg.n_heads, cfg.head_dim, cfg.d_model
-        stages = list(range(-1, nb))
-        depth = min(depth, len(stages))
+        self.slots = stage_slots(nb, depth)
+        depth = len(self.slots)
         self.depth = depth
-        per, extra = divmod(len(stages), depth)
-        self.slots, i = [], 0
-        for s in range(depth):   # consecutive stage ranges [lo, hi], the longer ones first
-            n = per + (1 if s < extra else 0)
-            self.slots.append((stages[i], stages[i + n - 1]))
-            i += n
         self.att = [torch.zeros(nb, L, H, 2 * dk, device=dev) for _ in range(2)]
         self.cnn = [torch.zeros(nb, d, cfg.conv_lorder, device=dev) for _ in range(2)]
         self.streams = [torch.cuda.Stream(dev) for _ in range(depth)]
@@ -391,8 +407,8 @@ class EndlessGraphPipeline:
                 self._buf(self.ctc_ws, p, ctc_b, torch.uint8)
         ids_out: List[Optional[torch.Tensor]] = [None] * n
         eo_out: List[Optional[torch.Tensor]] = [None] * n
-        for t in range(n + D - 1):
-            units = [(info[t - s], s) for s in range(D) if 0 <= t - s < n]
+        for t, tick in enumerate(pipeline_ticks(n, D)):
+            units = [(info[k], s) for k, s in tick]
             full = len(units) == D and all(u[0]["graph"] for u in units)
             if units and units[0][1] == 0 and units[0][0]["graph"]:
                 self.g_feats[: units[0][0]["len"]].copy_(units[0][0]["x"])   # the graph's input rows

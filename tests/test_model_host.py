@@ -124,3 +124,30 @@ def test_cmvn_loaders_agree(tmp_path):
     a, b = load_json_cmvn(str(tmp_path / "j")), load_kaldi_cmvn(str(tmp_path / "k"))
     np.testing.assert_allclose(a[0], b[0], rtol=1e-12)
     np.testing.assert_allclose(a[1], b[1], rtol=1e-12)
+
+
+def test_endless_pipeline_schedule():
+    """EndlessGraphPipeline's software-pipeline schedule (host logic): the stage slots cover -1 ..
+    nb-1 once, in order; every segment runs every slot exactly once, slot s one tick after slot s-1,
+    and segment k's slot s one tick after segment k-1's (its carried layer caches)."""
+    from chunkformer_amd.streaming import pipeline_ticks, stage_slots
+    for nb in (2, 12):
+        for depth in (1, 2, 3, 4, 5, 13, 20):
+            slots = stage_slots(nb, depth)
+            flat = [st for lo, hi in slots for st in range(lo, hi + 1)]
+            assert flat == list(range(-1, nb))
+            assert len(slots) == min(depth, nb + 1)
+            for n in (1, 2, 3, 7):
+                ticks = pipeline_ticks(n, len(slots))
+                when = {}
+                for t, tick in enumerate(ticks):
+                    assert len({k for k, _ in tick}) == len(tick)   # a segment at most once per tick
+                    for k, s in tick:
+                        assert (k, s) not in when
+                        when[(k, s)] = t
+                assert len(when) == n * len(slots)
+                for (k, s), t in when.items():
+                    if s > 0:
+                        assert when[(k, s - 1)] == t - 1
+                    if k > 0:
+                        assert when[(k - 1, s)] == t - 1
