@@ -101,6 +101,9 @@ cfm_rnnt_create = _sig("cfm_rnnt_create", I32, ctypes.POINTER(CfmRnntConfig), ct
 cfm_rnnt_destroy = _sig("cfm_rnnt_destroy", None, P)
 cfm_rnnt_workspace_bytes = _sig("cfm_rnnt_workspace_bytes", SZ, P, I32)
 cfm_rnnt_greedy = _sig("cfm_rnnt_greedy", I32, P, P, I32, P, P, I32, I32, P, P, SZ, P)
+cfm_rnnt_set_option = _sig("cfm_rnnt_set_option", I32, P, ctypes.c_char_p, I64)
+cfm_rnnt_grid_blocks = _sig("cfm_rnnt_grid_blocks", I32, P, I32)
+cfm_rnnt_error = _sig("cfm_rnnt_error", I32, P, P, I32)
 # include/cfm_ops.h
 cfm_op_gemm = _sig("cfm_op_gemm", I32, I32, I32, I32, P, I32, P, I32, I32, I32, I32, P, ctypes.c_float, P, I32, I32, P,
                    I32, P, I32, P, I32, P)
@@ -112,7 +115,8 @@ EXPORTED = ["cfm_version", "cfm_last_error", "cfm_model_create", "cfm_model_dest
             "cfm_ctc_logprobs", "cfm_ctc_ids_workspace_bytes", "cfm_ctc_ids", "cfm_ctc_collapse",
             "cfm_plan_stream", "cfm_workspace_bytes_stream", "cfm_encode_stream",
             "cfm_fbank_create", "cfm_fbank_destroy", "cfm_fbank_num_frames", "cfm_fbank_compute",
-            "cfm_rnnt_create", "cfm_rnnt_destroy", "cfm_rnnt_workspace_bytes", "cfm_rnnt_greedy"]
+            "cfm_rnnt_create", "cfm_rnnt_destroy", "cfm_rnnt_workspace_bytes", "cfm_rnnt_greedy",
+            "cfm_rnnt_set_option", "cfm_rnnt_grid_blocks", "cfm_rnnt_error"]
 
 
 def profile_read(h):

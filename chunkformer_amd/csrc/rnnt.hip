@@ -237,6 +237,278 @@ __global__ __launch_bounds__(RNNT_NT) void rnnt_greedy_kernel(RnntDev w, const f
   }
 }
 
+// ---- one long utterance over many CUs (B small: endless_decode's B = 1) ------------------------
+//
+// The single-workgroup search above streams every predictor / joint weight (≈19 MB for the vie recipe)
+// through ONE CU per emission.  rnnt_grid_kernel runs G workgroups per utterance instead; each owns a
+// fixed slice of every matrix-vector product's outputs (LSTM units with their four gates, projection
+// and pred_ffn outputs, vocabulary columns), stored block-major so a workgroup's slice is one
+// contiguous, coalesced stream.  The phases of an emission (nl LSTM layers, projection, pred_ffn, the
+// joint's candidates) are separated by grid barriers on a per-utterance counter; the shared vectors
+// (h / c state slots, projection and pred_ffn outputs, per-workgroup argmax candidates) live in the
+// workspace.  Every workgroup reduces the candidates in the same order, so all of them take the same
+// decisions and leave the loop together.  A barrier that does not complete within ~2^21 polls sets
+// the workspace's error word, after which every workgroup leaves at its next barrier.
+constexpr int RG_NT = 256;     // threads per workgroup (4 waves)
+constexpr int RG_MAXB = 32;    // utterances on the grid path (B * G <= CUs)
+
+struct RnntGrid {
+  const float4* wg[RNNT_MAXL];  // per layer, block-major [K_l][n_b] slices of gate quads (i, f, g, o of a unit)
+  const float4* bg[RNNT_MAXL];  // [H] gate-quad biases (b_ih + b_hh)
+  const float4 *wp, *wpj, *wo;  // block-major slices of the projection, pred_ffn, ffn_out float4 columns
+  int G;
+};
+
+// the contiguous range of M4 output groups owned by part p of G
+CFM_DEV void rg_range(int M4, int G, int p, int& g0, int& n) {
+  g0 = (int)((long long)M4 * p / G);
+  n = (int)((long long)M4 * (p + 1) / G) - g0;
+}
+
+// arrive and wait until all G workgroups of the utterance arrived `epoch` times; false on timeout / error
+CFM_DEV bool rg_barrier(unsigned long long* ctr, unsigned long long target, int* err, int* lflag) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();   // release this workgroup's stores (agent scope)
+    atomicAdd(ctr, 1ull);
+    int ok = 1;
+    unsigned spins = 0;
+    while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) { ok = 0; break; }
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > (1u << 21)) { __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); ok = 0; break; }
+    }
+    __threadfence();   // acquire the other workgroups' stores
+    *lflag = ok;
+  }
+  __syncthreads();
+  return *lflag != 0;
+}
+
+// sums[jj] = sum_k Wb[k][jj] * x[k] for jj < n (Wb: this workgroup's [K][n] float4 slice), threads
+// (s, jj) = (tid / np, tid % np) with np = pow2 >= n: a wave reads whole consecutive rows of the
+// slice; the ks = NT / np partial sums are added in order through `red`.  fin(jj, sum) runs on the
+// thread jj < n.
+template <class F>
+CFM_DEV void rg_matvec(const float4* __restrict__ Wb, int K, int n, const float* x, float4* red, F&& fin) {
+  const int tid = threadIdx.x;
+  if (n <= 0) return;
+  int np = 1;
+  while (np < n) np <<= 1;
+  const int ks = RG_NT / np, jj = tid % np, s = tid / np;
+  float4 acc = {0.f, 0.f, 0.f, 0.f};
+  if (jj < n) {
+#pragma unroll 4
+    for (int k = s; k < K; k += ks) {
+      const float4 wv = Wb[(size_t)k * n + jj];
+      const float xv = x[k];
+      acc.x = fmaf(wv.x, xv, acc.x);
+      acc.y = fmaf(wv.y, xv, acc.y);
+      acc.z = fmaf(wv.z, xv, acc.z);
+      acc.w = fmaf(wv.w, xv, acc.w);
+    }
+  }
+  red[tid] = acc;
+  __syncthreads();
+  if (tid < n) {
+    float4 v = red[tid];
+    for (int q = 1; q < ks; ++q) {
+      const float4 o = red[tid + q * np];
+      v.x += o.x; v.y += o.y; v.z += o.z; v.w += o.w;
+    }
+    fin(tid, v);
+  }
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(RG_NT) void rnnt_grid_kernel(RnntDev w, RnntGrid gw, float* __restrict__ scratch,
+                                                          int per_utt, unsigned long long* __restrict__ bars,
+                                                          int* __restrict__ err, const float* __restrict__ enc_proj,
+                                                          const int32_t* __restrict__ row_start,
+                                                          const int32_t* __restrict__ row_len, int n_steps,
+                                                          int32_t* __restrict__ out) {
+  extern __shared__ float lds[];
+  const int tid = threadIdx.x;
+  const int G = gw.G, utt = blockIdx.x / G, part = blockIdx.x - utt * G;
+  const int H = w.H, J = w.J, P = w.P, E = w.E, nl = w.nl;
+  const int r0 = row_start[utt], T = row_len[utt];
+  // workspace of the utterance: state slots, projection / pred_ffn outputs, candidates (2 parities)
+  float* hs = scratch + (size_t)utt * per_utt;   // [2][nl][H]
+  float* cs = hs + 2 * nl * H;                   // [2][nl][H]
+  float* pvec = cs + 2 * nl * H;                 // [P]
+  float* pj = pvec + P;                          // [J]
+  float* candv = pj + J;                         // [2][G][RF]
+  int* candi = reinterpret_cast<int*>(candv + 2 * G * RNNT_RF);   // [2][G][RF]
+  unsigned long long* bar = bars + (size_t)utt * 16;
+  // LDS: x vector, z block, partial sums, pred_ffn output, decisions
+  float* x = lds;                                // [max(E, H) + H]
+  float* z = x + (max(E, H) + H);                // [RF][J]
+  float* lpj = z + RNNT_RF * J;                  // [J]
+  float4* red = reinterpret_cast<float4*>(lpj + J + ((4 - ((max(E, H) + H + RNNT_RF * J + J) & 3)) & 3));  // [NT * RF]
+  int* dec = reinterpret_cast<int*>(red + RG_NT * RNNT_RF);   // [RF]
+  int* lflag = dec + RNNT_RF;
+  unsigned long long epoch = 0;
+  auto sync = [&]() { return rg_barrier(bar, ++epoch * (unsigned long long)G, err, lflag); };
+
+  int cur = 0;   // committed state slot (zero-initialised by the host)
+  // the predictor for token `tok` from slot cur into slot cur ^ 1; pj -> lpj
+  auto predictor = [&](int tok) -> bool {
+    int in = E;
+    for (int l = 0; l < nl; ++l) {
+      const float* src = l == 0 ? w.embed + (size_t)tok * E : hs + ((size_t)(cur ^ 1) * nl + (l - 1)) * H;
+      for (int e = tid; e < in; e += RG_NT) x[e] = src[e];
+      const float* hc = hs + ((size_t)cur * nl + l) * H;
+      for (int e = tid; e < H; e += RG_NT) x[in + e] = hc[e];
+      __syncthreads();
+      int u0, nu;
+      rg_range(H, G, part, u0, nu);
+      float* cold = cs + ((size_t)cur * nl + l) * H;
+      float* cnew = cs + ((size_t)(cur ^ 1) * nl + l) * H;
+      float* hnew = hs + ((size_t)(cur ^ 1) * nl + l) * H;
+      const float4* bq = gw.bg[l];
+      rg_matvec(gw.wg[l] + (size_t)(in + H) * u0, in + H, nu, x, red, [&](int jj, float4 a) {
+        const int u = u0 + jj;
+        const float4 b = bq[u];
+        const float ig = sigm(a.x + b.x), fg = sigm(a.y + b.y), gg = tanhf(a.z + b.z), og = sigm(a.w + b.w);
+        const float cv = fg * cold[u] + ig * gg;
+        cnew[u] = cv;
+        hnew[u] = og * tanhf(cv);
+      });
+      if (!sync()) return false;
+      in = H;
+    }
+    {
+      const float* ht = hs + ((size_t)(cur ^ 1) * nl + (nl - 1)) * H;
+      for (int e = tid; e < H; e += RG_NT) x[e] = ht[e];
+      __syncthreads();
+      int g0, n;
+      rg_range(P >> 2, G, part, g0, n);
+      const float4* b4 = reinterpret_cast<const float4*>(w.bp);
+      rg_matvec(gw.wp + (size_t)H * g0, H, n, x, red, [&](int jj, float4 a) {
+        const float4 b = b4[g0 + jj];
+        reinterpret_cast<float4*>(pvec)[g0 + jj] = make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+      });
+      if (!sync()) return false;
+    }
+    {
+      for (int e = tid; e < P; e += RG_NT) x[e] = pvec[e];
+      __syncthreads();
+      int g0, n;
+      rg_range(J >> 2, G, part, g0, n);
+      const float4* b4 = reinterpret_cast<const float4*>(w.bpj);
+      rg_matvec(gw.wpj + (size_t)P * g0, P, n, x, red, [&](int jj, float4 a) {
+        const float4 b = b4[g0 + jj];
+        reinterpret_cast<float4*>(pj)[g0 + jj] = make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+      });
+      if (!sync()) return false;
+    }
+    for (int e = tid; e < J; e += RG_NT) lpj[e] = pj[e];
+    __syncthreads();
+    return true;
+  };
+
+  if (!predictor(w.blank)) return;
+  int v0, nv;
+  rg_range(w.Vp >> 2, G, part, v0, nv);
+  int np = 1;
+  while (np < nv) np <<= 1;
+  const int ks = RG_NT / np, jj = tid % np, sp = tid / np;
+  const float4* wo = gw.wo + (size_t)J * v0;
+  const float4* bo4 = reinterpret_cast<const float4*>(w.bo);
+  int t = 0, step = 0;
+  while (t < T) {
+    const int nf = min(RNNT_RF, T - t);
+    for (int e = tid; e < RNNT_RF * J; e += RG_NT) {
+      const int f = e / J, j = e - f * J;
+      z[e] = f < nf ? tanhf(enc_proj[(size_t)(r0 + t + f) * J + j] + lpj[j]) : 0.f;
+    }
+    __syncthreads();
+    // this workgroup's vocabulary columns for all RF frames
+    float4 acc[RNNT_RF];
+#pragma unroll
+    for (int f = 0; f < RNNT_RF; ++f) acc[f] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (jj < nv) {
+#pragma unroll 2
+      for (int k = sp; k < J; k += ks) {
+        const float4 wv = wo[(size_t)k * nv + jj];
+#pragma unroll
+        for (int f = 0; f < RNNT_RF; ++f) {
+          const float zv = z[f * J + k];
+          acc[f].x = fmaf(wv.x, zv, acc[f].x);
+          acc[f].y = fmaf(wv.y, zv, acc[f].y);
+          acc[f].z = fmaf(wv.z, zv, acc[f].z);
+          acc[f].w = fmaf(wv.w, zv, acc[f].w);
+        }
+      }
+    }
+#pragma unroll
+    for (int f = 0; f < RNNT_RF; ++f) red[f * RG_NT + tid] = acc[f];
+    __syncthreads();
+    // (frame, column group) sums in order, then each frame's best over this workgroup's columns
+    float* sv = z;   // z is consumed: reuse as [RF][np] best values / ids
+    int* si = reinterpret_cast<int*>(z + RNNT_RF * 64);
+    for (int e = tid; e < RNNT_RF * nv; e += RG_NT) {
+      const int f = e / nv, c = e - f * nv;
+      float4 v = red[f * RG_NT + c];
+      for (int q = 1; q < ks; ++q) {
+        const float4 o = red[f * RG_NT + c + q * np];
+        v.x += o.x; v.y += o.y; v.z += o.z; v.w += o.w;
+      }
+      const float4 b = bo4[v0 + c];
+      const float v4[4] = {v.x + b.x, v.y + b.y, v.z + b.z, v.w + b.w};
+      float bv = -INFINITY;
+      int bi = 0x7fffffff;
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (v4[q] > bv) { bv = v4[q]; bi = 4 * (v0 + c) + q; }
+      sv[f * 64 + c] = bv;
+      si[f * 64 + c] = bi;
+    }
+    __syncthreads();
+    const int par = (int)(epoch & 1);
+    if (tid < RNNT_RF) {
+      float bv = -INFINITY;
+      int bi = 0x7fffffff;
+      for (int c = 0; c < nv; ++c)   // ascending ids: strict > keeps the lowest id of a tie
+        if (sv[tid * 64 + c] > bv) { bv = sv[tid * 64 + c]; bi = si[tid * 64 + c]; }
+      candv[((size_t)par * G + part) * RNNT_RF + tid] = bv;
+      candi[((size_t)par * G + part) * RNNT_RF + tid] = bi;
+    }
+    if (!sync()) return;
+    if (tid < RNNT_RF) {
+      float bv = -INFINITY;
+      int bi = 0x7fffffff;
+      for (int q = 0; q < G; ++q) {   // parts in ascending vocabulary order
+        const float v = candv[((size_t)par * G + q) * RNNT_RF + tid];
+        if (v > bv) { bv = v; bi = candi[((size_t)par * G + q) * RNNT_RF + tid]; }
+      }
+      dec[tid] = bi;
+    }
+    __syncthreads();
+    int f = 0;
+    while (f < nf && dec[f] == w.blank) ++f;
+    if (f == nf) {
+      t += nf;
+      step = 0;
+      __syncthreads();
+      continue;
+    }
+    if (f > 0) { t += f; step = 0; }
+    const int k = dec[f];
+    __syncthreads();
+    if (part == 0 && tid == 0) out[(size_t)(r0 + t) * n_steps + step] = k;
+    ++step;
+    cur ^= 1;   // commit: the evaluated state becomes the state, k the next input
+    if (!predictor(k)) return;
+    if (step == n_steps) { ++t; step = 0; }
+  }
+}
+
+size_t rnnt_grid_lds_bytes(const RnntDev& w) {
+  const size_t fl = (std::max(w.E, w.H) + w.H) + RNNT_RF * w.J + w.J;
+  return (fl + 3) / 4 * 16 + (size_t)RG_NT * RNNT_RF * 16 + 2 * RNNT_RF * 4 + 16;
+}
+
 size_t rnnt_lds_bytes(const RnntDev& w) {
   const size_t H = w.H, J = w.J, P = w.P;
   size_t f = 4 * w.nl * H + (std::max<size_t>(w.E, H) + H) + 4 * H + P + J + RNNT_RF * J + 4 * RNNT_NT +
@@ -252,8 +524,18 @@ struct cfm_rnnt {
   void* dev_mem = nullptr;
   cfm::RnntDev w{};
   const float *we = nullptr, *be = nullptr;   // enc_ffn [J, Eenc] (torch layout), [J]
+  // the grid path's block-major slices (built for grid_blocks workgroups per utterance)
+  int grid_blocks = 64;                       // 0: always one workgroup per utterance
+  int n_cu = 0;
+  void* grid_mem = nullptr;
+  cfm::RnntGrid gw{};
+  std::vector<std::vector<float>> host_wg;    // [(in_l + H)][4H] transposed gate weights per layer
+  std::vector<std::vector<float>> host_bg;    // [4H]
+  std::vector<float> host_wp, host_wpj, host_wo;   // [H][P], [P][J], [J][Vp]
   ~cfm_rnnt() {
-    if (dev_mem) { (void)hipSetDevice(device); (void)hipFree(dev_mem); }
+    (void)hipSetDevice(device);
+    if (dev_mem) (void)hipFree(dev_mem);
+    if (grid_mem) (void)hipFree(grid_mem);
   }
 };
 
@@ -271,6 +553,77 @@ struct Img {
     fix.push_back({off, slot});
   }
 };
+
+// block-major slices of the grid path for h->grid_blocks workgroups (the ranges of rg_range)
+int rnnt_grid_build(cfm_rnnt* h) {
+  if (h->grid_mem) { (void)hipFree(h->grid_mem); h->grid_mem = nullptr; }
+  const int G = h->grid_blocks;
+  h->gw = RnntGrid{};
+  h->gw.G = G;
+  if (G <= 0) return 0;
+  const RnntDev& w = h->w;
+  const int H = w.H;
+  std::vector<float> img;
+  std::vector<std::pair<size_t, const float4**>> fix;
+  auto put = [&](const std::vector<float>& v, const float4** slot) {
+    const size_t off = (img.size() + 63) / 64 * 64;
+    img.resize(off + v.size());
+    std::copy(v.begin(), v.end(), img.begin() + off);
+    fix.push_back({off, slot});
+  };
+  auto range = [&](int M4, int p, int& g0, int& n) {
+    g0 = (int)((long long)M4 * p / G);
+    n = (int)((long long)M4 * (p + 1) / G) - g0;
+  };
+  // quad(k, g) -> 4 floats; slices [part][k][n]
+  auto slices = [&](int K, int M4, auto quad) {
+    std::vector<float> o((size_t)K * M4 * 4);
+    size_t at = 0;
+    for (int p = 0; p < G; ++p) {
+      int g0, n;
+      range(M4, p, g0, n);
+      for (int k = 0; k < K; ++k)
+        for (int j = 0; j < n; ++j) {
+          quad(k, g0 + j, &o[at]);
+          at += 4;
+        }
+    }
+    return o;
+  };
+  for (int l = 0; l < w.nl; ++l) {
+    const std::vector<float>& a = h->host_wg[l];
+    const int K = (int)(a.size() / (4 * (size_t)H));
+    put(slices(K, H, [&](int k, int u, float* q) {
+          for (int gi = 0; gi < 4; ++gi) q[gi] = a[(size_t)k * 4 * H + gi * H + u];
+        }), &h->gw.wg[l]);
+    std::vector<float> bq(4 * (size_t)H);
+    for (int u = 0; u < H; ++u)
+      for (int gi = 0; gi < 4; ++gi) bq[4 * u + gi] = h->host_bg[l][gi * H + u];
+    put(bq, &h->gw.bg[l]);
+  }
+  auto cols = [&](const std::vector<float>& m, int K, int M) {
+    return slices(K, M / 4, [&](int k, int g, float* q) {
+      for (int i = 0; i < 4; ++i) q[i] = m[(size_t)k * M + 4 * g + i];
+    });
+  };
+  put(cols(h->host_wp, H, w.P), &h->gw.wp);
+  put(cols(h->host_wpj, w.P, w.J), &h->gw.wpj);
+  put(cols(h->host_wo, w.J, w.Vp), &h->gw.wo);
+  if (hipSetDevice(h->device) != hipSuccess || hipMalloc(&h->grid_mem, img.size() * 4) != hipSuccess ||
+      hipMemcpy(h->grid_mem, img.data(), img.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
+    set_error(CFM_ERR_RUNTIME, std::string("rnnt grid weights upload: ") + hipGetErrorString(hipGetLastError()));
+    return 1;
+  }
+  for (auto& f : fix) *f.second = reinterpret_cast<const float4*>((float*)h->grid_mem + f.first);
+  return 0;
+}
+
+// floats of one utterance's grid workspace
+size_t rnnt_grid_per_utt(const cfm_rnnt* h) {
+  const RnntDev& w = h->w;
+  const size_t G = std::max(h->grid_blocks, 1);
+  return ((size_t)4 * w.nl * w.H + w.P + w.J + 4 * G * RNNT_RF + 63) / 64 * 64;
+}
 
 }  // namespace
 
@@ -323,14 +676,19 @@ cfm_status cfm_rnnt_create(const cfm_rnnt_config* cfg, const cfm_tensor_view* we
       std::vector<float> bias(4 * H);
       for (int i = 0; i < 4 * H; ++i) bias[i] = bih[i] + bhh[i];
       img.put(bias, &w.bg[l]);
+      h->host_wg.push_back(std::move(a));
+      h->host_bg.push_back(std::move(bias));
     }
-    img.put(transpose(get("predictor.projection.weight", (int64_t)P * H), P, H, P), &w.wp);
+    h->host_wp = transpose(get("predictor.projection.weight", (int64_t)P * H), P, H, P);
+    img.put(h->host_wp, &w.wp);
     const float* bp = get("predictor.projection.bias", P);
     img.put(std::vector<float>(bp, bp + P), &w.bp);
-    img.put(transpose(get("joint.pred_ffn.weight", (int64_t)J * P), J, P, J), &w.wpj);
+    h->host_wpj = transpose(get("joint.pred_ffn.weight", (int64_t)J * P), J, P, J);
+    img.put(h->host_wpj, &w.wpj);
     const float* bpj = get("joint.pred_ffn.bias", J);
     img.put(std::vector<float>(bpj, bpj + J), &w.bpj);
-    img.put(transpose(get("joint.ffn_out.weight", (int64_t)V * J), V, J, w.Vp), &w.wo);
+    h->host_wo = transpose(get("joint.ffn_out.weight", (int64_t)V * J), V, J, w.Vp);
+    img.put(h->host_wo, &w.wo);
     const float* bo = get("joint.ffn_out.bias", V);
     std::vector<float> bov(w.Vp, -std::numeric_limits<float>::infinity());
     std::copy(bo, bo + V, bov.begin());
@@ -347,14 +705,46 @@ cfm_status cfm_rnnt_create(const cfm_rnnt_config* cfg, const cfm_tensor_view* we
       hipMemcpy(h->dev_mem, img.bytes.data(), img.bytes.size(), hipMemcpyHostToDevice) != hipSuccess)
     return set_error(CFM_ERR_RUNTIME, std::string("rnnt weights upload: ") + hipGetErrorString(hipGetLastError()));
   for (auto& f : img.fix) *f.second = reinterpret_cast<const float*>((char*)h->dev_mem + f.first);
+  h->n_cu = cu_count();
+  if (rnnt_grid_build(h.get())) return CFM_ERR_RUNTIME;
   *out = h.release();
   return CFM_OK;
 }
 
 void cfm_rnnt_destroy(cfm_rnnt* h) { delete h; }
 
+// enc_proj rows, then the grid path's state (RG_MAXB utterances), barrier counters and error word
 size_t cfm_rnnt_workspace_bytes(const cfm_rnnt* h, int32_t rows) {
-  return h && rows > 0 ? (size_t)rows * h->cfg.join_dim * sizeof(float) + 256 : 0;
+  if (!h || rows <= 0) return 0;
+  const size_t proj = ((size_t)rows * h->cfg.join_dim * sizeof(float) + 255) / 256 * 256;
+  return proj + (size_t)RG_MAXB * rnnt_grid_per_utt(h) * 4 + (size_t)RG_MAXB * 128 + 256;
+}
+
+cfm_status cfm_rnnt_set_option(cfm_rnnt* h, const char* key, int64_t value) {
+  if (!h || !key) return set_error(CFM_ERR_VALUE, "null argument");
+  if (std::string(key) == "grid_blocks") {
+    if (value < 0 || value > 256) return set_error(CFM_ERR_VALUE, "grid_blocks: 0 (off) .. 256");
+    h->grid_blocks = (int)value;
+    if (hipSetDevice(h->device) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
+      return set_error(CFM_ERR_RUNTIME, "rnnt: device sync");
+    return rnnt_grid_build(h) ? CFM_ERR_RUNTIME : CFM_OK;
+  }
+  return set_error(CFM_ERR_VALUE, std::string("unknown rnnt option ") + key);
+}
+
+int32_t cfm_rnnt_grid_blocks(const cfm_rnnt* h, int32_t B) {
+  if (!h || B <= 0 || h->grid_blocks <= 0 || B > RG_MAXB || (int64_t)B * h->grid_blocks > h->n_cu) return 0;
+  // the joint's per-workgroup candidates reuse the z block: <= 64 column groups per workgroup, J >= 128
+  if ((h->w.Vp / 4 + h->grid_blocks - 1) / h->grid_blocks > 64 || h->w.J < 128) return 0;
+  return h->grid_blocks;
+}
+
+int32_t cfm_rnnt_error(const cfm_rnnt* h, const void* ws, int32_t rows) {
+  if (!h || !ws || rows <= 0) return 0;
+  const size_t at = cfm_rnnt_workspace_bytes(h, rows) - 256;
+  int32_t e = 0;
+  if (hipMemcpy(&e, (const char*)ws + at, 4, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  return e;
 }
 
 cfm_status cfm_rnnt_greedy(const cfm_rnnt* h, const float* enc, int32_t rows, const int32_t* row_start,
@@ -373,6 +763,28 @@ cfm_status cfm_rnnt_greedy(const cfm_rnnt* h, const float* enc, int32_t rows, co
   int r = gemm<float>(EPI_STORE, ACT_NONE, enc, h->cfg.enc_dim, h->we, h->cfg.enc_dim, rows, h->cfg.join_dim,
                       h->cfg.enc_dim, e, st);
   if (r) return set_error(CFM_ERR_RUNTIME, std::string("rnnt enc_ffn gemm: ") + hipGetErrorString((hipError_t)r));
+  const int G = cfm_rnnt_grid_blocks(h, B);
+  if (G > 0) {
+    // grid path: zeroed state slots, counters and error word, then G workgroups per utterance
+    const size_t proj_b = ((size_t)rows * h->cfg.join_dim * sizeof(float) + 255) / 256 * 256;
+    const size_t per = rnnt_grid_per_utt(h);
+    char* gbase = (char*)ws + proj_b;
+    float* scratch = (float*)gbase;
+    unsigned long long* bars = (unsigned long long*)(gbase + (size_t)RG_MAXB * per * 4);
+    int* err = (int*)((char*)bars + (size_t)RG_MAXB * 128);
+    if (hipMemsetAsync(scratch, 0, (size_t)B * per * 4, st) != hipSuccess ||
+        hipMemsetAsync(bars, 0, (size_t)RG_MAXB * 128 + 256, st) != hipSuccess)
+      return set_error(CFM_ERR_RUNTIME, "rnnt: workspace memset");
+    const size_t glds = rnnt_grid_lds_bytes(h->w);
+    if (glds > 64 * 1024 && hipFuncSetAttribute((const void*)rnnt_grid_kernel,
+                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)glds) != hipSuccess)
+      return set_error(CFM_ERR_RUNTIME, "rnnt: dynamic LDS attribute");
+    hipLaunchKernelGGL(rnnt_grid_kernel, dim3(B * G), dim3(RG_NT), glds, st, h->w, h->gw, scratch, (int)per, bars, err,
+                       proj, row_start, row_len, n_steps, out);
+    const hipError_t ge = hipGetLastError();
+    if (ge != hipSuccess) return set_error(CFM_ERR_RUNTIME, std::string("rnnt_grid_kernel: ") + hipGetErrorString(ge));
+    return CFM_OK;
+  }
   const size_t lds = rnnt_lds_bytes(h->w);
   if (lds > 64 * 1024 &&
       hipFuncSetAttribute((const void*)rnnt_greedy_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)

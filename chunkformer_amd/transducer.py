@@ -108,7 +108,9 @@ def synthetic_transducer_state_dict(c: RNNTConfig, seed: int = 0, blank_bias: fl
 
 class RNNTGreedy:
     """The transducer greedy search on libcfm (cfm_rnnt_*): predictor LSTM + joint + argmax loop in
-    one persistent kernel, one workgroup per utterance, the predictor evaluated once per emitted
+    one persistent kernel — one workgroup per utterance for batches, `grid_blocks` workgroups per
+    utterance with grid barriers between the predictor / joint phases for a few long utterances
+    (endless_decode's B = 1) — the predictor evaluated once per emitted
     token and the joint evaluated over blocks of frames at a time (exact: frames before the first
     non-blank of a block see the same predictor state as in the sequential loop)."""
 
@@ -137,6 +139,15 @@ class RNNTGreedy:
         self._h = h
         self._finalizer = weakref.finalize(self, _lib.cfm_rnnt_destroy, ctypes.c_void_p(h.value))
 
+    def set_option(self, key: str, value: int) -> None:
+        """cfm_rnnt_set_option: "grid_blocks" = workgroups per utterance of the multi-CU search
+        (0 = one workgroup per utterance always)."""
+        _lib.check(_lib.cfm_rnnt_set_option(self._h, key.encode(), int(value)))
+
+    def grid_blocks(self, B: int) -> int:
+        """Workgroups per utterance a search over B utterances runs with (0: one-workgroup kernel)."""
+        return int(_lib.cfm_rnnt_grid_blocks(self._h, int(B)))
+
     @torch.no_grad()
     def greedy_packed(self, enc: torch.Tensor, row_start, row_len, n_steps: int = 64) -> torch.Tensor:
         """Greedy search over utterances b = rows [row_start[b], row_start[b] + row_len[b]) of
@@ -162,6 +173,11 @@ class RNNTGreedy:
                                         int(n_steps), out.data_ptr(), ws.data_ptr(), nbytes,
                                         torch.cuda.current_stream(self.device).cuda_stream))
         self._keep = (rs_d, rl_d, ws)   # alive until the stream consumed them
+        if self.grid_blocks(B):
+            # the multi-CU search stops early if a grid barrier timed out: never return a partial result
+            torch.cuda.current_stream(self.device).synchronize()
+            if int(_lib.cfm_rnnt_error(self._h, ws.data_ptr(), rows)) != 0:
+                raise RuntimeError("cfm_rnnt_greedy: multi-CU search barrier timed out")
         return out
 
     @torch.no_grad()

@@ -47,17 +47,25 @@ def test_batch_matches_reference(rnnt, golden_dir):
     assert [t for h in hyps for t in h] == g["batch_hyps"].tolist()
 
 
-def test_endless_b1_matches_reference(rnnt, golden_dir):
+@pytest.mark.parametrize("grid", [64, 16, 0])
+def test_endless_b1_matches_reference(rnnt, golden_dir, grid):
+    """B = 1: the multi-CU search (grid_blocks workgroups, grid barriers) and the one-workgroup kernel."""
     g, c, _, dec = rnnt
     ge = np.load(os.path.join(golden_dir, "large_endless.npz"))
     T = g["endless_out"].shape[1] // int(g["n_steps"])
     enc = torch.from_numpy(ge["out"][:T]).unsqueeze(0).cuda()
-    out = dec.optimized_search(enc, torch.tensor([T]), int(g["n_steps"]))
+    dec.set_option("grid_blocks", grid)
+    try:
+        assert dec.grid_blocks(1) == grid
+        out = dec.optimized_search(enc, torch.tensor([T]), int(g["n_steps"]))
+    finally:
+        dec.set_option("grid_blocks", 64)
     np.testing.assert_array_equal(out.cpu().numpy(), g["endless_out"])
 
 
+@pytest.mark.parametrize("grid", [64, 0])
 @pytest.mark.parametrize("key,n_steps", [("endless_out", 64), ("endless_out_steps3", 3)])
-def test_sparse_emission_matches_reference(golden_dir, key, n_steps):
+def test_sparse_emission_matches_reference(golden_dir, key, n_steps, grid):
     """rnnt_sparse.npz: a blank-dominated joint (80% of the frames decide blank first, in runs), B=1
     over the endless encoder rows: the regime of the kernel's 8-frame blank-block skip."""
     from chunkformer_amd.transducer import RNNTConfig, RNNTGreedy, synthetic_transducer_state_dict
@@ -66,6 +74,8 @@ def test_sparse_emission_matches_reference(golden_dir, key, n_steps):
     sd = synthetic_transducer_state_dict(c, int(g["seed"]), blank_bias=float(g["blank_bias"]),
                                          enc_scale=float(g["enc_scale"]))
     dec = RNNTGreedy(c, sd, "cuda")
+    dec.set_option("grid_blocks", grid)
+    assert dec.grid_blocks(1) == grid
     ge = np.load(os.path.join(golden_dir, "large_endless.npz"))
     T = g[key].shape[1] // n_steps
     enc = torch.from_numpy(ge["out"][:T]).unsqueeze(0).cuda()
@@ -73,16 +83,24 @@ def test_sparse_emission_matches_reference(golden_dir, key, n_steps):
     np.testing.assert_array_equal(out.cpu().numpy(), g[key])
 
 
+@pytest.mark.parametrize("grid", [64, 0])
 @pytest.mark.parametrize("n_steps", [1, 3])
-def test_small_cap_and_ragged_vs_oracle(rnnt, n_steps):
-    """n_steps 1 / 3 (the cap reached often), ragged packed utterances incl. empty and one frame."""
+def test_small_cap_and_ragged_vs_oracle(rnnt, n_steps, grid):
+    """n_steps 1 / 3 (the cap reached often), ragged packed utterances incl. empty and one frame; B = 4
+    runs on the multi-CU search (4 x 64 workgroups) or the one-workgroup kernel."""
     from oracle import rnnt_ref
     _, c, sd, dec = rnnt
     gen = torch.Generator().manual_seed(5)
     lens = [37, 0, 1, 90]
     enc = torch.randn(sum(lens), c.enc_dim, generator=gen)
     starts = np.cumsum([0] + lens[:-1]).tolist()
-    dense = dec.greedy_packed(enc.cuda(), starts, lens, n_steps).cpu()
+    dec.set_option("grid_blocks", grid)
+    try:
+        if grid and torch.cuda.get_device_properties(0).multi_processor_count >= 4 * grid:
+            assert dec.grid_blocks(len(lens)) == grid
+        dense = dec.greedy_packed(enc.cuda(), starts, lens, n_steps).cpu()
+    finally:
+        dec.set_option("grid_blocks", 64)
     for s0, n in zip(starts, lens):
         o, _ = rnnt_ref.greedy_one(sd, c.num_layers, c.hidden, enc[s0: s0 + n], n_steps)
         np.testing.assert_array_equal(dense[s0: s0 + n].numpy(), o.numpy())
@@ -163,3 +181,27 @@ def test_transducer_endless_segments(rnnt, golden_dir):
     assert tok.shape[1] == ge["out"].shape[0]
     np.testing.assert_allclose(eo[0].cpu().numpy(), ge["out"], atol=1e-4, rtol=0)
     np.testing.assert_array_equal(tok[0, :T].cpu().numpy(), g["endless_out"].reshape(-1, n))
+
+
+@pytest.mark.parametrize("G,B", [(8, 1), (37, 2), (128, 1), (256, 1), (64, 3)])
+def test_grid_search_equals_one_workgroup(G, B):
+    """The multi-CU search at odd / large workgroup counts (uneven output slices, slices with no
+    vocabulary columns) takes exactly the one-workgroup kernel's decisions on random rows, with a
+    vocabulary that is not a multiple of 4 (padded columns) and a 1-layer predictor."""
+    from chunkformer_amd.transducer import RNNTConfig, RNNTGreedy, synthetic_transducer_state_dict
+    c = RNNTConfig(vocab=1001, hidden=256, num_layers=1, embed_size=128, pred_out=256, join_dim=384)
+    sd = synthetic_transducer_state_dict(c, 7, blank_bias=5.0)
+    dec = RNNTGreedy(c, sd, "cuda")
+    if B * G > torch.cuda.get_device_properties(0).multi_processor_count:
+        pytest.skip("needs B * G CUs")
+    gen = torch.Generator().manual_seed(11)
+    lens = [300, 171, 64][:B]
+    enc = torch.randn(sum(lens), c.enc_dim, generator=gen).cuda()
+    starts = np.cumsum([0] + lens[:-1]).tolist()
+    dec.set_option("grid_blocks", 0)
+    ref = dec.greedy_packed(enc, starts, lens, 4).cpu()
+    dec.set_option("grid_blocks", G)
+    assert dec.grid_blocks(B) == G
+    out = dec.greedy_packed(enc, starts, lens, 4).cpu()
+    assert (ref != 0).any() and (ref == 0).any()
+    np.testing.assert_array_equal(out.numpy(), ref.numpy())

@@ -19,23 +19,32 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--frames", type=int, default=45000)
     ap.add_argument("--batch", type=int, default=1)
+    ap.add_argument("--grid", type=int, nargs="*", default=[64],
+                    help="workgroups per utterance of the multi-CU search (0 = one workgroup)")
+    ap.add_argument("--blank-bias", type=float, default=3.72)
     a = ap.parse_args()
     c = RNNTConfig()
-    g = RNNTGreedy(c, synthetic_transducer_state_dict(c, 0), device="cuda")
+    g = RNNTGreedy(c, synthetic_transducer_state_dict(c, 0, blank_bias=a.blank_bias), device="cuda")
     gen = torch.Generator(device="cuda").manual_seed(3)
     B, T = a.batch, a.frames
     enc = torch.randn(B * T, c.enc_dim, generator=gen, device="cuda")
     starts = [b * T for b in range(B)]
     lens = [T] * B
-    g.greedy_packed(enc[: min(B * T, 2000)], [0], [min(T, 2000)])   # warm-up
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    out = g.greedy_packed(enc, starts, lens)
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
-    emis = int((out != c.blank).sum().item()) if out.dtype != torch.bool else 0
-    print(f"B={B} T={T}: {dt * 1e3:.1f} ms, {B * T / dt:.0f} frames/s, {emis / (B * T):.3f} emissions per frame, "
-          f"{dt * 1e3 / max(emis / B, 1):.3f} ms per emission per utterance")
+    ref = None
+    for G in a.grid:
+        g.set_option("grid_blocks", G)
+        g.greedy_packed(enc[: min(B * T, 2000)], [0], [min(T, 2000)])   # warm-up
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        out = g.greedy_packed(enc, starts, lens)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        same = "" if ref is None else f", identical to grid {a.grid[0]}: {bool(torch.equal(out, ref))}"
+        ref = out if ref is None else ref
+        emis = int((out != c.blank).sum().item())
+        print(f"grid {G} (used {g.grid_blocks(B)}) B={B} T={T}: {dt * 1e3:.1f} ms, {B * T / dt:.0f} frames/s, "
+              f"{emis / (B * T):.3f} emissions per frame, {dt * 1e3 / max(emis / B, 1):.4f} ms per emission per "
+              f"utterance{same}", flush=True)
 
 
 if __name__ == "__main__":
