@@ -231,7 +231,7 @@ __global__ __launch_bounds__(RNNT_NT) void rnnt_greedy_kernel(RnntDev w, const f
     // commit the emission: the predictor's new state becomes the state, k the next input
     for (int e = tid; e < nl * H; e += RNNT_NT) { h[e] = hn[e]; c[e] = cn[e]; }
     __syncthreads();
-    tok = k;
+    tok = (unsigned)k < (unsigned)w.V ? k : w.blank;   // NaN logits leave no valid id: never index past embed
     predictor(w, tok, h, c, hn, cn, xin, gates, pvec, pj, red, tid);
     if (step == n_steps) { ++t; step = 0; }
   }
@@ -499,7 +499,7 @@ __global__ __launch_bounds__(RG_NT) void rnnt_grid_kernel(RnntDev w, RnntGrid gw
     if (part == 0 && tid == 0) out[(size_t)(r0 + t) * n_steps + step] = k;
     ++step;
     cur ^= 1;   // commit: the evaluated state becomes the state, k the next input
-    if (!predictor(k)) return;
+    if (!predictor((unsigned)k < (unsigned)w.V ? k : w.blank)) return;   // (NaN logits: no valid id)
     if (step == n_steps) { ++t; step = 0; }
   }
 }
