@@ -69,13 +69,16 @@ CFM_DEV f32x4 mfma_pa0(const bf16x8& a, const bf16x8& b) {   // C = 0 (inline co
 constexpr float Q32_DEFER = 5.545177444479562f;   // 8 / log2(e)
 }  // namespace
 
-// NH = W / 32 key halves per window (2..10; W = L + 64 + R); PIPE: 0 = one half after the other,
-// 1 = software-pipelined by one half
-template <int NH, int PIPE>
+// NH = W / 32 key halves per window (2..10; W = L + 64 + R); PIPE bit 0: software-pipelined by one
+// half (else one half after the other), bit 1: branch-free O rescale (alpha = 1 when no maximum grew:
+// one basic block per half for the scheduler); DG: the timing-only `diag` hooks are compiled in (the
+// production instantiation has no diag branch inside the half loop)
+template <int NH, int PIPE, bool DG>
 __global__ __launch_bounds__(256, 1) void chunk_attention_q32_kernel(
     const bf16* __restrict__ Q, const bf16* __restrict__ KV, int kv_rows, const bf16* __restrict__ P, int p_rows,
     int p_ld, const float* __restrict__ pos_u, const float* __restrict__ pos_v, const int32_t* __restrict__ desc,
-    int n_chunks, int H, int nch, bf16* __restrict__ out, int diag) {
+    int n_chunks, int H, int nch, bf16* __restrict__ out, int diag_arg) {
+  const int diag = DG ? diag_arg : 0;
   // diag (timing only, model option "attn_diag" >= 64): bit 0 no band MFMAs / writes, bit 1 no exp +
   // P.V, bit 2 no score MFMAs, bit 3 no LDS-DMA of the next pair (stale rows)
   constexpr int W = 32 * NH;
@@ -341,7 +344,18 @@ __global__ __launch_bounds__(256, 1) void chunk_attention_q32_kernel(
           grew |= up;
           ml[q] = up ? x : m[q];
         }
-        if (!first && __builtin_amdgcn_ballot_w64(grew)) {
+        if constexpr (PIPE & 2) {
+          if (!first) {
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+              // 1 where the maximum stayed (exp2(0)), 0 while no key of the query was unmasked
+              const float alpha = m[q] == -INFINITY ? 0.f : __builtin_amdgcn_exp2f((m[q] - ml[q]) * 1.4426950408889634f);
+              Ol[q] *= alpha;
+#pragma unroll
+              for (int dt = 0; dt < 4; ++dt) O[q][dt] *= alpha;
+            }
+          }
+        } else if (!first && __builtin_amdgcn_ballot_w64(grew)) {
 #pragma unroll
           for (int q = 0; q < 2; ++q) {
             // pass-through terms at the old maximum, rescaled (0 while no key of the query was unmasked)
@@ -377,7 +391,7 @@ __global__ __launch_bounds__(256, 1) void chunk_attention_q32_kernel(
       };
 
       HalfOps cur = load_ops(0);
-      if constexpr (PIPE == 0) {
+      if constexpr ((PIPE & 1) == 0) {
         // one half after the other: V^T reads, scores, the next half's band and operands, softmax, P.V
         sfor<0, NH>([&](auto HFc) {
           constexpr int hf = decltype(HFc)::value;
@@ -474,13 +488,16 @@ int chunk_attention_masked_q32(const bf16* q, const bf16* kv, int kv_rows, const
   int nch = (int)(((long long)n_chunks * H + cu_count() - 1) / cu_count());
   nch = max(4, (nch + 1) & ~1);
   const dim3 grid((n_chunks + nch - 1) / nch, H);
+#define Q32L(NH_, PP_, DG_)                                                                                          \
+  hipLaunchKernelGGL((chunk_attention_q32_kernel<NH_, PP_, DG_>), grid, dim3(256), 0, st, q, kv, kv_rows, P, p_rows, \
+                     p_ld, pos_u, pos_v, desc, n_chunks, H, nch, out, diag)
+  // the production shape (W = 320) also has the pipelining variants and the diag build; the others
+  // only the default
 #define Q32(NH_)                                                                                                     \
-  if (pipe)                                                                                                          \
-    hipLaunchKernelGGL((chunk_attention_q32_kernel<NH_, 1>), grid, dim3(256), 0, st, q, kv, kv_rows, P, p_rows,     \
-                       p_ld, pos_u, pos_v, desc, n_chunks, H, nch, out, diag);                                       \
-  else                                                                                                               \
-    hipLaunchKernelGGL((chunk_attention_q32_kernel<NH_, 0>), grid, dim3(256), 0, st, q, kv, kv_rows, P, p_rows,     \
-                       p_ld, pos_u, pos_v, desc, n_chunks, H, nch, out, diag)
+  if (NH_ != 10 || (pipe == 3 && !diag)) Q32L(NH_, 3, false);                                                        \
+  else if (diag) Q32L(NH_, 3, true);                                                                                 \
+  else if (pipe == 2) Q32L(NH_, 1, false);                                                                           \
+  else Q32L(NH_, 0, false)
   switch (W / 32) {
     case 2: Q32(2); break;
     case 3: Q32(3); break;
@@ -493,6 +510,7 @@ int chunk_attention_masked_q32(const bf16* q, const bf16* kv, int kv_rows, const
     default: Q32(10); break;
   }
 #undef Q32
+#undef Q32L
   CFM_CHECK_LAUNCH();
   return 0;
 }

@@ -56,8 +56,9 @@ struct Tuning {
   int fe_fuse_dw2 = 1;           // front-end: pw1 + ReLU + dw2 in one weight-stationary GEMM (bf16; bench A/B
                                  // 50.85 -> 50.15 ms/step, 3 interleaved pairs; 0 = pw1 GEMM + fe_dw2_kernel)
   int attn128_var = 1;           // head_dim 128 attention kernel variant (A/B)
-  int attn_q32 = 2;              // dk 64, C 64: the 32-queries-per-wave kernel (attention_q32.hip; 2 = software-
-                                 // pipelined by one half, 1 = half after half); 0 = the 8-wave ring kernel
+  int attn_q32 = 0;              // dk 64, C 64: the 32-queries-per-wave kernel (attention_q32.hip; 1 = half after
+                                 // half, 2 = software-pipelined by one half, 3 = pipelined with a branch-free
+                                 // rescale); 0 = the 8-wave ring kernel
   // GEMM sites whose bf16 outputs are stored non-temporally ("nt_sites" bit mask, SITE_* below).
   // Default: FFN w2 (its y goes straight to the LayerNorm; bench A/B 52.2 -> 51.4 ms/step); nt on
   // the front-end pointwise outputs (+0.45 ms) or FFN w1's hidden (w1 slower) measured worse.
@@ -126,7 +127,7 @@ bool attention_a128_eligible(int C, int W, int p_rows, int dk);
 bool attention_q32_eligible(int C, int W, int p_rows);
 int chunk_attention_masked_q32(const bf16* q, const bf16* kv, int kv_rows, const bf16* P, int p_rows, int p_ld,
                                const float* pos_u, const float* pos_v, const int32_t* desc, int n_chunks, int H, int C,
-                               int W, bf16* out, hipStream_t st, int diag = 0, int pipe = 1);
+                               int W, bf16* out, hipStream_t st, int diag = 0, int pipe = 3);
 int vt_transpose_bf16(const bf16* kv, int kv_rows, int H, bf16* vt, int vt_ld, hipStream_t st);
 int chunk_attention_masked_a128(const bf16* q, const bf16* kv, int kv_rows, const bf16* vt, int vt_ld, const bf16* P,
                                 int p_rows, int p_ld, const float* pos_u, const float* pos_v, const int32_t* desc,

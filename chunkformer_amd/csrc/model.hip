@@ -373,7 +373,7 @@ struct ModelT : public cfm_model {
           if (masked && use_ring_attention && dk == 64 && tune.attn_q32)
             r = chunk_attention_masked_q32(w.q, w.kv, kv_rows, w.P + (size_t)l * d, p_rows, p_ld, Lw.pu, Lw.pv, attd,
                                            natt, H, C, hh[PH_L] + C + hh[PH_R], w.ao, st,
-                                           attn_diag >= 64 ? attn_diag - 64 : 0, tune.attn_q32 >= 2);
+                                           attn_diag >= 64 ? attn_diag - 64 : 0, tune.attn_q32);
           if (r == -1 && masked && use_ring_attention && dk == 64)
             r = chunk_attention_masked_bf16(w.q, w.kv, kv_rows, w.P + (size_t)l * d, p_rows, Lw.pu, Lw.pv,
                                             attd, natt, H, C, hh[PH_L] + C + hh[PH_R], w.ao, st, attn_diag, p_ld,

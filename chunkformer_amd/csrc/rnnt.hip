@@ -244,13 +244,14 @@ __global__ __launch_bounds__(RNNT_NT) void rnnt_greedy_kernel(RnntDev w, const f
 // fixed slice of every matrix-vector product's outputs (LSTM units with their four gates, projection
 // and pred_ffn outputs, vocabulary columns), stored block-major so a workgroup's slice is one
 // contiguous, coalesced stream.  The phases of an emission (nl LSTM layers, projection, pred_ffn, the
-// joint's candidates) are separated by grid barriers on a per-utterance counter; the shared vectors
+// joint's candidates) are separated by grid barriers on per-utterance flag words; the shared vectors
 // (h / c state slots, projection and pred_ffn outputs, per-workgroup argmax candidates) live in the
 // workspace.  Every workgroup reduces the candidates in the same order, so all of them take the same
 // decisions and leave the loop together.  A barrier that does not complete within ~2^21 polls sets
 // the workspace's error word, after which every workgroup leaves at its next barrier.
 constexpr int RG_NT = 256;     // threads per workgroup (4 waves)
 constexpr int RG_MAXB = 32;    // utterances on the grid path (B * G <= CUs)
+constexpr int RG_MAXG = 256;   // workgroups per utterance
 
 struct RnntGrid {
   const float4* wg[RNNT_MAXL];  // per layer, block-major [K_l][n_b] slices of gate quads (i, f, g, o of a unit)
@@ -265,21 +266,36 @@ CFM_DEV void rg_range(int M4, int G, int p, int& g0, int& n) {
   n = (int)((long long)M4 * (p + 1) / G) - g0;
 }
 
-// arrive and wait until all G workgroups of the utterance arrived `epoch` times; false on timeout / error
-CFM_DEV bool rg_barrier(unsigned long long* ctr, unsigned long long target, int* err, int* lflag) {
+// Grid barrier over the G workgroups of one utterance: workgroup p publishes the barrier's epoch in
+// its own flag word (no contended atomic: a counter serialised the G arrivals, ≈0.1 µs each), wave 0
+// of every workgroup polls all G flags (one load per lane) until each holds the epoch.  Release /
+// acquire: __syncthreads, then an agent-scope fence before the flag store and after the poll.
+// Returns false on timeout (after ~2^21 polls the error word is set) or when another workgroup set it.
+CFM_DEV bool rg_barrier(unsigned long long* flags, int G, int part, unsigned long long epoch, int* err, int* lflag) {
   __syncthreads();
-  if (threadIdx.x == 0) {
-    __threadfence();   // release this workgroup's stores (agent scope)
-    atomicAdd(ctr, 1ull);
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    if (lane == 0) {
+      __threadfence();   // release this workgroup's stores (agent scope)
+      __hip_atomic_store(flags + part, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     int ok = 1;
     unsigned spins = 0;
-    while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+    for (;;) {
+      bool ready = true;
+      for (int q = lane; q < G; q += 64)
+        ready &= __hip_atomic_load(flags + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= epoch;
+      if (__builtin_amdgcn_ballot_w64(!ready) == 0) break;
       if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) { ok = 0; break; }
       __builtin_amdgcn_s_sleep(1);
-      if (++spins > (1u << 21)) { __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); ok = 0; break; }
+      if (++spins > (1u << 21)) {
+        if (lane == 0) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ok = 0;
+        break;
+      }
     }
     __threadfence();   // acquire the other workgroups' stores
-    *lflag = ok;
+    if (lane == 0) *lflag = ok;
   }
   __syncthreads();
   return *lflag != 0;
@@ -339,7 +355,7 @@ __global__ __launch_bounds__(RG_NT) void rnnt_grid_kernel(RnntDev w, RnntGrid gw
   float* pj = pvec + P;                          // [J]
   float* candv = pj + J;                         // [2][G][RF]
   int* candi = reinterpret_cast<int*>(candv + 2 * G * RNNT_RF);   // [2][G][RF]
-  unsigned long long* bar = bars + (size_t)utt * 16;
+  unsigned long long* flags = bars + (size_t)utt * RG_MAXG;   // [G] barrier epochs, one word per workgroup
   // LDS: x vector, z block, partial sums, pred_ffn output, decisions
   float* x = lds;                                // [max(E, H) + H]
   float* z = x + (max(E, H) + H);                // [RF][J]
@@ -348,7 +364,7 @@ __global__ __launch_bounds__(RG_NT) void rnnt_grid_kernel(RnntDev w, RnntGrid gw
   int* dec = reinterpret_cast<int*>(red + RG_NT * RNNT_RF);   // [RF]
   int* lflag = dec + RNNT_RF;
   unsigned long long epoch = 0;
-  auto sync = [&]() { return rg_barrier(bar, ++epoch * (unsigned long long)G, err, lflag); };
+  auto sync = [&]() { return rg_barrier(flags, G, part, ++epoch, err, lflag); };
 
   int cur = 0;   // committed state slot (zero-initialised by the host)
   // the predictor for token `tok` from slot cur into slot cur ^ 1; pj -> lpj
@@ -717,7 +733,7 @@ void cfm_rnnt_destroy(cfm_rnnt* h) { delete h; }
 size_t cfm_rnnt_workspace_bytes(const cfm_rnnt* h, int32_t rows) {
   if (!h || rows <= 0) return 0;
   const size_t proj = ((size_t)rows * h->cfg.join_dim * sizeof(float) + 255) / 256 * 256;
-  return proj + (size_t)RG_MAXB * rnnt_grid_per_utt(h) * 4 + (size_t)RG_MAXB * 128 + 256;
+  return proj + (size_t)RG_MAXB * rnnt_grid_per_utt(h) * 4 + (size_t)RG_MAXB * RG_MAXG * 8 + 256;
 }
 
 cfm_status cfm_rnnt_set_option(cfm_rnnt* h, const char* key, int64_t value) {
@@ -771,9 +787,9 @@ cfm_status cfm_rnnt_greedy(const cfm_rnnt* h, const float* enc, int32_t rows, co
     char* gbase = (char*)ws + proj_b;
     float* scratch = (float*)gbase;
     unsigned long long* bars = (unsigned long long*)(gbase + (size_t)RG_MAXB * per * 4);
-    int* err = (int*)((char*)bars + (size_t)RG_MAXB * 128);
+    int* err = (int*)((char*)bars + (size_t)RG_MAXB * RG_MAXG * 8);
     if (hipMemsetAsync(scratch, 0, (size_t)B * per * 4, st) != hipSuccess ||
-        hipMemsetAsync(bars, 0, (size_t)RG_MAXB * 128 + 256, st) != hipSuccess)
+        hipMemsetAsync(bars, 0, (size_t)RG_MAXB * RG_MAXG * 8 + 256, st) != hipSuccess)
       return set_error(CFM_ERR_RUNTIME, "rnnt: workspace memset");
     const size_t glds = rnnt_grid_lds_bytes(h->w);
     if (glds > 64 * 1024 && hipFuncSetAttribute((const void*)rnnt_grid_kernel,
