@@ -248,10 +248,15 @@ CFM_DEV int sw128(int row, int ch) { return row * 128 + ((ch ^ ((row >> 1) & 7))
 #define ATTN_STORE16 1   // ring kernel output as 16-B stores after permlane swaps (A/B: 0 = 8-B stores)
 #endif
 
+// DG: the timing / A-B hooks of `diag` are compiled in (the production instantiation has none of their
+// uniform branches inside the tile loop, which would cut it into basic blocks the scheduler cannot
+// interleave across); NTI = W / 64 when W is whole 64-key tiles (1..5), else 0
+template <bool DG, int NTI>
 __global__ __launch_bounds__(512, 1) void chunk_attention_ring_kernel(
     const bf16* __restrict__ Q, const bf16* __restrict__ KV, int kv_rows, const bf16* __restrict__ P, int p_rows,
     const float* __restrict__ pos_u, const float* __restrict__ pos_v, const int32_t* __restrict__ desc, int n_chunks,
-    int H, int C, int W, bf16* __restrict__ out, int diag, int nch, int p_ld) {
+    int H, int C, int W, bf16* __restrict__ out, int diag_arg, int nch, int p_ld) {
+  const int diag = DG ? diag_arg : 0;
   const bool reuse_band = (diag & 15) != 5;   // diag 5: recompute band subtile 0 of every tile (A/B)
   __shared__ __attribute__((aligned(16))) char smem[RING_LDS];
   char* kr = smem;
@@ -389,180 +394,188 @@ __global__ __launch_bounds__(512, 1) void chunk_attention_ring_kernel(
           qv[s][e] = (bf16)((qf + (e < 4 ? v0_[e] : v1_[e - 4])) * 0.125f);
         }
       }
-      // interior chunks see the whole window (key_lo = 0, key_hi = W): no per-score mask
-      const bool need_mask = __builtin_amdgcn_readfirstlane((key_lo != (key_lo & ~15)) || ((key_hi - (key_lo & ~15)) & 63)) != 0;
-      const int jb = key_lo & ~15;
-      f32x4 S[5][4];
-      f32x4 band_next = (f32x4){0.f, 0.f, 0.f, 0.f};
-      float mx = -INFINITY;
+      // interior chunks of a window that is whole 64-key tiles (key_lo = 0, key_hi = W = 64 NTI): no
+      // per-score mask and no tile test -- the tile loop is one straight-line block; every other chunk
+      // (utterance edges, W % 64 != 0) runs the masked copy (tiles from key_lo & ~15, skipped past key_hi)
+      const bool whole = NTI > 0 && __builtin_amdgcn_readfirstlane(key_lo == 0 && key_hi == W) != 0;
+      auto body = [&](auto MASKc) {
+        constexpr bool MASK = decltype(MASKc)::value;
+        constexpr int NTT = MASK ? 5 : (NTI > 0 ? NTI : 1);
+        const int jb = MASK ? (key_lo & ~15) : 0;
+        f32x4 S[NTT][4];
+        f32x4 band_next = (f32x4){0.f, 0.f, 0.f, 0.f};
+        float mx = -INFINITY;
 #pragma unroll
-      for (int t = 0; t < 5; ++t) {
-        const int j0 = jb + 64 * t;
-        if (j0 >= key_hi) {
+        for (int t = 0; t < NTT; ++t) {
+          const int j0 = jb + 64 * t;
+          if (MASK && j0 >= key_hi) {
 #pragma unroll
-          for (int st = 0; st < 4; ++st) S[t][st] = (f32x4){-INFINITY, -INFINITY, -INFINITY, -INFINITY};
-          continue;
-        }
-        // the band first: its skewed values (bf16, through the per-wave scratch) become the C
-        // operand of the score MFMAs, so S = K.(q+u) + band costs no VALU add
-        bf16x8 kf[4][2], pf[5][2];
-        const int kb0 = p_base - i0 - 15 + j0;
-        // band subtile 0 of tile t is subtile 4 of tile t - 1 (P rows kb0 .. kb0 + 15, 64 rows on):
-        // carried in registers (tiles past key_hi are skipped only at the end, so tile t - 1 ran)
-        const bool carry = t > 0 && reuse_band;
-#pragma unroll
-        for (int pt = 0; pt < 5; ++pt) {
-          if (pt == 0 && carry) continue;
-          const char* pb_ = pl + (kb0 + 16 * pt) * 128;
-#pragma unroll
-          for (int s = 0; s < 2; ++s) pf[pt][s] = *reinterpret_cast<const bf16x8*>(pb_ + frag_lane[s]);
-        }
-#pragma unroll
-        for (int st = 0; st < 4; ++st) {
-          const char* kb_ = kr + ring16(j0 + 16 * st) * 128;
-#pragma unroll
-          for (int s = 0; s < 2; ++s) kf[st][s] = *reinterpret_cast<const bf16x8*>(kb_ + frag_lane[s]);
-        }
-        // band^T[P row kb0 + 16pt + 4g + rr][query fr], pt = 0..4 (80 rows for 64 keys + 15 skew); the
-        // two 32-key halves use subtiles 0-2 and 2-4 -> scratch[query][band pos] (16 x 48 bf16 per wave)
-        f32x4 band[5];
-#pragma unroll
-        for (int pt = 0; pt < 5; ++pt) {
-          if (pt == 0 && carry) {
-            band[0] = band_next;
+            for (int st = 0; st < 4; ++st) S[t][st] = (f32x4){-INFINITY, -INFINITY, -INFINITY, -INFINITY};
             continue;
           }
-          f32x4 a = (f32x4){0.f, 0.f, 0.f, 0.f};
+          // the band first: its skewed values (bf16, through the per-wave scratch) become the C
+          // operand of the score MFMAs, so S = K.(q+u) + band costs no VALU add
+          bf16x8 kf[4][2], pf[5][2];
+          const int kb0 = p_base - i0 - 15 + j0;
+          // band subtile 0 of tile t is subtile 4 of tile t - 1 (P rows kb0 .. kb0 + 15, 64 rows on):
+          // carried in registers (tiles past key_hi are skipped only at the end, so tile t - 1 ran)
+          const bool carry = t > 0 && reuse_band;
 #pragma unroll
-          for (int s = 0; s < 2; ++s) a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pf[pt][s], qv[s], a, 0, 0, 0);
-          band[pt] = a;
-        }
-        band_next = band[4];
+          for (int pt = 0; pt < 5; ++pt) {
+            if (pt == 0 && carry) continue;
+            const char* pb_ = pl + (kb0 + 16 * pt) * 128;
 #pragma unroll
-        for (int hh = 0; hh < 2; ++hh) {
-#pragma unroll
-          for (int pt = 0; pt < 3; ++pt) {
-            const f32x4 a = band[2 * hh + pt];
-            // rel_shift by the reshape trick: row fr is written at pitch 49 (+1) and read back at
-            // pitch 48, so query fr's band for key jj starts 16 - fr elements later: the reads
-            // are aligned 8-B vectors (4 keys), the writes 2-B aligned, as four ds_write_b16
-            const unsigned waddr = scr_base + 2u * (unsigned)(fr * SCR_PITCH + 1 + 16 * pt + 4 * g);
-            const unsigned lo = pack_bf16x2_a(a[0], a[1]), hi = pack_bf16x2_a(a[2], a[3]);
-            if (diag & 16)   // A/B: one unaligned ds_write_b64 (replayed by the LDS)
-              asm volatile("ds_write_b64 %0, %1" ::"v"(waddr), "v"((u32x2_a){lo, hi}) : "memory");
-            else
-              lds_store_4bf16_a2(waddr, lo, hi);
+            for (int s = 0; s < 2; ++s) pf[pt][s] = *reinterpret_cast<const bf16x8*>(pb_ + frag_lane[s]);
           }
-          // band of (query fr, key j0+32hh+16st2+4g+rr) = scratch[fr][16st2 + 4g + rr + 15 - fr]
-          typedef bf16 bf16x4 __attribute__((ext_vector_type(4)));
-          bf16x4 bdv4[2];
 #pragma unroll
-          for (int st2 = 0; st2 < 2; ++st2)
-            asm volatile("ds_read_b64 %0, %1"
-                         : "=v"(bdv4[st2])
-                         : "v"(scr_base + 2u * (unsigned)(fr * (SCR_PITCH - 1) + 16 + 16 * st2 + 4 * g))
-                         : "memory");
-          asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(bdv4[0]), "+v"(bdv4[1])::"memory");
-          // S^T[key 16st + 4g + rr][query fr] = band + K.(q+u)
+          for (int st = 0; st < 4; ++st) {
+            const char* kb_ = kr + ring16(j0 + 16 * st) * 128;
 #pragma unroll
-          for (int st2 = 0; st2 < 2; ++st2) {
-            const int st = 2 * hh + st2;
-            f32x4 a = (f32x4){(float)bdv4[st2][0], (float)bdv4[st2][1], (float)bdv4[st2][2], (float)bdv4[st2][3]};
+            for (int s = 0; s < 2; ++s) kf[st][s] = *reinterpret_cast<const bf16x8*>(kb_ + frag_lane[s]);
+          }
+          // band^T[P row kb0 + 16pt + 4g + rr][query fr], pt = 0..4 (80 rows for 64 keys + 15 skew); the
+          // two 32-key halves use subtiles 0-2 and 2-4 -> scratch[query][band pos] (16 x 48 bf16 per wave)
+          f32x4 band[5];
 #pragma unroll
-            for (int s = 0; s < 2; ++s) a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[st][s], qu[s], a, 0, 0, 0);
-            S[t][st] = a;
+          for (int pt = 0; pt < 5; ++pt) {
+            if (pt == 0 && carry) {
+              band[0] = band_next;
+              continue;
+            }
+            f32x4 a = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int s = 0; s < 2; ++s) a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pf[pt][s], qv[s], a, 0, 0, 0);
+            band[pt] = a;
+          }
+          band_next = band[4];
+#pragma unroll
+          for (int hh = 0; hh < 2; ++hh) {
+#pragma unroll
+            for (int pt = 0; pt < 3; ++pt) {
+              const f32x4 a = band[2 * hh + pt];
+              // rel_shift by the reshape trick: row fr is written at pitch 49 (+1) and read back at
+              // pitch 48, so query fr's band for key jj starts 16 - fr elements later: the reads
+              // are aligned 8-B vectors (4 keys), the writes 2-B aligned, as four ds_write_b16
+              const unsigned waddr = scr_base + 2u * (unsigned)(fr * SCR_PITCH + 1 + 16 * pt + 4 * g);
+              const unsigned lo = pack_bf16x2_a(a[0], a[1]), hi = pack_bf16x2_a(a[2], a[3]);
+              if (diag & 16)   // A/B: one unaligned ds_write_b64 (replayed by the LDS)
+                asm volatile("ds_write_b64 %0, %1" ::"v"(waddr), "v"((u32x2_a){lo, hi}) : "memory");
+              else
+                lds_store_4bf16_a2(waddr, lo, hi);
+            }
+            // band of (query fr, key j0+32hh+16st2+4g+rr) = scratch[fr][16st2 + 4g + rr + 15 - fr]
+            typedef bf16 bf16x4 __attribute__((ext_vector_type(4)));
+            bf16x4 bdv4[2];
+#pragma unroll
+            for (int st2 = 0; st2 < 2; ++st2)
+              asm volatile("ds_read_b64 %0, %1"
+                           : "=v"(bdv4[st2])
+                           : "v"(scr_base + 2u * (unsigned)(fr * (SCR_PITCH - 1) + 16 + 16 * st2 + 4 * g))
+                           : "memory");
+            asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(bdv4[0]), "+v"(bdv4[1])::"memory");
+            // S^T[key 16st + 4g + rr][query fr] = band + K.(q+u)
+#pragma unroll
+            for (int st2 = 0; st2 < 2; ++st2) {
+              const int st = 2 * hh + st2;
+              f32x4 a = (f32x4){(float)bdv4[st2][0], (float)bdv4[st2][1], (float)bdv4[st2][2], (float)bdv4[st2][3]};
+#pragma unroll
+              for (int s = 0; s < 2; ++s) a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[st][s], qu[s], a, 0, 0, 0);
+              S[t][st] = a;
+            }
+          }
+          if constexpr (MASK) {
+#pragma unroll
+            for (int st = 0; st < 4; ++st)
+#pragma unroll
+              for (int rr = 0; rr < 4; ++rr) {
+                const int j = j0 + 16 * st + 4 * g + rr;
+                float sv = S[t][st][rr];
+                if (j < key_lo || j >= key_hi) sv = -INFINITY;
+                S[t][st][rr] = sv;
+                mx = fmaxf(mx, sv);
+              }
+          } else {
+#pragma unroll
+            for (int st = 0; st < 4; ++st)
+#pragma unroll
+              for (int rr = 0; rr < 4; ++rr) mx = fmaxf(mx, S[t][st][rr]);
           }
         }
-        if (need_mask) {
+        // ---- exact softmax per query (lanes fr, fr+16, fr+32, fr+48 share a query)
+        mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+        if (mx == -INFINITY) mx = 0.f;   // fully masked query: every p = 0, output 0 (reference: NaN -> 0)
+        const float mxl = mx * 1.4426950408889634f;
+#pragma unroll
+        for (int t = 0; t < NTT; ++t)
 #pragma unroll
           for (int st = 0; st < 4; ++st)
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr) S[t][st][rr] = __builtin_amdgcn_exp2f(fmaf(S[t][st][rr], 1.4426950408889634f, -mxl));
+        // ---- O^T[dim 16nt + 4g + rr][query fr] = sum_keys V^T . P^T (key order permuted, same for both);
+        // the softmax denominator as a fifth MFMA against a constant "ones" row (row 0 of an A
+        // fragment held in registers): l = sum over keys of the bf16 p the numerator uses, and no
+        // VALU add per score
+        f32x4 O[4], Ol = (f32x4){0.f, 0.f, 0.f, 0.f};
+        const bf16 one_or_zero = (bf16)(fr == 0 ? 1.f : 0.f);
+        const bf16x8 ones = (bf16x8){one_or_zero, one_or_zero, one_or_zero, one_or_zero,
+                                     one_or_zero, one_or_zero, one_or_zero, one_or_zero};
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) O[nt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int t = 0; t < NTT; ++t) {
+          const int j0 = jb + 64 * t;
+          if ((MASK && j0 >= key_hi) || (diag & 15) == 3) continue;
+#pragma unroll
+          for (int s = 0; s < 2; ++s) {
+            bf16x8 pb;
 #pragma unroll
             for (int rr = 0; rr < 4; ++rr) {
-              const int j = j0 + 16 * st + 4 * g + rr;
-              float sv = S[t][st][rr];
-              if (j < key_lo || j >= key_hi) sv = -INFINITY;
-              S[t][st][rr] = sv;
-              mx = fmaxf(mx, sv);
+              pb[rr] = (bf16)S[t][2 * s][rr];
+              pb[4 + rr] = (bf16)S[t][2 * s + 1][rr];
             }
-        } else {
+            const char* va_ = vt + vt_lane + ring16(j0 + 32 * s) * 2;
+            const char* vb_ = vt + vt_lane + ring16(j0 + 32 * s + 16) * 2;
 #pragma unroll
-          for (int st = 0; st < 4; ++st)
-#pragma unroll
-            for (int rr = 0; rr < 4; ++rr) mx = fmaxf(mx, S[t][st][rr]);
-        }
-      }
-      // ---- exact softmax per query (lanes fr, fr+16, fr+32, fr+48 share a query)
-      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      if (mx == -INFINITY) mx = 0.f;   // fully masked query: every p = 0, output 0 (reference: NaN -> 0)
-      const float mxl = mx * 1.4426950408889634f;
-#pragma unroll
-      for (int t = 0; t < 5; ++t)
-#pragma unroll
-        for (int st = 0; st < 4; ++st)
-#pragma unroll
-          for (int rr = 0; rr < 4; ++rr) S[t][st][rr] = __builtin_amdgcn_exp2f(fmaf(S[t][st][rr], 1.4426950408889634f, -mxl));
-      // ---- O^T[dim 16nt + 4g + rr][query fr] = sum_keys V^T . P^T (key order permuted, same for both);
-      // the softmax denominator as a fifth MFMA against a constant "ones" row (row 0 of an A
-      // fragment held in registers): l = sum over keys of the bf16 p the numerator uses, and no
-      // VALU add per score
-      f32x4 O[4], Ol = (f32x4){0.f, 0.f, 0.f, 0.f};
-      const bf16 one_or_zero = (bf16)(fr == 0 ? 1.f : 0.f);
-      const bf16x8 ones = (bf16x8){one_or_zero, one_or_zero, one_or_zero, one_or_zero,
-                                   one_or_zero, one_or_zero, one_or_zero, one_or_zero};
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt) O[nt] = (f32x4){0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int t = 0; t < 5; ++t) {
-        const int j0 = jb + 64 * t;
-        if (j0 >= key_hi || (diag & 15) == 3) continue;
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-          bf16x8 pb;
-#pragma unroll
-          for (int rr = 0; rr < 4; ++rr) {
-            pb[rr] = (bf16)S[t][2 * s][rr];
-            pb[4 + rr] = (bf16)S[t][2 * s + 1][rr];
+            for (int nt = 0; nt < 4; ++nt) {
+              typedef bf16 bf16x4 __attribute__((ext_vector_type(4)));
+              const bf16x4 lo = *reinterpret_cast<const bf16x4*>(va_ + 16 * nt * VT_PITCH_B);
+              const bf16x4 hi = *reinterpret_cast<const bf16x4*>(vb_ + 16 * nt * VT_PITCH_B);
+              const bf16x8 va = (bf16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+              O[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va, pb, O[nt], 0, 0, 0);
+            }
+            Ol = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pb, Ol, 0, 0, 0);
           }
-          const char* va_ = vt + vt_lane + ring16(j0 + 32 * s) * 2;
-          const char* vb_ = vt + vt_lane + ring16(j0 + 32 * s + 16) * 2;
-#pragma unroll
-          for (int nt = 0; nt < 4; ++nt) {
-            typedef bf16 bf16x4 __attribute__((ext_vector_type(4)));
-            const bf16x4 lo = *reinterpret_cast<const bf16x4*>(va_ + 16 * nt * VT_PITCH_B);
-            const bf16x4 hi = *reinterpret_cast<const bf16x4*>(vb_ + 16 * nt * VT_PITCH_B);
-            const bf16x8 va = (bf16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-            O[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va, pb, O[nt], 0, 0, 0);
-          }
-          Ol = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pb, Ol, 0, 0, 0);
         }
-      }
-      // row 0 of Ol^T (query fr) sits in register 0 of lane fr (g = 0)
-      const float l = __shfl(Ol[0], fr, 64);
-      const int qi = i0 + fr;
-      const bool live = qi < q_valid && l > 0.f;
-      const float inv = live ? 1.f / l : 0.f;
-      bf16* op = out + (size_t)(q_row0 + qi) * d + h * 64;
-#if ATTN_STORE16
-      // dim pairs (16 nt .. +15, 16 (nt+1) ..): one permlane16 swap per packed dword leaves lane g with
-      // 8 contiguous dims, so each query row leaves as two 64-B pieces (2 x 16-B stores per lane)
+        // row 0 of Ol^T (query fr) sits in register 0 of lane fr (g = 0)
+        const float l = __shfl(Ol[0], fr, 64);
+        const int qi = i0 + fr;
+        const bool live = qi < q_valid && l > 0.f;
+        const float inv = live ? 1.f / l : 0.f;
+        bf16* op = out + (size_t)(q_row0 + qi) * d + h * 64;
+  #if ATTN_STORE16
+        // dim pairs (16 nt .. +15, 16 (nt+1) ..): one permlane16 swap per packed dword leaves lane g with
+        // 8 contiguous dims, so each query row leaves as two 64-B pieces (2 x 16-B stores per lane)
 #pragma unroll
-      for (int pr = 0; pr < 2; ++pr) {
-        const unsigned x0 = pack_bf16x2_a(O[2 * pr][0] * inv, O[2 * pr][1] * inv), x1 = pack_bf16x2_a(O[2 * pr][2] * inv, O[2 * pr][3] * inv);
-        const unsigned y0 = pack_bf16x2_a(O[2 * pr + 1][0] * inv, O[2 * pr + 1][1] * inv),
-                       y1 = pack_bf16x2_a(O[2 * pr + 1][2] * inv, O[2 * pr + 1][3] * inv);
-        const auto r0 = __builtin_amdgcn_permlane16_swap(x0, y0, false, false);
-        const auto r1 = __builtin_amdgcn_permlane16_swap(x1, y1, false, false);
-        *reinterpret_cast<u32x4*>(op + 32 * pr + 16 * (g & 1) + 8 * (g >> 1)) = (u32x4){r0[0], r1[0], r0[1], r1[1]};
-      }
-#else
+        for (int pr = 0; pr < 2; ++pr) {
+          const unsigned x0 = pack_bf16x2_a(O[2 * pr][0] * inv, O[2 * pr][1] * inv), x1 = pack_bf16x2_a(O[2 * pr][2] * inv, O[2 * pr][3] * inv);
+          const unsigned y0 = pack_bf16x2_a(O[2 * pr + 1][0] * inv, O[2 * pr + 1][1] * inv),
+                         y1 = pack_bf16x2_a(O[2 * pr + 1][2] * inv, O[2 * pr + 1][3] * inv);
+          const auto r0 = __builtin_amdgcn_permlane16_swap(x0, y0, false, false);
+          const auto r1 = __builtin_amdgcn_permlane16_swap(x1, y1, false, false);
+          *reinterpret_cast<u32x4*>(op + 32 * pr + 16 * (g & 1) + 8 * (g >> 1)) = (u32x4){r0[0], r1[0], r0[1], r1[1]};
+        }
+  #else
 #pragma unroll
-      for (int nt = 0; nt < 4; ++nt) {
-        typedef bf16 bf16x4 __attribute__((ext_vector_type(4)));
-        *reinterpret_cast<bf16x4*>(op + 16 * nt + 4 * g) =
-            (bf16x4){(bf16)(O[nt][0] * inv), (bf16)(O[nt][1] * inv), (bf16)(O[nt][2] * inv), (bf16)(O[nt][3] * inv)};
-      }
-#endif
+        for (int nt = 0; nt < 4; ++nt) {
+          typedef bf16 bf16x4 __attribute__((ext_vector_type(4)));
+          *reinterpret_cast<bf16x4*>(op + 16 * nt + 4 * g) =
+              (bf16x4){(bf16)(O[nt][0] * inv), (bf16)(O[nt][1] * inv), (bf16)(O[nt][2] * inv), (bf16)(O[nt][3] * inv)};
+        }
+  #endif
+      };
+      if (whole) body(std::false_type{});
+      else body(std::true_type{});
     }
     // ---- the prefetched rows replace the first 2C rows of this pair's windows (no longer needed)
     __syncthreads();
@@ -587,8 +600,21 @@ int chunk_attention_masked_bf16(const bf16* q, const bf16* kv, int kv_rows, cons
   int nch = (int)(((long long)n_chunks * H + n_cu - 1) / n_cu);
   nch = max(NCH, (nch + 1) & ~1);
   const dim3 grid((n_chunks + nch - 1) / nch, H);
-  hipLaunchKernelGGL(chunk_attention_ring_kernel, grid, dim3(512), 0, st, q, kv, kv_rows, P, p_rows, pos_u, pos_v,
-                     desc, n_chunks, H, C, W, out, diag, nch, p_ld);
+#define RING_L(DG_, NT_)                                                                                             \
+  hipLaunchKernelGGL((chunk_attention_ring_kernel<DG_, NT_>), grid, dim3(512), 0, st, q, kv, kv_rows, P, p_rows, pos_u, \
+                     pos_v, desc, n_chunks, H, C, W, out, diag, nch, p_ld)
+  const int nti = W % 64 == 0 ? W / 64 : 0;
+  if (diag) {
+    if (nti == 5) RING_L(true, 5);
+    else RING_L(true, 0);
+  }
+  else if (nti == 5) RING_L(false, 5);
+  else if (nti == 4) RING_L(false, 4);
+  else if (nti == 3) RING_L(false, 3);
+  else if (nti == 2) RING_L(false, 2);
+  else if (nti == 1) RING_L(false, 1);
+  else RING_L(false, 0);
+#undef RING_L
   CFM_CHECK_LAUNCH();
   return 0;
 }

@@ -314,7 +314,9 @@ CFM_DEV void rg_matvec(const float4* __restrict__ Wb, int K, int n, const float*
   const int ks = RG_NT / np, jj = tid % np, s = tid / np;
   float4 acc = {0.f, 0.f, 0.f, 0.f};
   if (jj < n) {
-#pragma unroll 4
+    // 16 loads in flight per thread: after a barrier's acquire the slices come from the MALL / HBM,
+    // so the loop is latency-bound, not bandwidth-bound
+#pragma unroll 16
     for (int k = s; k < K; k += ks) {
       const float4 wv = Wb[(size_t)k * n + jj];
       const float xv = x[k];
@@ -444,7 +446,7 @@ __global__ __launch_bounds__(RG_NT) void rnnt_grid_kernel(RnntDev w, RnntGrid gw
 #pragma unroll
     for (int f = 0; f < RNNT_RF; ++f) acc[f] = make_float4(0.f, 0.f, 0.f, 0.f);
     if (jj < nv) {
-#pragma unroll 2
+#pragma unroll 8
       for (int k = sp; k < J; k += ks) {
         const float4 wv = wo[(size_t)k * nv + jj];
 #pragma unroll
