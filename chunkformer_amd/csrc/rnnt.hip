@@ -301,6 +301,26 @@ CFM_DEV bool rg_barrier(unsigned long long* flags, int G, int part, unsigned lon
   return *lflag != 0;
 }
 
+// Partial sums of the ks = NT / np threads (s, jj), tid = s * np + jj, down to one per column: xor
+// shuffles across the lanes of a wave that share jj (np < 64), then the 4 waves' (or, for np >= 64,
+// the ks) partials through LDS, summed in a fixed order by thread jj.  rg_parts(np) = partials left.
+CFM_DEV int rg_parts(int np) { return np < 64 ? RG_NT / 64 : RG_NT / np; }
+CFM_DEV float4 rg_wave_reduce(float4 v, int np) {
+  for (int o = np; o < 64; o <<= 1) {
+    v.x += __shfl_xor(v.x, o, 64);
+    v.y += __shfl_xor(v.y, o, 64);
+    v.z += __shfl_xor(v.z, o, 64);
+    v.w += __shfl_xor(v.w, o, 64);
+  }
+  return v;
+}
+// the LDS slot of this thread's reduced partial, or -1 when the thread holds none
+CFM_DEV int rg_slot(int np) {
+  const int tid = threadIdx.x, lane = tid & 63;
+  if (np >= 64) return tid;                             // slot q * np + jj with q = s
+  return lane < np ? (tid >> 6) * np + lane : -1;       // q = wave, jj = lane
+}
+
 // sums[jj] = sum_k Wb[k][jj] * x[k] for jj < n (Wb: this workgroup's [K][n] float4 slice), threads
 // (s, jj) = (tid / np, tid % np) with np = pow2 >= n: a wave reads whole consecutive rows of the
 // slice; the ks = NT / np partial sums are added in order through `red`.  fin(jj, sum) runs on the
@@ -326,11 +346,14 @@ CFM_DEV void rg_matvec(const float4* __restrict__ Wb, int K, int n, const float*
       acc.w = fmaf(wv.w, xv, acc.w);
     }
   }
-  red[tid] = acc;
+  acc = rg_wave_reduce(acc, np);
+  const int slot = rg_slot(np);
+  if (slot >= 0) red[slot] = acc;
   __syncthreads();
   if (tid < n) {
     float4 v = red[tid];
-    for (int q = 1; q < ks; ++q) {
+    const int parts = rg_parts(np);
+    for (int q = 1; q < parts; ++q) {
       const float4 o = red[tid + q * np];
       v.x += o.x; v.y += o.y; v.z += o.z; v.w += o.w;
     }
@@ -459,8 +482,14 @@ __global__ __launch_bounds__(RG_NT) void rnnt_grid_kernel(RnntDev w, RnntGrid gw
         }
       }
     }
+    {
+      const int slot = rg_slot(np);
 #pragma unroll
-    for (int f = 0; f < RNNT_RF; ++f) red[f * RG_NT + tid] = acc[f];
+      for (int f = 0; f < RNNT_RF; ++f) {
+        const float4 v = rg_wave_reduce(acc[f], np);
+        if (slot >= 0) red[f * RG_NT + slot] = v;
+      }
+    }
     __syncthreads();
     // (frame, column group) sums in order, then each frame's best over this workgroup's columns
     float* sv = z;   // z is consumed: reuse as [RF][np] best values / ids
@@ -468,7 +497,8 @@ __global__ __launch_bounds__(RG_NT) void rnnt_grid_kernel(RnntDev w, RnntGrid gw
     for (int e = tid; e < RNNT_RF * nv; e += RG_NT) {
       const int f = e / nv, c = e - f * nv;
       float4 v = red[f * RG_NT + c];
-      for (int q = 1; q < ks; ++q) {
+      const int parts = rg_parts(np);
+      for (int q = 1; q < parts; ++q) {
         const float4 o = red[f * RG_NT + c + q * np];
         v.x += o.x; v.y += o.y; v.z += o.z; v.w += o.w;
       }
