@@ -715,176 +715,185 @@ __global__ __launch_bounds__(512, 1) void full_attention_bf16_kernel(
 
   const int i0 = wq * 16;
   const bool active = has && i0 < nq;
-  f32x4 S[FA_NT][4];
-  float l = 0.f;
-  const int key8 = (fr >> 1) & 7;
-  const int frag_lane[2] = {fr * 128 + ((g ^ key8) << 4), fr * 128 + (((4 + g) ^ key8) << 4)};
-  if (active) {
-    bf16x8 qraw[2];
-    {
-      const bf16* qp = Q + ((size_t)q_row0 + min(i0 + fr, nq - 1)) * d + h * 64;
-      qraw[0] = *reinterpret_cast<const bf16x8*>(qp + 8 * g);
-      qraw[1] = *reinterpret_cast<const bf16x8*>(qp + 32 + 8 * g);
-    }
-    bf16x8 qu[2], qv[2];
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const f32x4 u0 = *reinterpret_cast<const f32x4*>(uv + s * 32 + 8 * g);
-      const f32x4 u1 = *reinterpret_cast<const f32x4*>(uv + s * 32 + 8 * g + 4);
-      const f32x4 v0_ = *reinterpret_cast<const f32x4*>(uv + 64 + s * 32 + 8 * g);
-      const f32x4 v1_ = *reinterpret_cast<const f32x4*>(uv + 64 + s * 32 + 8 * g + 4);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const float qf = (float)qraw[s][e];   // 1/sqrt(64) = 2^-3 folded in: exact in bf16 and f32
-        qu[s][e] = (bf16)((qf + (e < 4 ? u0[e] : u1[e - 4])) * 0.125f);
-        qv[s][e] = (bf16)((qf + (e < 4 ? v0_[e] : v1_[e - 4])) * 0.125f);
+  // the block's key tiles (one utterance: uniform), as a compile-time count: the tile loops are
+  // straight-line code without per-tile skip branches; only the last tile can need the key mask
+  const int ntv = __builtin_amdgcn_readfirstlane((key_hi + 63) >> 6);
+  auto body = [&](auto NTVc) {
+    constexpr int NTV = decltype(NTVc)::value;
+    f32x4 S[NTV][4];
+    float l = 0.f;
+    const int key8 = (fr >> 1) & 7;
+    const int frag_lane[2] = {fr * 128 + ((g ^ key8) << 4), fr * 128 + (((4 + g) ^ key8) << 4)};
+    if (active) {
+      bf16x8 qraw[2];
+      {
+        const bf16* qp = Q + ((size_t)q_row0 + min(i0 + fr, nq - 1)) * d + h * 64;
+        qraw[0] = *reinterpret_cast<const bf16x8*>(qp + 8 * g);
+        qraw[1] = *reinterpret_cast<const bf16x8*>(qp + 32 + 8 * g);
       }
-    }
-    f32x4 band_next = (f32x4){0.f, 0.f, 0.f, 0.f};
-    float mx = -INFINITY;
-    // band rows kb0 = p_base - i0 - 15 + j0 .. +79 -> LDS row kb0 - pb0
-    const int lbase = p_base - i0 - 15 - pb0;
+      bf16x8 qu[2], qv[2];
 #pragma unroll
-    for (int t = 0; t < FA_NT; ++t) {
-      const int j0 = 64 * t;
-      if (j0 >= key_hi) {
+      for (int s = 0; s < 2; ++s) {
+        const f32x4 u0 = *reinterpret_cast<const f32x4*>(uv + s * 32 + 8 * g);
+        const f32x4 u1 = *reinterpret_cast<const f32x4*>(uv + s * 32 + 8 * g + 4);
+        const f32x4 v0_ = *reinterpret_cast<const f32x4*>(uv + 64 + s * 32 + 8 * g);
+        const f32x4 v1_ = *reinterpret_cast<const f32x4*>(uv + 64 + s * 32 + 8 * g + 4);
 #pragma unroll
-        for (int st = 0; st < 4; ++st) S[t][st] = (f32x4){-INFINITY, -INFINITY, -INFINITY, -INFINITY};
-        continue;
-      }
-      // the band first; its skewed values are the C operand of the score MFMAs (no VALU add)
-      f32x4 band[5];
-#pragma unroll
-      for (int pt = 0; pt < 5; ++pt) {
-        if (pt == 0 && t > 0) {   // subtile 0 of this tile is subtile 4 of the previous one
-          band[0] = band_next;
-          continue;
+        for (int e = 0; e < 8; ++e) {
+          const float qf = (float)qraw[s][e];   // 1/sqrt(64) = 2^-3 folded in: exact in bf16 and f32
+          qu[s][e] = (bf16)((qf + (e < 4 ? u0[e] : u1[e - 4])) * 0.125f);
+          qv[s][e] = (bf16)((qf + (e < 4 ? v0_[e] : v1_[e - 4])) * 0.125f);
         }
-        f32x4 a = (f32x4){0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int s = 0; s < 2; ++s)
-          a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-              *reinterpret_cast<const bf16x8*>(pl + (lbase + j0 + 16 * pt) * 128 + frag_lane[s]), qv[s], a, 0, 0, 0);
-        band[pt] = a;
       }
-      band_next = band[4];
-      const bool tmask = j0 + 64 > key_hi;   // the last tile of a short utterance
+      f32x4 band_next = (f32x4){0.f, 0.f, 0.f, 0.f};
+      float mx = -INFINITY;
+      // band rows kb0 = p_base - i0 - 15 + j0 .. +79 -> LDS row kb0 - pb0
+      const int lbase = p_base - i0 - 15 - pb0;
 #pragma unroll
-      for (int hh = 0; hh < 2; ++hh) {
+      for (int t = 0; t < NTV; ++t) {
+        const int j0 = 64 * t;
+        // the band first; its skewed values are the C operand of the score MFMAs (no VALU add)
+        f32x4 band[5];
 #pragma unroll
-        for (int pt = 0; pt < 3; ++pt) {
-          const f32x4 a = band[2 * hh + pt];
-          const unsigned waddr = scr_base + 2u * (unsigned)(fr * SCR_PITCH + 1 + 16 * pt + 4 * g);
-          lds_store_4bf16_a2(waddr, pack_bf16x2_a(a[0], a[1]), pack_bf16x2_a(a[2], a[3]));
-        }
-        typedef bf16 bf16x4 __attribute__((ext_vector_type(4)));
-        bf16x4 bdv4[2];
-#pragma unroll
-        for (int st2 = 0; st2 < 2; ++st2)
-          asm volatile("ds_read_b64 %0, %1"
-                       : "=v"(bdv4[st2])
-                       : "v"(scr_base + 2u * (unsigned)(fr * (SCR_PITCH - 1) + 16 + 16 * st2 + 4 * g))
-                       : "memory");
-        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(bdv4[0]), "+v"(bdv4[1])::"memory");
-#pragma unroll
-        for (int st2 = 0; st2 < 2; ++st2) {
-          const int st = 2 * hh + st2;
-          f32x4 a = (f32x4){(float)bdv4[st2][0], (float)bdv4[st2][1], (float)bdv4[st2][2], (float)bdv4[st2][3]};
+        for (int pt = 0; pt < 5; ++pt) {
+          if (pt == 0 && t > 0) {   // subtile 0 of this tile is subtile 4 of the previous one
+            band[0] = band_next;
+            continue;
+          }
+          f32x4 a = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
           for (int s = 0; s < 2; ++s)
             a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                *reinterpret_cast<const bf16x8*>(kr + (j0 + 16 * st) * 128 + frag_lane[s]), qu[s], a, 0, 0, 0);
+                *reinterpret_cast<const bf16x8*>(pl + (lbase + j0 + 16 * pt) * 128 + frag_lane[s]), qv[s], a, 0, 0, 0);
+          band[pt] = a;
+        }
+        band_next = band[4];
+        const bool tmask = t == NTV - 1 && j0 + 64 > key_hi;   // only the last valid tile can be partial
 #pragma unroll
-          for (int rr = 0; rr < 4; ++rr) {
-            float sv = a[rr];
-            if (tmask && j0 + 32 * hh + 16 * st2 + 4 * g + rr >= key_hi) sv = -INFINITY;
-            S[t][st][rr] = sv;
-            mx = fmaxf(mx, sv);
+        for (int hh = 0; hh < 2; ++hh) {
+#pragma unroll
+          for (int pt = 0; pt < 3; ++pt) {
+            const f32x4 a = band[2 * hh + pt];
+            const unsigned waddr = scr_base + 2u * (unsigned)(fr * SCR_PITCH + 1 + 16 * pt + 4 * g);
+            lds_store_4bf16_a2(waddr, pack_bf16x2_a(a[0], a[1]), pack_bf16x2_a(a[2], a[3]));
+          }
+          typedef bf16 bf16x4 __attribute__((ext_vector_type(4)));
+          bf16x4 bdv4[2];
+#pragma unroll
+          for (int st2 = 0; st2 < 2; ++st2)
+            asm volatile("ds_read_b64 %0, %1"
+                         : "=v"(bdv4[st2])
+                         : "v"(scr_base + 2u * (unsigned)(fr * (SCR_PITCH - 1) + 16 + 16 * st2 + 4 * g))
+                         : "memory");
+          asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(bdv4[0]), "+v"(bdv4[1])::"memory");
+#pragma unroll
+          for (int st2 = 0; st2 < 2; ++st2) {
+            const int st = 2 * hh + st2;
+            f32x4 a = (f32x4){(float)bdv4[st2][0], (float)bdv4[st2][1], (float)bdv4[st2][2], (float)bdv4[st2][3]};
+#pragma unroll
+            for (int s = 0; s < 2; ++s)
+              a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                  *reinterpret_cast<const bf16x8*>(kr + (j0 + 16 * st) * 128 + frag_lane[s]), qu[s], a, 0, 0, 0);
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr) {
+              float sv = a[rr];
+              if (tmask && j0 + 32 * hh + 16 * st2 + 4 * g + rr >= key_hi) sv = -INFINITY;
+              S[t][st][rr] = sv;
+              mx = fmaxf(mx, sv);
+            }
           }
         }
       }
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      if (mx == -INFINITY) mx = 0.f;   // no valid key: every p = 0, output 0
+      const float mxl = mx * 1.4426950408889634f;
+#pragma unroll
+      for (int t = 0; t < NTV; ++t)
+#pragma unroll
+        for (int st = 0; st < 4; ++st)
+#pragma unroll
+          for (int rr = 0; rr < 4; ++rr) {
+            const float p = __builtin_amdgcn_exp2f(fmaf(S[t][st][rr], 1.4426950408889634f, -mxl));
+            S[t][st][rr] = p;
+            l += p;
+          }
+      l += __shfl_xor(l, 16, 64);
+      l += __shfl_xor(l, 32, 64);
     }
-    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    if (mx == -INFINITY) mx = 0.f;   // no valid key: every p = 0, output 0
-    const float mxl = mx * 1.4426950408889634f;
+    // ---- phase 2: V^T over the K region (every wave is past its K reads)
+    __syncthreads();
+    typedef bf16 bf16x2_ __attribute__((ext_vector_type(2)));
 #pragma unroll
-    for (int t = 0; t < FA_NT; ++t)
+    for (int it = 0; it < VIT; ++it) {
+      const int idx = tid + 512 * it, pr = idx % (FA_KEYS / 2), ch = idx / (FA_KEYS / 2), j = 2 * pr;
+      const bf16x8 a = __builtin_bit_cast(bf16x8, sv0[it]), b = __builtin_bit_cast(bf16x8, sv1[it]);
 #pragma unroll
-      for (int st = 0; st < 4; ++st)
+      for (int e = 0; e < 8; ++e) *reinterpret_cast<bf16x2_*>(vt + (ch * 8 + e) * FA_VT_PITCH + j * 2) = (bf16x2_){a[e], b[e]};
+    }
+    __syncthreads();
+    if (!active) return;
+    const int vt_lane = fr * FA_VT_PITCH + 8 * g;
+    f32x4 O[4];
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) O[nt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int t = 0; t < NTV; ++t) {
+      const int j0 = 64 * t;
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        bf16x8 pb;
 #pragma unroll
         for (int rr = 0; rr < 4; ++rr) {
-          const float p = __builtin_amdgcn_exp2f(fmaf(S[t][st][rr], 1.4426950408889634f, -mxl));
-          S[t][st][rr] = p;
-          l += p;
+          pb[rr] = (bf16)S[t][2 * s][rr];
+          pb[4 + rr] = (bf16)S[t][2 * s + 1][rr];
         }
-    l += __shfl_xor(l, 16, 64);
-    l += __shfl_xor(l, 32, 64);
-  }
-  // ---- phase 2: V^T over the K region (every wave is past its K reads)
-  __syncthreads();
-  typedef bf16 bf16x2_ __attribute__((ext_vector_type(2)));
+        const char* va_ = vt + vt_lane + (j0 + 32 * s) * 2;
+        const char* vb_ = vt + vt_lane + (j0 + 32 * s + 16) * 2;
 #pragma unroll
-  for (int it = 0; it < VIT; ++it) {
-    const int idx = tid + 512 * it, pr = idx % (FA_KEYS / 2), ch = idx / (FA_KEYS / 2), j = 2 * pr;
-    const bf16x8 a = __builtin_bit_cast(bf16x8, sv0[it]), b = __builtin_bit_cast(bf16x8, sv1[it]);
-#pragma unroll
-    for (int e = 0; e < 8; ++e) *reinterpret_cast<bf16x2_*>(vt + (ch * 8 + e) * FA_VT_PITCH + j * 2) = (bf16x2_){a[e], b[e]};
-  }
-  __syncthreads();
-  if (!active) return;
-  const int vt_lane = fr * FA_VT_PITCH + 8 * g;
-  f32x4 O[4];
-#pragma unroll
-  for (int nt = 0; nt < 4; ++nt) O[nt] = (f32x4){0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int t = 0; t < FA_NT; ++t) {
-    const int j0 = 64 * t;
-    if (j0 >= key_hi) continue;
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      bf16x8 pb;
-#pragma unroll
-      for (int rr = 0; rr < 4; ++rr) {
-        pb[rr] = (bf16)S[t][2 * s][rr];
-        pb[4 + rr] = (bf16)S[t][2 * s + 1][rr];
-      }
-      const char* va_ = vt + vt_lane + (j0 + 32 * s) * 2;
-      const char* vb_ = vt + vt_lane + (j0 + 32 * s + 16) * 2;
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt) {
-        typedef bf16 bf16x4 __attribute__((ext_vector_type(4)));
-        const bf16x4 lo = *reinterpret_cast<const bf16x4*>(va_ + 16 * nt * FA_VT_PITCH);
-        const bf16x4 hi = *reinterpret_cast<const bf16x4*>(vb_ + 16 * nt * FA_VT_PITCH);
-        const bf16x8 va = (bf16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        O[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va, pb, O[nt], 0, 0, 0);
+        for (int nt = 0; nt < 4; ++nt) {
+          typedef bf16 bf16x4 __attribute__((ext_vector_type(4)));
+          const bf16x4 lo = *reinterpret_cast<const bf16x4*>(va_ + 16 * nt * FA_VT_PITCH);
+          const bf16x4 hi = *reinterpret_cast<const bf16x4*>(vb_ + 16 * nt * FA_VT_PITCH);
+          const bf16x8 va = (bf16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          O[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va, pb, O[nt], 0, 0, 0);
+        }
       }
     }
-  }
-  const int qi = i0 + fr;
-  const bool live = qi < q_valid && l > 0.f;
-  const float inv = live ? 1.f / l : 0.f;
-  bf16* op = out + ((size_t)q_row0 + qi) * d + h * 64;
+    const int qi = i0 + fr;
+    const bool live = qi < q_valid && l > 0.f;
+    const float inv = live ? 1.f / l : 0.f;
+    bf16* op = out + ((size_t)q_row0 + qi) * d + h * 64;
 #if ATTN_STORE16
-  // as the ring kernel: 16-B stores after permlane16 swaps (every lane takes part in the swaps)
+    // as the ring kernel: 16-B stores after permlane16 swaps (every lane takes part in the swaps)
 #pragma unroll
-  for (int pr = 0; pr < 2; ++pr) {
-    const unsigned x0 = pack_bf16x2_a(O[2 * pr][0] * inv, O[2 * pr][1] * inv), x1 = pack_bf16x2_a(O[2 * pr][2] * inv, O[2 * pr][3] * inv);
-    const unsigned y0 = pack_bf16x2_a(O[2 * pr + 1][0] * inv, O[2 * pr + 1][1] * inv),
-                   y1 = pack_bf16x2_a(O[2 * pr + 1][2] * inv, O[2 * pr + 1][3] * inv);
-    const auto r0 = __builtin_amdgcn_permlane16_swap(x0, y0, false, false);
-    const auto r1 = __builtin_amdgcn_permlane16_swap(x1, y1, false, false);
-    if (qi < nq) *reinterpret_cast<u32x4*>(op + 32 * pr + 16 * (g & 1) + 8 * (g >> 1)) = (u32x4){r0[0], r1[0], r0[1], r1[1]};
-  }
+    for (int pr = 0; pr < 2; ++pr) {
+      const unsigned x0 = pack_bf16x2_a(O[2 * pr][0] * inv, O[2 * pr][1] * inv), x1 = pack_bf16x2_a(O[2 * pr][2] * inv, O[2 * pr][3] * inv);
+      const unsigned y0 = pack_bf16x2_a(O[2 * pr + 1][0] * inv, O[2 * pr + 1][1] * inv),
+                     y1 = pack_bf16x2_a(O[2 * pr + 1][2] * inv, O[2 * pr + 1][3] * inv);
+      const auto r0 = __builtin_amdgcn_permlane16_swap(x0, y0, false, false);
+      const auto r1 = __builtin_amdgcn_permlane16_swap(x1, y1, false, false);
+      if (qi < nq) *reinterpret_cast<u32x4*>(op + 32 * pr + 16 * (g & 1) + 8 * (g >> 1)) = (u32x4){r0[0], r1[0], r0[1], r1[1]};
+    }
 #else
-  if (qi >= nq) return;
+    if (qi >= nq) return;
 #pragma unroll
-  for (int nt = 0; nt < 4; ++nt) {
-    typedef bf16 bf16x4 __attribute__((ext_vector_type(4)));
-    *reinterpret_cast<bf16x4*>(op + 16 * nt + 4 * g) =
-        (bf16x4){(bf16)(O[nt][0] * inv), (bf16)(O[nt][1] * inv), (bf16)(O[nt][2] * inv), (bf16)(O[nt][3] * inv)};
-  }
+    for (int nt = 0; nt < 4; ++nt) {
+      typedef bf16 bf16x4 __attribute__((ext_vector_type(4)));
+      *reinterpret_cast<bf16x4*>(op + 16 * nt + 4 * g) =
+          (bf16x4){(bf16)(O[nt][0] * inv), (bf16)(O[nt][1] * inv), (bf16)(O[nt][2] * inv), (bf16)(O[nt][3] * inv)};
+    }
 #endif
+  };
+  switch (ntv) {
+    case 0:   // (no key: tile 0 fully masked, output 0)
+    case 1: body(std::integral_constant<int, 1>{}); break;
+    case 2: body(std::integral_constant<int, 2>{}); break;
+    case 3: body(std::integral_constant<int, 3>{}); break;
+    case 4: body(std::integral_constant<int, 4>{}); break;
+    case 5: body(std::integral_constant<int, 5>{}); break;
+    default: body(std::integral_constant<int, FA_NT>{}); break;
+  }
 }
 
 // -1 when not eligible (T' > 384, dk != 64): the caller uses chunk_attention_kernel.  `nd` = the
