@@ -362,6 +362,12 @@ CFM_DEV void rg_matvec(const float4* __restrict__ Wb, int K, int n, const float*
   __syncthreads();
 }
 
+__host__ __device__ size_t rnnt_grid_lds_bytes(const RnntDev& w);
+
+// LDSW: the workgroup's weight slices are copied into LDS once (after the work area of
+// rnnt_grid_lds_bytes) and every emission's matrix-vector products read them there, not from the
+// MALL / HBM after each barrier's acquire
+template <bool LDSW>
 __global__ __launch_bounds__(RG_NT) void rnnt_grid_kernel(RnntDev w, RnntGrid gw, float* __restrict__ scratch,
                                                           int per_utt, unsigned long long* __restrict__ bars,
                                                           int* __restrict__ err, const float* __restrict__ enc_proj,
@@ -391,23 +397,53 @@ __global__ __launch_bounds__(RG_NT) void rnnt_grid_kernel(RnntDev w, RnntGrid gw
   unsigned long long epoch = 0;
   auto sync = [&]() { return rg_barrier(flags, G, part, ++epoch, err, lflag); };
 
+  // this workgroup's output ranges and weight slices
+  int u0, nu, pg0, pn, jg0, jn, v0, nv;
+  rg_range(H, G, part, u0, nu);
+  rg_range(P >> 2, G, part, pg0, pn);
+  rg_range(J >> 2, G, part, jg0, jn);
+  rg_range(w.Vp >> 2, G, part, v0, nv);
+  const float4* sl_wp = gw.wp + (size_t)H * pg0;
+  const float4* sl_wpj = gw.wpj + (size_t)P * jg0;
+  const float4* sl_wo = gw.wo + (size_t)J * v0;
+  float4* wcache = reinterpret_cast<float4*>(lds + rnnt_grid_lds_bytes(w) / 4);   // [layers][wp][wpj][wo]
+  if constexpr (LDSW) {
+    float4* c = wcache;
+    auto copy = [&](const float4* src, size_t n4) {
+      for (size_t i = tid; i < n4; i += RG_NT) c[i] = src[i];
+      c += n4;
+    };
+    int in = E;
+    for (int l = 0; l < nl; ++l) {
+      copy(gw.wg[l] + (size_t)(in + H) * u0, (size_t)(in + H) * nu);
+      in = H;
+    }
+    copy(sl_wp, (size_t)H * pn);
+    sl_wp = c - (size_t)H * pn;
+    copy(sl_wpj, (size_t)P * jn);
+    sl_wpj = c - (size_t)P * jn;
+    copy(sl_wo, (size_t)J * nv);
+    sl_wo = c - (size_t)J * nv;
+    __syncthreads();
+  }
+
   int cur = 0;   // committed state slot (zero-initialised by the host)
   // the predictor for token `tok` from slot cur into slot cur ^ 1; pj -> lpj
   auto predictor = [&](int tok) -> bool {
     int in = E;
+    const float4* wl = wcache;   // LDSW: layer l's slice follows layer l - 1's
     for (int l = 0; l < nl; ++l) {
       const float* src = l == 0 ? w.embed + (size_t)tok * E : hs + ((size_t)(cur ^ 1) * nl + (l - 1)) * H;
       for (int e = tid; e < in; e += RG_NT) x[e] = src[e];
       const float* hc = hs + ((size_t)cur * nl + l) * H;
       for (int e = tid; e < H; e += RG_NT) x[in + e] = hc[e];
       __syncthreads();
-      int u0, nu;
-      rg_range(H, G, part, u0, nu);
       float* cold = cs + ((size_t)cur * nl + l) * H;
       float* cnew = cs + ((size_t)(cur ^ 1) * nl + l) * H;
       float* hnew = hs + ((size_t)(cur ^ 1) * nl + l) * H;
       const float4* bq = gw.bg[l];
-      rg_matvec(gw.wg[l] + (size_t)(in + H) * u0, in + H, nu, x, red, [&](int jj, float4 a) {
+      if constexpr (!LDSW) wl = gw.wg[l] + (size_t)(in + H) * u0;
+      rg_matvec(wl, in + H, nu, x, red, [&](int jj, float4 a) {
         const int u = u0 + jj;
         const float4 b = bq[u];
         const float ig = sigm(a.x + b.x), fg = sigm(a.y + b.y), gg = tanhf(a.z + b.z), og = sigm(a.w + b.w);
@@ -416,16 +452,16 @@ __global__ __launch_bounds__(RG_NT) void rnnt_grid_kernel(RnntDev w, RnntGrid gw
         hnew[u] = og * tanhf(cv);
       });
       if (!sync()) return false;
+      wl += (size_t)(in + H) * nu;
       in = H;
     }
     {
       const float* ht = hs + ((size_t)(cur ^ 1) * nl + (nl - 1)) * H;
       for (int e = tid; e < H; e += RG_NT) x[e] = ht[e];
       __syncthreads();
-      int g0, n;
-      rg_range(P >> 2, G, part, g0, n);
+      const int g0 = pg0, n = pn;
       const float4* b4 = reinterpret_cast<const float4*>(w.bp);
-      rg_matvec(gw.wp + (size_t)H * g0, H, n, x, red, [&](int jj, float4 a) {
+      rg_matvec(sl_wp, H, n, x, red, [&](int jj, float4 a) {
         const float4 b = b4[g0 + jj];
         reinterpret_cast<float4*>(pvec)[g0 + jj] = make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
       });
@@ -434,10 +470,9 @@ __global__ __launch_bounds__(RG_NT) void rnnt_grid_kernel(RnntDev w, RnntGrid gw
     {
       for (int e = tid; e < P; e += RG_NT) x[e] = pvec[e];
       __syncthreads();
-      int g0, n;
-      rg_range(J >> 2, G, part, g0, n);
+      const int g0 = jg0, n = jn;
       const float4* b4 = reinterpret_cast<const float4*>(w.bpj);
-      rg_matvec(gw.wpj + (size_t)P * g0, P, n, x, red, [&](int jj, float4 a) {
+      rg_matvec(sl_wpj, P, n, x, red, [&](int jj, float4 a) {
         const float4 b = b4[g0 + jj];
         reinterpret_cast<float4*>(pj)[g0 + jj] = make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
       });
@@ -449,12 +484,10 @@ __global__ __launch_bounds__(RG_NT) void rnnt_grid_kernel(RnntDev w, RnntGrid gw
   };
 
   if (!predictor(w.blank)) return;
-  int v0, nv;
-  rg_range(w.Vp >> 2, G, part, v0, nv);
   int np = 1;
   while (np < nv) np <<= 1;
   const int ks = RG_NT / np, jj = tid % np, sp = tid / np;
-  const float4* wo = gw.wo + (size_t)J * v0;
+  const float4* wo = sl_wo;
   const float4* bo4 = reinterpret_cast<const float4*>(w.bo);
   int t = 0, step = 0;
   while (t < T) {
@@ -552,8 +585,8 @@ __global__ __launch_bounds__(RG_NT) void rnnt_grid_kernel(RnntDev w, RnntGrid gw
   }
 }
 
-size_t rnnt_grid_lds_bytes(const RnntDev& w) {
-  const size_t fl = (std::max(w.E, w.H) + w.H) + RNNT_RF * w.J + w.J;
+__host__ __device__ size_t rnnt_grid_lds_bytes(const RnntDev& w) {
+  const size_t fl = (size_t)((w.E > w.H ? w.E : w.H) + w.H) + RNNT_RF * w.J + w.J;
   return (fl + 3) / 4 * 16 + (size_t)RG_NT * RNNT_RF * 16 + 2 * RNNT_RF * 4 + 16;
 }
 
@@ -574,6 +607,7 @@ struct cfm_rnnt {
   const float *we = nullptr, *be = nullptr;   // enc_ffn [J, Eenc] (torch layout), [J]
   // the grid path's block-major slices (built for grid_blocks workgroups per utterance)
   int grid_blocks = 64;                       // 0: always one workgroup per utterance
+  int grid_lds = 1;                           // cache the grid path's weight slices in LDS when they fit
   int n_cu = 0;
   void* grid_mem = nullptr;
   cfm::RnntGrid gw{};
@@ -777,6 +811,10 @@ cfm_status cfm_rnnt_set_option(cfm_rnnt* h, const char* key, int64_t value) {
       return set_error(CFM_ERR_RUNTIME, "rnnt: device sync");
     return rnnt_grid_build(h) ? CFM_ERR_RUNTIME : CFM_OK;
   }
+  if (std::string(key) == "grid_lds") {
+    h->grid_lds = value != 0;
+    return CFM_OK;
+  }
   return set_error(CFM_ERR_VALUE, std::string("unknown rnnt option ") + key);
 }
 
@@ -823,12 +861,25 @@ cfm_status cfm_rnnt_greedy(const cfm_rnnt* h, const float* enc, int32_t rows, co
     if (hipMemsetAsync(scratch, 0, (size_t)B * per * 4, st) != hipSuccess ||
         hipMemsetAsync(bars, 0, (size_t)RG_MAXB * RG_MAXG * 8 + 256, st) != hipSuccess)
       return set_error(CFM_ERR_RUNTIME, "rnnt: workspace memset");
-    const size_t glds = rnnt_grid_lds_bytes(h->w);
-    if (glds > 64 * 1024 && hipFuncSetAttribute((const void*)rnnt_grid_kernel,
-                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)glds) != hipSuccess)
+    // the largest workgroup's weight slices (float4s): cached in LDS when they fit beside the work area
+    const RnntDev& w = h->w;
+    auto cdiv = [&](int a) { return (size_t)((a + G - 1) / G); };
+    size_t slice4 = 0;
+    for (int l = 0, in = w.E; l < w.nl; ++l, in = w.H) slice4 += (size_t)(in + w.H) * cdiv(w.H);
+    slice4 += (size_t)w.H * cdiv(w.P / 4) + (size_t)w.P * cdiv(w.J / 4) + (size_t)w.J * cdiv(w.Vp / 4);
+    const size_t work = rnnt_grid_lds_bytes(w);
+    const bool cache = h->grid_lds && work + slice4 * 16 <= 160 * 1024;
+    const size_t glds = work + (cache ? slice4 * 16 : 0);
+    const void* fn = cache ? (const void*)rnnt_grid_kernel<true> : (const void*)rnnt_grid_kernel<false>;
+    if (glds > 64 * 1024 &&
+        hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)glds) != hipSuccess)
       return set_error(CFM_ERR_RUNTIME, "rnnt: dynamic LDS attribute");
-    hipLaunchKernelGGL(rnnt_grid_kernel, dim3(B * G), dim3(RG_NT), glds, st, h->w, h->gw, scratch, (int)per, bars, err,
-                       proj, row_start, row_len, n_steps, out);
+    if (cache)
+      hipLaunchKernelGGL(rnnt_grid_kernel<true>, dim3(B * G), dim3(RG_NT), glds, st, h->w, h->gw, scratch, (int)per,
+                         bars, err, proj, row_start, row_len, n_steps, out);
+    else
+      hipLaunchKernelGGL(rnnt_grid_kernel<false>, dim3(B * G), dim3(RG_NT), glds, st, h->w, h->gw, scratch, (int)per,
+                         bars, err, proj, row_start, row_len, n_steps, out);
     const hipError_t ge = hipGetLastError();
     if (ge != hipSuccess) return set_error(CFM_ERR_RUNTIME, std::string("rnnt_grid_kernel: ") + hipGetErrorString(ge));
     return CFM_OK;

@@ -202,6 +202,8 @@ def test_grid_search_equals_one_workgroup(G, B):
     ref = dec.greedy_packed(enc, starts, lens, 4).cpu()
     dec.set_option("grid_blocks", G)
     assert dec.grid_blocks(B) == G
-    out = dec.greedy_packed(enc, starts, lens, 4).cpu()
-    assert (ref != 0).any() and (ref == 0).any()
-    np.testing.assert_array_equal(out.numpy(), ref.numpy())
+    for lds in (1, 0):   # weight slices cached in LDS where they fit (G >= 37 here) / always from HBM
+        dec.set_option("grid_lds", lds)
+        out = dec.greedy_packed(enc, starts, lens, 4).cpu()
+        assert (ref != 0).any() and (ref == 0).any()
+        np.testing.assert_array_equal(out.numpy(), ref.numpy())
