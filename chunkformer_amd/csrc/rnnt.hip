@@ -268,15 +268,22 @@ CFM_DEV void rg_range(int M4, int G, int p, int& g0, int& n) {
 
 // Grid barrier over the G workgroups of one utterance: workgroup p publishes the barrier's epoch in
 // its own flag word (no contended atomic: a counter serialised the G arrivals, ≈0.1 µs each), wave 0
-// of every workgroup polls all G flags (one load per lane) until each holds the epoch.  Release /
-// acquire: __syncthreads, then an agent-scope fence before the flag store and after the poll.
+// of every workgroup polls all G flags (one load per lane) until each holds the epoch.
+// ATOM = false: release / acquire by agent-scope fences around the flag store / after the poll (an
+// L2 write-back and invalidate on gfx950: the weight slices then come from the MALL every phase).
+// ATOM = true: every access to the exchanged vectors is itself an agent-scope relaxed atomic (sc1:
+// coherent across the XCDs' L2s), so the barrier only has to order completion: each wave waits for
+// its stores (vmcnt(0)) before the workgroup barrier, the flag store follows, and the readers' loads
+// issue after their poll returned -- no cache-wide fence, the weight slices stay in L2.
 // Returns false on timeout (after ~2^21 polls the error word is set) or when another workgroup set it.
+template <bool ATOM>
 CFM_DEV bool rg_barrier(unsigned long long* flags, int G, int part, unsigned long long epoch, int* err, int* lflag) {
+  if constexpr (ATOM) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x < 64) {
     const int lane = threadIdx.x;
     if (lane == 0) {
-      __threadfence();   // release this workgroup's stores (agent scope)
+      if constexpr (!ATOM) __threadfence();   // release this workgroup's stores (agent scope)
       __hip_atomic_store(flags + part, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     int ok = 1;
@@ -294,11 +301,22 @@ CFM_DEV bool rg_barrier(unsigned long long* flags, int G, int part, unsigned lon
         break;
       }
     }
-    __threadfence();   // acquire the other workgroups' stores
+    if constexpr (!ATOM) __threadfence();   // acquire the other workgroups' stores
     if (lane == 0) *lflag = ok;
   }
   __syncthreads();
   return *lflag != 0;
+}
+// accesses to the vectors the workgroups exchange (see rg_barrier)
+template <bool ATOM, class V>
+CFM_DEV V sh_ld(const V* p) {
+  if constexpr (ATOM) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else return *p;
+}
+template <bool ATOM, class V>
+CFM_DEV void sh_st(V* p, V v) {
+  if constexpr (ATOM) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else *p = v;
 }
 
 // Partial sums of the ks = NT / np threads (s, jj), tid = s * np + jj, down to one per column: xor
@@ -367,7 +385,7 @@ __host__ __device__ size_t rnnt_grid_lds_bytes(const RnntDev& w);
 // LDSW: the workgroup's weight slices are copied into LDS once (after the work area of
 // rnnt_grid_lds_bytes) and every emission's matrix-vector products read them there, not from the
 // MALL / HBM after each barrier's acquire
-template <bool LDSW>
+template <bool LDSW, bool ATOM>
 __global__ __launch_bounds__(RG_NT) void rnnt_grid_kernel(RnntDev w, RnntGrid gw, float* __restrict__ scratch,
                                                           int per_utt, unsigned long long* __restrict__ bars,
                                                           int* __restrict__ err, const float* __restrict__ enc_proj,
@@ -395,7 +413,7 @@ __global__ __launch_bounds__(RG_NT) void rnnt_grid_kernel(RnntDev w, RnntGrid gw
   int* dec = reinterpret_cast<int*>(red + RG_NT * RNNT_RF);   // [RF]
   int* lflag = dec + RNNT_RF;
   unsigned long long epoch = 0;
-  auto sync = [&]() { return rg_barrier(flags, G, part, ++epoch, err, lflag); };
+  auto sync = [&]() { return rg_barrier<ATOM>(flags, G, part, ++epoch, err, lflag); };
 
   // this workgroup's output ranges and weight slices
   int u0, nu, pg0, pn, jg0, jn, v0, nv;
@@ -433,10 +451,14 @@ __global__ __launch_bounds__(RG_NT) void rnnt_grid_kernel(RnntDev w, RnntGrid gw
     int in = E;
     const float4* wl = wcache;   // LDSW: layer l's slice follows layer l - 1's
     for (int l = 0; l < nl; ++l) {
-      const float* src = l == 0 ? w.embed + (size_t)tok * E : hs + ((size_t)(cur ^ 1) * nl + (l - 1)) * H;
-      for (int e = tid; e < in; e += RG_NT) x[e] = src[e];
+      if (l == 0) {
+        for (int e = tid; e < in; e += RG_NT) x[e] = w.embed[(size_t)tok * E + e];
+      } else {
+        const float* src = hs + ((size_t)(cur ^ 1) * nl + (l - 1)) * H;
+        for (int e = tid; e < in; e += RG_NT) x[e] = sh_ld<ATOM>(src + e);
+      }
       const float* hc = hs + ((size_t)cur * nl + l) * H;
-      for (int e = tid; e < H; e += RG_NT) x[in + e] = hc[e];
+      for (int e = tid; e < H; e += RG_NT) x[in + e] = sh_ld<ATOM>(hc + e);
       __syncthreads();
       float* cold = cs + ((size_t)cur * nl + l) * H;
       float* cnew = cs + ((size_t)(cur ^ 1) * nl + l) * H;
@@ -448,8 +470,8 @@ __global__ __launch_bounds__(RG_NT) void rnnt_grid_kernel(RnntDev w, RnntGrid gw
         const float4 b = bq[u];
         const float ig = sigm(a.x + b.x), fg = sigm(a.y + b.y), gg = tanhf(a.z + b.z), og = sigm(a.w + b.w);
         const float cv = fg * cold[u] + ig * gg;
-        cnew[u] = cv;
-        hnew[u] = og * tanhf(cv);
+        cnew[u] = cv;   // (read back only by this workgroup)
+        sh_st<ATOM>(hnew + u, og * tanhf(cv));
       });
       if (!sync()) return false;
       wl += (size_t)(in + H) * nu;
@@ -457,28 +479,30 @@ __global__ __launch_bounds__(RG_NT) void rnnt_grid_kernel(RnntDev w, RnntGrid gw
     }
     {
       const float* ht = hs + ((size_t)(cur ^ 1) * nl + (nl - 1)) * H;
-      for (int e = tid; e < H; e += RG_NT) x[e] = ht[e];
+      for (int e = tid; e < H; e += RG_NT) x[e] = sh_ld<ATOM>(ht + e);
       __syncthreads();
       const int g0 = pg0, n = pn;
       const float4* b4 = reinterpret_cast<const float4*>(w.bp);
       rg_matvec(sl_wp, H, n, x, red, [&](int jj, float4 a) {
         const float4 b = b4[g0 + jj];
-        reinterpret_cast<float4*>(pvec)[g0 + jj] = make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+        float* o = pvec + 4 * (g0 + jj);
+        sh_st<ATOM>(o, a.x + b.x); sh_st<ATOM>(o + 1, a.y + b.y); sh_st<ATOM>(o + 2, a.z + b.z); sh_st<ATOM>(o + 3, a.w + b.w);
       });
       if (!sync()) return false;
     }
     {
-      for (int e = tid; e < P; e += RG_NT) x[e] = pvec[e];
+      for (int e = tid; e < P; e += RG_NT) x[e] = sh_ld<ATOM>(pvec + e);
       __syncthreads();
       const int g0 = jg0, n = jn;
       const float4* b4 = reinterpret_cast<const float4*>(w.bpj);
       rg_matvec(sl_wpj, P, n, x, red, [&](int jj, float4 a) {
         const float4 b = b4[g0 + jj];
-        reinterpret_cast<float4*>(pj)[g0 + jj] = make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+        float* o = pj + 4 * (g0 + jj);
+        sh_st<ATOM>(o, a.x + b.x); sh_st<ATOM>(o + 1, a.y + b.y); sh_st<ATOM>(o + 2, a.z + b.z); sh_st<ATOM>(o + 3, a.w + b.w);
       });
       if (!sync()) return false;
     }
-    for (int e = tid; e < J; e += RG_NT) lpj[e] = pj[e];
+    for (int e = tid; e < J; e += RG_NT) lpj[e] = sh_ld<ATOM>(pj + e);
     __syncthreads();
     return true;
   };
@@ -552,16 +576,16 @@ __global__ __launch_bounds__(RG_NT) void rnnt_grid_kernel(RnntDev w, RnntGrid gw
       int bi = 0x7fffffff;
       for (int c = 0; c < nv; ++c)   // ascending ids: strict > keeps the lowest id of a tie
         if (sv[tid * 64 + c] > bv) { bv = sv[tid * 64 + c]; bi = si[tid * 64 + c]; }
-      candv[((size_t)par * G + part) * RNNT_RF + tid] = bv;
-      candi[((size_t)par * G + part) * RNNT_RF + tid] = bi;
+      sh_st<ATOM>(candv + ((size_t)par * G + part) * RNNT_RF + tid, bv);
+      sh_st<ATOM>(candi + ((size_t)par * G + part) * RNNT_RF + tid, bi);
     }
     if (!sync()) return;
     if (tid < RNNT_RF) {
       float bv = -INFINITY;
       int bi = 0x7fffffff;
       for (int q = 0; q < G; ++q) {   // parts in ascending vocabulary order
-        const float v = candv[((size_t)par * G + q) * RNNT_RF + tid];
-        if (v > bv) { bv = v; bi = candi[((size_t)par * G + q) * RNNT_RF + tid]; }
+        const float v = sh_ld<ATOM>(candv + ((size_t)par * G + q) * RNNT_RF + tid);
+        if (v > bv) { bv = v; bi = sh_ld<ATOM>(candi + ((size_t)par * G + q) * RNNT_RF + tid); }
       }
       dec[tid] = bi;
     }
@@ -608,6 +632,7 @@ struct cfm_rnnt {
   // the grid path's block-major slices (built for grid_blocks workgroups per utterance)
   int grid_blocks = 64;                       // 0: always one workgroup per utterance
   int grid_lds = 1;                           // cache the grid path's weight slices in LDS when they fit
+  int grid_atomic = 1;                        // exchanged vectors by agent-scope atomics, no cache-wide fences
   int n_cu = 0;
   void* grid_mem = nullptr;
   cfm::RnntGrid gw{};
@@ -815,6 +840,10 @@ cfm_status cfm_rnnt_set_option(cfm_rnnt* h, const char* key, int64_t value) {
     h->grid_lds = value != 0;
     return CFM_OK;
   }
+  if (std::string(key) == "grid_atomic") {
+    h->grid_atomic = value != 0;
+    return CFM_OK;
+  }
   return set_error(CFM_ERR_VALUE, std::string("unknown rnnt option ") + key);
 }
 
@@ -870,16 +899,18 @@ cfm_status cfm_rnnt_greedy(const cfm_rnnt* h, const float* enc, int32_t rows, co
     const size_t work = rnnt_grid_lds_bytes(w);
     const bool cache = h->grid_lds && work + slice4 * 16 <= 160 * 1024;
     const size_t glds = work + (cache ? slice4 * 16 : 0);
-    const void* fn = cache ? (const void*)rnnt_grid_kernel<true> : (const void*)rnnt_grid_kernel<false>;
-    if (glds > 64 * 1024 &&
-        hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)glds) != hipSuccess)
-      return set_error(CFM_ERR_RUNTIME, "rnnt: dynamic LDS attribute");
-    if (cache)
-      hipLaunchKernelGGL(rnnt_grid_kernel<true>, dim3(B * G), dim3(RG_NT), glds, st, h->w, h->gw, scratch, (int)per,
-                         bars, err, proj, row_start, row_len, n_steps, out);
-    else
-      hipLaunchKernelGGL(rnnt_grid_kernel<false>, dim3(B * G), dim3(RG_NT), glds, st, h->w, h->gw, scratch, (int)per,
-                         bars, err, proj, row_start, row_len, n_steps, out);
+    auto launch = [&](auto kern) -> bool {
+      if (glds > 64 * 1024 &&
+          hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)glds) != hipSuccess)
+        return false;
+      hipLaunchKernelGGL(kern, dim3(B * G), dim3(RG_NT), glds, st, h->w, h->gw, scratch, (int)per, bars, err, proj,
+                         row_start, row_len, n_steps, out);
+      return true;
+    };
+    const bool atom = h->grid_atomic != 0;
+    const bool okl = cache ? (atom ? launch(rnnt_grid_kernel<true, true>) : launch(rnnt_grid_kernel<true, false>))
+                           : (atom ? launch(rnnt_grid_kernel<false, true>) : launch(rnnt_grid_kernel<false, false>));
+    if (!okl) return set_error(CFM_ERR_RUNTIME, "rnnt: dynamic LDS attribute");
     const hipError_t ge = hipGetLastError();
     if (ge != hipSuccess) return set_error(CFM_ERR_RUNTIME, std::string("rnnt_grid_kernel: ") + hipGetErrorString(ge));
     return CFM_OK;

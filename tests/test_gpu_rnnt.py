@@ -202,8 +202,11 @@ def test_grid_search_equals_one_workgroup(G, B):
     ref = dec.greedy_packed(enc, starts, lens, 4).cpu()
     dec.set_option("grid_blocks", G)
     assert dec.grid_blocks(B) == G
-    for lds in (1, 0):   # weight slices cached in LDS where they fit (G >= 37 here) / always from HBM
+    # weight slices cached in LDS where they fit (G >= 37 here) or not; exchange by agent-scope
+    # atomics (default) or plain accesses behind cache-wide fences
+    for lds, atom in ((1, 1), (0, 1), (1, 0)):
         dec.set_option("grid_lds", lds)
+        dec.set_option("grid_atomic", atom)
         out = dec.greedy_packed(enc, starts, lens, 4).cpu()
         assert (ref != 0).any() and (ref == 0).any()
         np.testing.assert_array_equal(out.numpy(), ref.numpy())

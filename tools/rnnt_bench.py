@@ -23,6 +23,8 @@ def main():
                     help="workgroups per utterance of the multi-CU search (0 = one workgroup)")
     ap.add_argument("--blank-bias", type=float, default=3.72)
     ap.add_argument("--grid-lds", type=int, nargs="*", default=[1], help="weight slices cached in LDS (0 / 1)")
+    ap.add_argument("--grid-atomic", type=int, nargs="*", default=[1],
+                    help="exchange by agent-scope atomics (1) or fences (0)")
     a = ap.parse_args()
     c = RNNTConfig()
     g = RNNTGreedy(c, synthetic_transducer_state_dict(c, 0, blank_bias=a.blank_bias), device="cuda")
@@ -32,9 +34,10 @@ def main():
     starts = [b * T for b in range(B)]
     lens = [T] * B
     ref = None
-    for G, lds in [(G, l) for G in a.grid for l in a.grid_lds]:
+    for G, lds, atom in [(G, l, at) for G in a.grid for l in a.grid_lds for at in a.grid_atomic]:
         g.set_option("grid_blocks", G)
         g.set_option("grid_lds", lds)
+        g.set_option("grid_atomic", atom)
         g.greedy_packed(enc[: min(B * T, 2000)], [0], [min(T, 2000)])   # warm-up
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -44,7 +47,7 @@ def main():
         same = "" if ref is None else f", identical to grid {a.grid[0]}: {bool(torch.equal(out, ref))}"
         ref = out if ref is None else ref
         emis = int((out != c.blank).sum().item())
-        print(f"grid {G} lds {lds} (used {g.grid_blocks(B)}) B={B} T={T}: {dt * 1e3:.1f} ms, {B * T / dt:.0f} frames/s, "
+        print(f"grid {G} lds {lds} atomic {atom} (used {g.grid_blocks(B)}) B={B} T={T}: {dt * 1e3:.1f} ms, {B * T / dt:.0f} frames/s, "
               f"{emis / (B * T):.3f} emissions per frame, {dt * 1e3 / max(emis / B, 1):.4f} ms per emission per "
               f"utterance{same}", flush=True)
 
