@@ -307,6 +307,12 @@ CFM_DEV bool rg_barrier(unsigned long long* flags, int G, int part, unsigned lon
   __syncthreads();
   return *lflag != 0;
 }
+#ifndef RG_UNROLL
+#define RG_UNROLL 16   // weight loads in flight per thread in the predictor matvecs
+#endif
+#ifndef RG_JUNROLL
+#define RG_JUNROLL 8   // ... in the joint
+#endif
 // accesses to the vectors the workgroups exchange (see rg_barrier)
 template <bool ATOM, class V>
 CFM_DEV V sh_ld(const V* p) {
@@ -317,6 +323,22 @@ template <bool ATOM, class V>
 CFM_DEV void sh_st(V* p, V v) {
   if constexpr (ATOM) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   else *p = v;
+}
+// dst[0:n) (LDS) = src[0:n) (an exchanged vector, n <= 8 NT): every load issued before the first
+// LDS store, so the copy costs one round trip
+template <bool ATOM>
+CFM_DEV void rg_fetch(float* dst, const float* src, int n) {
+  float v[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int e = (int)threadIdx.x + i * RG_NT;
+    v[i] = e < n ? sh_ld<ATOM>(src + e) : 0.f;
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int e = (int)threadIdx.x + i * RG_NT;
+    if (e < n) dst[e] = v[i];
+  }
 }
 
 // Partial sums of the ks = NT / np threads (s, jj), tid = s * np + jj, down to one per column: xor
@@ -352,9 +374,8 @@ CFM_DEV void rg_matvec(const float4* __restrict__ Wb, int K, int n, const float*
   const int ks = RG_NT / np, jj = tid % np, s = tid / np;
   float4 acc = {0.f, 0.f, 0.f, 0.f};
   if (jj < n) {
-    // 16 loads in flight per thread: after a barrier's acquire the slices come from the MALL / HBM,
-    // so the loop is latency-bound, not bandwidth-bound
-#pragma unroll 16
+    // several loads in flight per thread: the loop is latency-bound, not bandwidth-bound
+#pragma unroll RG_UNROLL
     for (int k = s; k < K; k += ks) {
       const float4 wv = Wb[(size_t)k * n + jj];
       const float xv = x[k];
@@ -454,11 +475,9 @@ __global__ __launch_bounds__(RG_NT) void rnnt_grid_kernel(RnntDev w, RnntGrid gw
       if (l == 0) {
         for (int e = tid; e < in; e += RG_NT) x[e] = w.embed[(size_t)tok * E + e];
       } else {
-        const float* src = hs + ((size_t)(cur ^ 1) * nl + (l - 1)) * H;
-        for (int e = tid; e < in; e += RG_NT) x[e] = sh_ld<ATOM>(src + e);
+        rg_fetch<ATOM>(x, hs + ((size_t)(cur ^ 1) * nl + (l - 1)) * H, in);
       }
-      const float* hc = hs + ((size_t)cur * nl + l) * H;
-      for (int e = tid; e < H; e += RG_NT) x[in + e] = sh_ld<ATOM>(hc + e);
+      rg_fetch<ATOM>(x + in, hs + ((size_t)cur * nl + l) * H, H);
       __syncthreads();
       float* cold = cs + ((size_t)cur * nl + l) * H;
       float* cnew = cs + ((size_t)(cur ^ 1) * nl + l) * H;
@@ -479,7 +498,7 @@ __global__ __launch_bounds__(RG_NT) void rnnt_grid_kernel(RnntDev w, RnntGrid gw
     }
     {
       const float* ht = hs + ((size_t)(cur ^ 1) * nl + (nl - 1)) * H;
-      for (int e = tid; e < H; e += RG_NT) x[e] = sh_ld<ATOM>(ht + e);
+      rg_fetch<ATOM>(x, ht, H);
       __syncthreads();
       const int g0 = pg0, n = pn;
       const float4* b4 = reinterpret_cast<const float4*>(w.bp);
@@ -491,7 +510,7 @@ __global__ __launch_bounds__(RG_NT) void rnnt_grid_kernel(RnntDev w, RnntGrid gw
       if (!sync()) return false;
     }
     {
-      for (int e = tid; e < P; e += RG_NT) x[e] = sh_ld<ATOM>(pvec + e);
+      rg_fetch<ATOM>(x, pvec, P);
       __syncthreads();
       const int g0 = jg0, n = jn;
       const float4* b4 = reinterpret_cast<const float4*>(w.bpj);
@@ -502,7 +521,7 @@ __global__ __launch_bounds__(RG_NT) void rnnt_grid_kernel(RnntDev w, RnntGrid gw
       });
       if (!sync()) return false;
     }
-    for (int e = tid; e < J; e += RG_NT) lpj[e] = sh_ld<ATOM>(pj + e);
+    rg_fetch<ATOM>(lpj, pj, J);
     __syncthreads();
     return true;
   };
@@ -526,7 +545,7 @@ __global__ __launch_bounds__(RG_NT) void rnnt_grid_kernel(RnntDev w, RnntGrid gw
 #pragma unroll
     for (int f = 0; f < RNNT_RF; ++f) acc[f] = make_float4(0.f, 0.f, 0.f, 0.f);
     if (jj < nv) {
-#pragma unroll 8
+#pragma unroll RG_JUNROLL
       for (int k = sp; k < J; k += ks) {
         const float4 wv = wo[(size_t)k * nv + jj];
 #pragma unroll
