@@ -6,7 +6,7 @@
 #   tests "<pytest -k expr>"   selected GPU tests              -> gpurun_out/tests.log
 #   suite                      the whole -m gpu suite + smoke   -> gpurun_out/suite.log
 #   ab <ab_bench.py args>      in-process A/B of model options  -> gpurun_out/ab.log
-#   bench <bench.py args>      one bench line                   -> gpurun_out/bench.log
+#   bench [@NAME] <bench.py args>  one bench line              -> gpurun_out/bench[_NAME].log
 #   prof <round> [pmc]         tools/profile_round.sh (rocprof stats + PMC traffic + MFMA busy)
 #   py <script> [args]         any repo script under a 600 s limit -> gpurun_out/py.log
 # Several jobs can be chained with '+': gpu_job.sh tests "ring" + ab --layers 1 --variant attn_diag=0
@@ -31,9 +31,11 @@ run_job() {
     ab)
       timeout -k 10 500 python3 tools/ab_bench.py "$@" > "$O/ab.log" 2>&1 || { tail -30 "$O/ab.log"; return 1; }
       grep -v amdgpu.ids "$O/ab.log" ;;
-    bench)
-      timeout -k 10 500 python3 bench.py "$@" > "$O/bench.log" 2>&1 || { tail -30 "$O/bench.log"; return 1; }
-      grep '^{' "$O/bench.log" | tail -1 ;;
+    bench)   # optional first argument @NAME: log to bench_NAME.log (several bench jobs in one call)
+      local bl="$O/bench.log"
+      case "$1" in @*) bl="$O/bench_${1#@}.log"; shift ;; esac
+      timeout -k 10 500 python3 bench.py "$@" > "$bl" 2>&1 || { tail -30 "$bl"; return 1; }
+      grep '^{' "$bl" | tail -1 ;;
     prof)
       bash "$R/tools/profile_round.sh" "$@" ;;
     py)
