@@ -280,8 +280,9 @@ def main():
                          "attention, B=256)")
     ap.add_argument("--hours", type=float, default=16.0, help="endless: audio hours")
     ap.add_argument("--endless-mode", default="graphpipe", choices=["graphpipe", "pipeline", "graph"],
-                    help="endless: --pipeline-depth segments in flight whose steady-state ticks replay captured "
-                         "HIP graphs (graphpipe), the same pipeline launched eagerly (pipeline), or one segment "
+                    help="endless: --pipeline-depth segments in flight, runs of up to 12 middle segments replaying "
+                         "one captured HIP graph of that multi-stream pipeline (graphpipe), the same pipeline "
+                         "launched eagerly (pipeline), or one segment "
                          "at a time replaying one captured graph per middle segment (graph); all bit-identical "
                          "to the eager loop")
     ap.add_argument("--pipeline-depth", type=int, default=3, help="endless pipeline: segments in flight")
@@ -575,9 +576,9 @@ def bench_single(args):
         workload = (f"endless_decode over one {args.hours:g} h utterance (synthetic N(0,1) fbank), C=64 L=128 "
                     f"R=128, total_batch_duration={args.tbd}: {len(segs)} segments of <= {seg_len} frames "
                     f"(trunc {trunc} rows kept each), att/cnn caches carried, " +
-                    {"graphpipe": f"{args.pipeline_depth} segments in flight (stage slots of a software pipeline "
-                                  "on as many HIP streams, each steady-state tick one replay of a captured HIP "
-                                  "graph; segment k+1's layer l after segment k's layer l)",
+                    {"graphpipe": f"{args.pipeline_depth} segments in flight on as many HIP streams (segment k+1 "
+                                  "layer l after segment k layer l), each run of up to 12 middle segments one "
+                                  "replay of a captured HIP graph of that whole multi-stream pipeline",
                      "pipeline": f"{args.pipeline_depth} segments in flight on {args.pipeline_depth} HIP streams "
                                  "(segment k+1 layer l waits for segment k layer l), launched eagerly",
                      "graph": "middle segments replayed one at a time from one captured HIP graph (front-end + "

@@ -308,10 +308,10 @@ CFM_DEV bool rg_barrier(unsigned long long* flags, int G, int part, unsigned lon
   return *lflag != 0;
 }
 #ifndef RG_UNROLL
-#define RG_UNROLL 16   // weight loads in flight per thread in the predictor matvecs
+#define RG_UNROLL 4    // weight loads in flight per thread in the predictor matvecs (16: 10-35% slower)
 #endif
 #ifndef RG_JUNROLL
-#define RG_JUNROLL 8   // ... in the joint
+#define RG_JUNROLL 2   // ... in the joint (8: slower)
 #endif
 // accesses to the vectors the workgroups exchange (see rg_barrier)
 template <bool ATOM, class V>
@@ -649,7 +649,7 @@ struct cfm_rnnt {
   cfm::RnntDev w{};
   const float *we = nullptr, *be = nullptr;   // enc_ffn [J, Eenc] (torch layout), [J]
   // the grid path's block-major slices (built for grid_blocks workgroups per utterance)
-  int grid_blocks = 64;                       // 0: always one workgroup per utterance
+  int grid_blocks = 32;                       // 0: always one workgroup per utterance
   int grid_lds = 1;                           // cache the grid path's weight slices in LDS when they fit
   int grid_atomic = 1;                        // exchanged vectors by agent-scope atomics, no cache-wide fences
   int n_cu = 0;

@@ -247,46 +247,46 @@ class EndlessPipeline:
         return ids_out, eo_out, len(segs) % 2
 
 
-def stage_slots(num_blocks: int, depth: int):
-    """The encoder stages (-1 = front-end, 0 .. num_blocks-1 = layers) cut into `depth` consecutive
-    slots [lo, hi] (the longer ones first): EndlessGraphPipeline's stage slots."""
-    stages = list(range(-1, num_blocks))
-    depth = max(1, min(depth, len(stages)))
-    per, extra = divmod(len(stages), depth)
-    slots, i = [], 0
-    for s in range(depth):
-        n = per + (1 if s < extra else 0)
-        slots.append((stages[i], stages[i + n - 1]))
-        i += n
-    return slots
-
-
-def pipeline_ticks(n_segments: int, depth: int):
-    """Tick t of the software pipeline runs slot s of segment t - s for every valid s: a list of
-    [(segment, slot), ...] per tick.  Every segment runs its slots 0 .. depth-1 in consecutive ticks,
-    and segment k's slot s runs one tick after segment k - 1's (its layer caches) and one tick after
-    its own slot s - 1."""
-    return [[(t - s, s) for s in range(depth) if 0 <= t - s < n_segments] for t in range(n_segments + depth - 1)]
+def graph_blocks(graph_ok: List[bool], kmax: int):
+    """EndlessGraphPipeline's schedule (host logic): the segments as [(start, count, replay), ...] in
+    order -- maximal runs of graph-eligible segments cut into blocks of at most `kmax` (replayed from
+    one captured graph each), every other segment a block of 1 run eagerly."""
+    out, k, n = [], 0, len(graph_ok)
+    while k < n:
+        if not graph_ok[k]:
+            out.append((k, 1, False))
+            k += 1
+            continue
+        m = k
+        while m < n and graph_ok[m]:
+            m += 1
+        while k < m:
+            cnt = min(kmax, m - k)
+            out.append((k, cnt, True))
+            k += cnt
+    return out
 
 
 class EndlessGraphPipeline:
-    """endless_decode's segments as a software pipeline of `depth` stage slots whose steady state is
+    """endless_decode's segments with `depth` in flight (as EndlessPipeline: segment k on stream
+    k % depth, its layer l waiting only for segment k - 1's layer l) where runs of middle segments are
     replayed from HIP graphs (BASELINE configs[3]: context caches carried across graph-captured steps,
-    with several segments in flight).
+    several segments in flight).
 
-    The encoder stages (-1 = front-end, 0..nb-1 = layers) are cut into `depth` consecutive slots.  Tick
-    t runs slot s of segment t - s for every s: those units are independent (segment k's slot s needs
-    segment k - 1's slot s, i.e. the layer caches it carries, and its own slot s - 1, both from tick
-    t - 1), so within a tick they run on `depth` streams at once, and tick t + 1 starts after tick t.
-    A tick whose units all belong to middle segments (the same length and, once offset >= max(L, 7),
-    the same plan: streaming.py's module note) is one HIP graph replay; the graph only depends on the
-    tick's phase (segment k uses workspace / output slot k % depth and cache pair k % 2), so
-    lcm(depth, 2) graphs are captured once per segment geometry.  The first segments (offset 0), the
-    ragged last one and the pipeline's fill / drain ticks run the same stage calls eagerly.  Every unit
-    is a cfm_encode_masked_stages call with that segment's plan, caches and workspace, so the result is
+    A block of up to `block` consecutive middle segments (the same length and, once offset >= max(L, 7),
+    the same plan: streaming.py's module note) is captured once as ONE graph holding the whole
+    multi-stream pipeline of those segments -- every stage call, the per-layer cross-stream event
+    edges, the CTC head and the copies of each segment's kept rows / ids into the block's output
+    slots -- and replayed for every later block at the same phase (segment k uses stream, workspace and
+    output slot k % depth and cache pair k % 2, so a block's graph depends on its first segment's
+    phase k mod lcm(depth, 2) and its length).  Inside a replay the segments overlap exactly as in the
+    eager pipeline; a block's first segment starts after the previous block (one pipeline drain per
+    block of `block` segments, instead of one per tick).  The first segments (offset 0), the ragged
+    last one and short runs are launched eagerly through the same calls, so the result is
     bit-identical to the one-call-per-segment loop."""
 
-    def __init__(self, encoder, C: int, L: int, R: int, trunc: int, seg_len: int, want_out: bool, depth: int = 3):
+    def __init__(self, encoder, C: int, L: int, R: int, trunc: int, seg_len: int, want_out: bool, depth: int = 3,
+                 block: int = 12):
         if depth < 1:
             raise ValueError(f"pipeline depth {depth} < 1")
         self.enc = encoder
@@ -296,91 +296,82 @@ class EndlessGraphPipeline:
         dev = encoder.device
         self.dev = dev
         nb, H, dk, d = cfg.num_blocks, cfg.n_heads, cfg.head_dim, cfg.d_model
-        self.slots = stage_slots(nb, depth)
-        depth = len(self.slots)
         self.depth = depth
+        self.period = depth if depth % 2 == 0 else 2 * depth
+        self.block = max(1, block)
         self.att = [torch.zeros(nb, L, H, 2 * dk, device=dev) for _ in range(2)]
         self.cnn = [torch.zeros(nb, d, cfg.conv_lorder, device=dev) for _ in range(2)]
         self.streams = [torch.cuda.Stream(dev) for _ in range(depth)]
         self.ws: List[Optional[torch.Tensor]] = [None] * depth
         self.out: List[Optional[torch.Tensor]] = [None] * depth
-        self.ids: List[Optional[torch.Tensor]] = [None] * depth
         self.ctc_ws: List[Optional[torch.Tensor]] = [None] * depth
-        self.period = depth if depth % 2 == 0 else 2 * depth
+        # the graphs' fixed input / output slots, by position in a block
+        self.g_feats: List[Optional[torch.Tensor]] = [None] * self.block
+        self.g_ids: List[Optional[torch.Tensor]] = [None] * self.block
+        self.g_eo: List[Optional[torch.Tensor]] = [None] * self.block
         self.graphs: dict = {}
         self.g_plan = None
-        self.g_feats = torch.zeros(max(seg_len, 1), cfg.input_dim, device=dev)
         self.vocab = cfg.vocab
-        self.replayed = 0   # ticks replayed from graphs in the last run (tests / bench)
+        self.replayed = 0   # segments replayed from graphs in the last run (tests / bench)
 
-    def _buf(self, lst, i, n, dtype) -> None:
+    def _buf(self, lst, i, n, dtype) -> torch.Tensor:
         t = lst[i]
         if t is None or t.numel() < n:
             lst[i] = torch.empty(n, dtype=dtype, device=self.dev)
             self.graphs.clear()   # captured graphs hold the old buffer's address
+        return lst[i]
 
-    def _unit(self, seg: dict, slot: int, st) -> None:
-        """Slot `slot`'s stage calls for one segment on stream `st` (+ the CTC head after the last)."""
-        enc = self.enc
-        k, p = seg["k"], seg["k"] % self.depth
-        c = k % 2
-        lo, hi = self.slots[slot]
-        _lib.check(_lib.cfm_encode_masked_stages(
-            enc._h, seg["feats"].data_ptr(), seg["plan"].data_ptr(), seg["plan_dev"].data_ptr(),
-            self.att[c].data_ptr(), self.cnn[c].data_ptr(), int(self.trunc), self.att[1 - c].data_ptr(),
-            self.cnn[1 - c].data_ptr(), self.out[p].data_ptr(), self.ws[p].data_ptr(), seg["wsb"], lo, hi,
-            st.cuda_stream))
-        if slot == self.depth - 1 and self.vocab > 0 and seg["rows"] > 0:
+    def _segment(self, seg: dict, prev, ids_dst, eo_dst):
+        """Segment seg["k"]'s stage calls on stream k % depth, layer l after `prev[l]` (the previous
+        segment's layer-l event); its CTC ids into ids_dst and (want_out) its kept rows into eo_dst.
+        Returns its per-layer events."""
+        enc, C = self.enc, self.C
+        d = enc.cfg.d_model
+        k = seg["k"]
+        p, c = k % self.depth, k % 2
+        st = self.streams[p]
+        cur = []
+        for stage in range(-1, enc.cfg.num_blocks):
+            if stage >= 0 and prev is not None:
+                st.wait_event(prev[stage])
+            _lib.check(_lib.cfm_encode_masked_stages(
+                enc._h, seg["feats"].data_ptr(), seg["plan"].data_ptr(), seg["plan_dev"].data_ptr(),
+                self.att[c].data_ptr(), self.cnn[c].data_ptr(), int(self.trunc), self.att[1 - c].data_ptr(),
+                self.cnn[1 - c].data_ptr(), self.out[p].data_ptr(), self.ws[p].data_ptr(), seg["wsb"], stage, stage,
+                st.cuda_stream))
+            if stage >= 0:
+                ev = torch.cuda.Event()
+                ev.record(st)
+                cur.append(ev)
+        rows = seg["rows"]
+        if rows > 0:
             with torch.cuda.stream(st):
-                enc._ctc_raw(self.out[p], seg["rows"], None, self.ids[p], self.ctc_ws[p])
-
-    def _tick(self, units, graph_key=None) -> None:
-        """One tick: its units on `depth` streams (fork from / join into the caller's stream), either
-        eagerly or by replaying (capturing first) the graph of `graph_key`."""
-        caller = torch.cuda.current_stream(self.dev)
-        if graph_key is not None:
-            g = self.graphs.get(graph_key)
-            if g is None:
-                g = torch.cuda.CUDAGraph()
-                cap = self.streams[0]
-                cap.wait_stream(caller)
-                with torch.cuda.graph(g, stream=cap):
-                    self._fork_join(units, cap)
-                self.graphs[graph_key] = g
-            g.replay()
-            self.replayed += 1
-            return
-        self._fork_join(units, caller)
-
-    def _fork_join(self, units, base) -> None:
-        for i, (seg, slot) in enumerate(units):
-            st = self.streams[i]
-            if st is not base:
-                st.wait_stream(base)
-            self._unit(seg, slot, st)
-        for i in range(len(units)):
-            if self.streams[i] is not base:
-                base.wait_stream(self.streams[i])
+                eo = self.out[p][: seg["N"] * C * d].view(seg["N"] * C, d)[:rows]
+                if ids_dst is not None:
+                    enc._ctc_raw(eo, rows, None, ids_dst, self.ctc_ws[p])
+                if eo_dst is not None:
+                    eo_dst.copy_(eo)
+        return cur
 
     def run(self, xs_dev: torch.Tensor, segs):
         """Returns (per-segment CTC ids of the kept rows, per-segment kept encoder rows or None, index of
         the cache pair holding the caches after the last segment), ready on the caller's stream."""
         enc, C, L, R, D = self.enc, self.C, self.L, self.R, self.depth
         d = enc.cfg.d_model
-        self.att[0].zero_()
-        self.cnn[0].zero_()
         self.replayed = 0
         caller = torch.cuda.current_stream(self.dev)
         n = len(segs)
         if n == 0:
             return [], [], 0
+        self.att[0].zero_()
+        self.cnn[0].zero_()
         info, offset = [], 0
         for k, (start, stop, keep_trunc, _) in enumerate(segs):
             n_frames = stop - start
             plan, n_chunks, out_lens = _lib.plan_masked([n_frames], [offset], C, L, R)
             N = n_chunks[0]
             kept = min(out_lens[0], self.trunc) if keep_trunc else out_lens[0]
-            info.append({"k": k, "x": xs_dev[start:stop], "plan": plan, "N": N, "n": out_lens[0], "rows": kept,
+            info.append({"k": k, "x": xs_dev[start:stop], "plan": plan, "N": N, "rows": kept,
                          "wsb": int(_lib.cfm_workspace_bytes_masked(enc._h, N, C, L, R)), "len": n_frames})
             offset += kept
         # the graph plan: the first middle segment whose plan no longer depends on the offset
@@ -389,11 +380,13 @@ class EndlessGraphPipeline:
                 if s["len"] == self.seg_len and sum(s2["rows"] for s2 in info[: s["k"]]) >= max(L, 7):
                     self.g_plan = s["plan"]
                     self.g_plan_dev = enc._upload(s["plan"])
+                    self.g_rows = s["rows"]
                     break
         for s in info:
-            s["graph"] = self.g_plan is not None and s["len"] == self.seg_len and torch.equal(s["plan"], self.g_plan)
+            s["graph"] = (self.g_plan is not None and s["len"] == self.seg_len and s["rows"] == self.g_rows
+                          and torch.equal(s["plan"], self.g_plan))
             if s["graph"]:
-                s["plan"], s["plan_dev"], s["feats"] = self.g_plan, self.g_plan_dev, self.g_feats
+                s["plan"], s["plan_dev"] = self.g_plan, self.g_plan_dev
             else:
                 s["plan_dev"] = enc._upload(s["plan"])
                 s["feats"] = s["x"].contiguous()
@@ -402,25 +395,74 @@ class EndlessGraphPipeline:
         for p in range(D):   # slot buffers sized for the largest segment
             self._buf(self.ws, p, max(s["wsb"] for s in info), torch.uint8)
             self._buf(self.out, p, max(s["N"] for s in info) * C * d, torch.float32)
-            self._buf(self.ids, p, max_rows, torch.int32)
             if ctc_b > 0:
                 self._buf(self.ctc_ws, p, ctc_b, torch.uint8)
+        if self.g_plan is not None:
+            for i in range(self.block):
+                self._buf(self.g_feats, i, self.seg_len * enc.cfg.input_dim, torch.float32)
+                if self.vocab > 0:
+                    self._buf(self.g_ids, i, max(self.g_rows, 1), torch.int32)
+                if self.want_out:
+                    self._buf(self.g_eo, i, max(self.g_rows, 1) * d, torch.float32)
+        for st in self.streams:
+            st.wait_stream(caller)   # inputs, zeroed caches, buffers
         ids_out: List[Optional[torch.Tensor]] = [None] * n
         eo_out: List[Optional[torch.Tensor]] = [None] * n
-        for t, tick in enumerate(pipeline_ticks(n, D)):
-            units = [(info[k], s) for k, s in tick]
-            full = len(units) == D and all(u[0]["graph"] for u in units)
-            if units and units[0][1] == 0 and units[0][0]["graph"]:
-                self.g_feats[: units[0][0]["len"]].copy_(units[0][0]["x"])   # the graph's input rows
-            self._tick(units, (t % self.period) if full else None)
-            done = t - (D - 1)   # the segment whose last slot ran in this tick
-            if 0 <= done < n:
-                s = info[done]
-                p = done % D
-                eo = self.out[p][: s["N"] * C * d].view(s["N"] * C, d)[: s["rows"]]
-                if self.vocab > 0 and s["rows"] > 0:
-                    ids_out[done] = self.ids[p][: s["rows"]].clone()
+        prev = None
+        for k0, cnt, replay in graph_blocks([s["graph"] for s in info], self.block):
+            if not replay:
+                s = info[k0]
+                st = self.streams[k0 % D]
+                ids = eo = None
+                with torch.cuda.stream(st):
+                    if self.vocab > 0 and s["rows"] > 0:
+                        ids = torch.empty(s["rows"], dtype=torch.int32, device=self.dev)
+                    if self.want_out:
+                        eo = torch.empty(s["rows"], d, dtype=torch.float32, device=self.dev)
+                prev = self._segment(s, prev, ids, eo)
+                for t in (ids, eo):
+                    if t is not None:
+                        t.record_stream(caller)
+                ids_out[k0], eo_out[k0] = ids, eo
+                continue
+            # a block: everything before it has finished when the replay starts (one drain)
+            for st in self.streams:
+                caller.wait_stream(st)
+            for i in range(cnt):
+                s = info[k0 + i]
+                self.g_feats[i][: s["len"] * enc.cfg.input_dim].view(s["len"], -1).copy_(s["x"])
+            key = (k0 % self.period, cnt)
+            g = self.graphs.get(key)
+            if g is None:
+                g = torch.cuda.CUDAGraph()
+                cap = self.streams[0]
+                cap.wait_stream(caller)
+                with torch.cuda.graph(g, stream=cap):
+                    for st in self.streams[1:]:
+                        st.wait_stream(cap)
+                    gp = None
+                    for i in range(cnt):
+                        s = dict(info[k0 + i])
+                        s["feats"] = self.g_feats[i]
+                        gp = self._segment(s, gp,
+                                           self.g_ids[i][: s["rows"]] if self.vocab > 0 else None,
+                                           self.g_eo[i][: s["rows"] * d].view(s["rows"], d) if self.want_out else None)
+                    for st in self.streams[1:]:
+                        cap.wait_stream(st)
+                self.graphs[key] = g
+                caller.wait_stream(cap)
+            g.replay()
+            self.replayed += cnt
+            for i in range(cnt):
+                rows = info[k0 + i]["rows"]
+                if self.vocab > 0 and rows > 0:
+                    ids_out[k0 + i] = self.g_ids[i][:rows].clone()
                 if self.want_out:
-                    eo_out[done] = eo.clone()
+                    eo_out[k0 + i] = self.g_eo[i][: rows * d].view(rows, d).clone()
+            for st in self.streams:
+                st.wait_stream(caller)
+            prev = None   # the next segment's layer waits are covered by the stream order
+        for st in self.streams:
+            caller.wait_stream(st)
         self._keep = info
         return ids_out, eo_out, n % 2

@@ -126,28 +126,21 @@ def test_cmvn_loaders_agree(tmp_path):
     np.testing.assert_allclose(a[1], b[1], rtol=1e-12)
 
 
-def test_endless_pipeline_schedule():
-    """EndlessGraphPipeline's software-pipeline schedule (host logic): the stage slots cover -1 ..
-    nb-1 once, in order; every segment runs every slot exactly once, slot s one tick after slot s-1,
-    and segment k's slot s one tick after segment k-1's (its carried layer caches)."""
-    from chunkformer_amd.streaming import pipeline_ticks, stage_slots
-    for nb in (2, 12):
-        for depth in (1, 2, 3, 4, 5, 13, 20):
-            slots = stage_slots(nb, depth)
-            flat = [st for lo, hi in slots for st in range(lo, hi + 1)]
-            assert flat == list(range(-1, nb))
-            assert len(slots) == min(depth, nb + 1)
-            for n in (1, 2, 3, 7):
-                ticks = pipeline_ticks(n, len(slots))
-                when = {}
-                for t, tick in enumerate(ticks):
-                    assert len({k for k, _ in tick}) == len(tick)   # a segment at most once per tick
-                    for k, s in tick:
-                        assert (k, s) not in when
-                        when[(k, s)] = t
-                assert len(when) == n * len(slots)
-                for (k, s), t in when.items():
-                    if s > 0:
-                        assert when[(k, s - 1)] == t - 1
-                    if k > 0:
-                        assert when[(k - 1, s)] == t - 1
+def test_endless_graph_blocks_schedule():
+    """EndlessGraphPipeline's schedule (host logic): every segment exactly once, in order; runs of
+    graph-eligible segments cut into replayed blocks of at most kmax, every other segment eager."""
+    import itertools
+    from chunkformer_amd.streaming import graph_blocks
+    for n in range(0, 9):
+        for flags in itertools.product([False, True], repeat=n):
+            for kmax in (1, 2, 3, 12):
+                blocks = graph_blocks(list(flags), kmax)
+                covered = [k for k0, cnt, _ in blocks for k in range(k0, k0 + cnt)]
+                assert covered == list(range(n))
+                for k0, cnt, replay in blocks:
+                    assert 1 <= cnt <= (kmax if replay else 1)
+                    assert all(flags[k] == replay for k in range(k0, k0 + cnt))
+                # maximal packing: two adjacent replayed blocks only where the first one is full
+                for (a0, ac, ar), (b0, bc, br) in zip(blocks, blocks[1:]):
+                    if ar and br:
+                        assert ac == kmax
