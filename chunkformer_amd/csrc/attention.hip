@@ -271,7 +271,9 @@ __global__ __launch_bounds__(512, 1) void chunk_attention_ring_kernel(
   float* uv = reinterpret_cast<float*>(vt + VT_BYTES_ + 8 * SCR_BYTES);   // [2][64]: pos_bias_u / v of head h
   const int h = blockIdx.y;
   const int d = H * 64;
-  const int c0 = blockIdx.x * nch, c1 = min(c0 + nch, n_chunks);
+  // balanced runs: block x of gridDim.x takes chunks [x n / gx, (x + 1) n / gx) of its head (nch unused)
+  const int c0 = (int)((long long)blockIdx.x * n_chunks / gridDim.x),
+            c1 = (int)((long long)(blockIdx.x + 1) * n_chunks / gridDim.x);
   if (c0 >= c1) return;
 
   // ---- zero the K / V^T rings (rows past a window's end are read as masked keys: p = 0 must not meet NaN)
@@ -597,9 +599,12 @@ int chunk_attention_masked_bf16(const bf16* q, const bf16* kv, int kv_rows, cons
   // (P rows + first window) per block instead of one per 8 chunks
   const int n_cu = cu_count();
   if (!reuse && (diag & 15) == 0) diag |= 5;   // "attn_reuse" 0: recompute the shared band subtile (A/B)
-  int nch = (int)(((long long)n_chunks * H + n_cu - 1) / n_cu);
-  nch = max(NCH, (nch + 1) & ~1);
-  const dim3 grid((n_chunks + nch - 1) / nch, H);
+  // one block per CU (CUs / H runs per head), each a balanced run of >= 2 chunks: a small launch (an
+  // endless_decode segment at tbd 1800: 199 chunks) still fills every CU (was: runs of >= NCH chunks,
+  // rounded to pairs -- 200 blocks on 256 CUs there)
+  const int gx = max(1, min(n_cu / max(H, 1), n_chunks / 2));
+  const int nch = (n_chunks + gx - 1) / gx;
+  const dim3 grid(gx, H);
 #define RING_L(DG_, NT_)                                                                                             \
   hipLaunchKernelGGL((chunk_attention_ring_kernel<DG_, NT_>), grid, dim3(512), 0, st, q, kv, kv_rows, P, p_rows, pos_u, \
                      pos_v, desc, n_chunks, H, C, W, out, diag, nch, p_ld)

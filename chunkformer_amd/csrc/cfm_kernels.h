@@ -34,6 +34,7 @@ struct EpiArgs {
   int diag = 0;                  // timing diagnostics of the bf16 kernels ("gemm_diag"; 0 = normal)
   int wst = 1;                   // K = 512 weight-stationary kernel ("gemm_wst")
   int small_tiles = 0;           // force the 128 x 128 kernel (cfm_op_gemm A/B)
+  int big_min_tiles = 0;         // 256 x 256 kernel only from this many tiles (fewer: the 128 x 128 kernel)
   // DW2 (front-end pw1 + ReLU + dw2, K = N = 512 weight-stationary only): dw2 taps tap-major [9][N]
   // f32, bias [N]; the pw1 rows are (window, t2 < t2n, f2 < 19); out = dw2 rows (window, t3 < t3n, f3 < 9)
   const float* dw_w = nullptr;
@@ -63,8 +64,11 @@ struct Tuning {
   // Default: FFN w2 (its y goes straight to the LayerNorm; bench A/B 52.2 -> 51.4 ms/step); nt on
   // the front-end pointwise outputs (+0.45 ms) or FFN w1's hidden (w1 slower) measured worse.
   int nt_sites = 8;   // SITE_FFN2
+  int big_min_tiles = 0;         // 256 x 256 tiles only from this many tiles ("gemm_big_min"; small launches:
+                                 // an endless segment's 12.7k rows are 100 tiles of 256 x 256 for 256 CUs)
   void apply(EpiArgs& e, int site = 0) const {
     e.diag = gemm_diag;
+    e.big_min_tiles = big_min_tiles;
     e.wst = gemm_wst;
     e.store_mode = (nt_sites & site) ? 2 : store_mode;
     e.col_group = col_group;

@@ -250,6 +250,7 @@ int gemm_bf16_big(int epi, int act, const bf16* A, int lda, const bf16* W, int l
     if (r != -1) return r;
   }
   if (N % 256 || K % 64 || lda % 8 || ldw % 8) return -1;
+  if (((M + 255) / 256) * (N / 256) < ep.big_min_tiles) return -1;   // too few tiles to fill the chip
   if (epi == EPI_GLU && ep.bias == nullptr) return -1;
   switch (epi) {
     case EPI_STORE:

@@ -703,7 +703,8 @@ cfm_status cfm_model_set_option(cfm_model* m, const char* key, int64_t value) {
         {"col_group", &m->tune.col_group}, {"attn_reuse", &m->tune.attn_reuse}, {"conv_dot2", &m->tune.conv_dot2},
         {"conv_dma", &m->tune.conv_dma},   {"dw2_seg", &m->tune.dw2_seg},   {"nt_sites", &m->tune.nt_sites},
         {"fe_fuse_dw2", &m->tune.fe_fuse_dw2},
-        {"attn128_var", &m->tune.attn128_var}, {"attn_q32", &m->tune.attn_q32}};
+        {"attn128_var", &m->tune.attn128_var}, {"attn_q32", &m->tune.attn_q32},
+        {"gemm_big_min", &m->tune.big_min_tiles}};
     for (auto& k : knobs)
       if (!std::strcmp(key, k.first)) { *k.second = (int)value; return CFM_OK; }
   }
