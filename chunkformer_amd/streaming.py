@@ -273,20 +273,21 @@ class EndlessGraphPipeline:
     replayed from HIP graphs (BASELINE configs[3]: context caches carried across graph-captured steps,
     several segments in flight).
 
-    A block of up to `block` consecutive middle segments (the same length and, once offset >= max(L, 7),
+    A block of up to `block` (64: a 16 h input at tbd 1800 is one block) consecutive middle segments (the same length and, once offset >= max(L, 7),
     the same plan: streaming.py's module note) is captured once as ONE graph holding the whole
     multi-stream pipeline of those segments -- every stage call, the per-layer cross-stream event
     edges, the CTC head and the copies of each segment's kept rows / ids into the block's output
     slots -- and replayed for every later block at the same phase (segment k uses stream, workspace and
     output slot k % depth and cache pair k % 2, so a block's graph depends on its first segment's
     phase k mod lcm(depth, 2) and its length).  Inside a replay the segments overlap exactly as in the
-    eager pipeline; a block's first segment starts after the previous block (one pipeline drain per
-    block of `block` segments, instead of one per tick).  The first segments (offset 0), the ragged
+    eager pipeline; a block's first segment starts after the previous block, so the pipeline drains
+    once per block (blocks of 12 at tbd 1800: 21.5 M frames/s against 22.1 M eager -- five drains; a
+    join after every tick of 3 segments: 18.0 M).  The first segments (offset 0), the ragged
     last one and short runs are launched eagerly through the same calls, so the result is
     bit-identical to the one-call-per-segment loop."""
 
     def __init__(self, encoder, C: int, L: int, R: int, trunc: int, seg_len: int, want_out: bool, depth: int = 3,
-                 block: int = 12):
+                 block: int = 64):
         if depth < 1:
             raise ValueError(f"pipeline depth {depth} < 1")
         self.enc = encoder
