@@ -285,7 +285,9 @@ def main():
                          "launched eagerly (pipeline), or one segment "
                          "at a time replaying one captured graph per middle segment (graph); all bit-identical "
                          "to the eager loop")
-    ap.add_argument("--pipeline-depth", type=int, default=3, help="endless pipeline: segments in flight")
+    ap.add_argument("--pipeline-depth", type=int, default=None,
+                    help="endless pipeline: segments in flight (default 4 for graphpipe, 3 for pipeline: the "
+                         "measured best of each at tbd 1800)")
     ap.add_argument("--tbd", type=int, default=7200,
                     help="endless: total_batch_duration (s); a memory budget that does not change results "
                          "(tests/test_gpu_model.py): 7200 s segments fill one MI355X better than the "
@@ -558,6 +560,7 @@ def bench_single(args):
     g = torch.Generator(device=dev).manual_seed(1234)
     d_, ff_ = LARGE.d_model, LARGE.ffn_dim
     if args.config == "endless":
+        depth = args.pipeline_depth if args.pipeline_depth is not None else (3 if args.endless_mode == "pipeline" else 4)
         T = int(args.hours * 3600 * 100)
         x = torch.randn(T, 80, generator=g, device=dev)
         frames = T
@@ -565,7 +568,7 @@ def bench_single(args):
         def step():
             return model.endless_decode(x, C, L, R, total_batch_duration=args.tbd, return_timestamps=False,
                                         pipeline=args.endless_mode in ("pipeline", "graphpipe"),
-                                        cuda_graph=args.endless_mode != "pipeline", pipeline_depth=args.pipeline_depth)
+                                        cuda_graph=args.endless_mode != "pipeline", pipeline_depth=depth)
         from chunkformer_amd.model import endless_segments
         trunc, segs = endless_segments(T, C, L, R, args.tbd, LARGE.num_blocks, LARGE.kernel_size)
         seg_len = max(b - a for a, b, _, _ in segs)
@@ -576,15 +579,15 @@ def bench_single(args):
         workload = (f"endless_decode over one {args.hours:g} h utterance (synthetic N(0,1) fbank), C=64 L=128 "
                     f"R=128, total_batch_duration={args.tbd}: {len(segs)} segments of <= {seg_len} frames "
                     f"(trunc {trunc} rows kept each), att/cnn caches carried, " +
-                    {"graphpipe": f"{args.pipeline_depth} segments in flight on as many HIP streams (segment k+1 "
+                    {"graphpipe": f"{depth} segments in flight on as many HIP streams (segment k+1 "
                                   "layer l after segment k layer l), each run of up to 64 middle segments one "
                                   "replay of a captured HIP graph of that whole multi-stream pipeline",
-                     "pipeline": f"{args.pipeline_depth} segments in flight on {args.pipeline_depth} HIP streams "
+                     "pipeline": f"{depth} segments in flight on {depth} HIP streams "
                                  "(segment k+1 layer l waits for segment k layer l), launched eagerly",
                      "graph": "middle segments replayed one at a time from one captured HIP graph (front-end + "
                               "12 blocks + after_norm + CTC argmax)"}[args.endless_mode])
         extra = {"segments": len(segs), "segment_frames": seg_len, "truncated_context_size": trunc,
-                 "endless_mode": args.endless_mode, "pipeline_depth": args.pipeline_depth}
+                 "endless_mode": args.endless_mode, "pipeline_depth": depth}
     else:
         B, T = args.batch, 3000
         xs = torch.randn(B, T, 80, generator=g, device=dev)

@@ -299,14 +299,16 @@ class ChunkFormerModel:
                        left_context_size: Optional[int] = 128, right_context_size: Optional[int] = 128,
                        total_batch_duration: int = 1800, return_timestamps: bool = True,
                        max_silence_duration: float = 0.5, return_encoder_out: bool = False,
-                       cuda_graph: bool = True, pipeline: Optional[bool] = None, pipeline_depth: int = 3):
+                       cuda_graph: bool = True, pipeline: Optional[bool] = None,
+                       pipeline_depth: Optional[int] = None):
         """chunkformer_model.py:321-459.  Segments of `total_batch_duration` seconds (halved,
         like the reference) go through forward_parallel_chunk with the attention/conv caches
         and `offset` carried; the CTC argmax runs per segment on the kept rows (row-wise, so
         identical to the reference's argmax over the concatenation).
         Returns text (with char_dict) or ids [1, T', 1] like the reference; with
         `return_encoder_out` also the concatenated encoder output [1, T', d] (fp32).
-        `pipeline` (default: on from 3 segments up): `pipeline_depth` segments in flight on as many
+        `pipeline` (default: on from 3 segments up): `pipeline_depth` (default 4 with graphs, 3 eager:
+        the measured best of each at tbd 1800) segments in flight on as many
         streams, segment k + 1's layer l waiting only for segment k's layer l; with `cuda_graph` runs of
         up to 64 middle segments replay one captured HIP graph of that whole multi-stream pipeline
         (EndlessGraphPipeline), without it every call is launched eagerly (EndlessPipeline).  pipeline=False: one segment at a time, the full-size
@@ -325,6 +327,8 @@ class ChunkFormerModel:
         want_eo = bool(return_encoder_out) or transducer   # the RNN-T search consumes the encoder rows
         if pipeline is None:
             pipeline = len(segs) >= 3
+        if pipeline_depth is None:
+            pipeline_depth = 4 if cuda_graph else 3
         key = (C, L, R, trunc, seg_len, want_eo, bool(cuda_graph), bool(pipeline), int(pipeline_depth))
         runner = self._endless_runners.get(key)
         if runner is None:   # graphs are captured once per segment geometry and reused across calls
