@@ -285,7 +285,7 @@ cfm_status cfm_rnnt_greedy(const cfm_rnnt* h, const float* enc_dev, int32_t rows
                            size_t workspace_bytes, cfm_stream stream);
 /* Options: "grid_lds" (default 1) caches each workgroup's weight slices in LDS when they fit;
  * "grid_atomic" (default 1) exchanges the shared vectors by agent-scope atomics instead of fences;
- * "grid_blocks" = workgroups per utterance of the multi-CU search (default 64; 0 = one
+ * "grid_blocks" = workgroups per utterance of the multi-CU search (default 32; 0 = one
  * workgroup per utterance always).  The multi-CU search runs when B <= 32 and B * grid_blocks <= the
  * device's CU count; cfm_rnnt_grid_blocks returns the workgroups per utterance a call with B
  * utterances uses (0: the one-workgroup kernel). */
