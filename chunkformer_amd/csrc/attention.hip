@@ -667,8 +667,15 @@ __global__ __launch_bounds__(512, 1) void full_attention_bf16_kernel(
   bf16* scr = reinterpret_cast<bf16*>(pl + FA_P_BYTES + w * SCR_BYTES);
   const unsigned scr_base = (unsigned)(size_t)(__attribute__((address_space(3))) char*)scr;
   float* uv = reinterpret_cast<float*>(pl + FA_P_BYTES + 8 * SCR_BYTES);
-  const int h = blockIdx.y, d = H * 64;
-  const int npair = (nd + 1) >> 1, u = blockIdx.x / npair, pr2 = blockIdx.x % npair;
+  // XCD-aware order: the dispatcher deals consecutive workgroups round-robin to the 8 XCDs, so the
+  // hardware index is remapped (bijectively) to give each XCD a contiguous run of (head, utterance,
+  // query-pair) items: the query pairs of one utterance x head -- which stage the same K / V rows --
+  // and the utterances of one head -- the same P rows -- share that XCD's L2
+  const int npair = (nd + 1) >> 1, gx = gridDim.x;
+  const int T = gx * gridDim.y, b = blockIdx.y * gx + blockIdx.x, xcd = b & 7, q8 = T >> 3, r8 = T & 7;
+  const int item = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b >> 3);
+  const int h = item / gx, d = H * 64;
+  const int u = (item - h * gx) / npair, pr2 = (item - h * gx) % npair;
   const int dix = u * nd + 2 * pr2 + half;
   const bool has = 2 * pr2 + half < nd;
   const int32_t* D0 = desc + (size_t)(u * nd + 2 * pr2) * AD_INTS;
