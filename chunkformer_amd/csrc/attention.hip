@@ -684,11 +684,21 @@ __global__ __launch_bounds__(512, 1) void full_attention_bf16_kernel(
   const int q_row0 = D[AD_Q_ROW0], nq = D[AD_NQ], p_base = D[AD_P_BASE], q_valid = D[AD_Q_VALID];
   const int pb0 = D0[AD_P_BASE] - 127;   // P row of LDS row 0
 
+  // ---- phase 1: the P rows pb0 .. straight into LDS by LDS-DMA (wave w, instruction i fills rows
+  // 8 (8 i + w) .. +7 lane-linearly, the row's 16-B chunk swizzle applied on the source address; rows
+  // outside [0, p_rows) are clamped: they reach masked scores only), then every global load of the
+  // thread (K, and V for phase 2), then the K stores
+#pragma unroll
+  for (int i = 0; i < FA_PROWS / 64; ++i) {
+    const int r = 8 * (8 * i + w) + (lane >> 3), ch = (lane & 7) ^ ((r >> 1) & 7);
+    const int prow = min(max(pb0 + r, 0), p_rows - 1);
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(P + (size_t)prow * p_ld + h * 64 + ch * 8),
+                                     (__attribute__((address_space(3))) void*)(pl + 8 * (8 * i + w) * 128), 16, 0, 0);
+  }
   if (tid < 128) uv[tid] = (tid < 64 ? pos_u : pos_v)[h * 64 + (tid & 63)];
-  // ---- phase 1: issue every global load of the thread (K, P, and V for phase 2), then the stores
-  constexpr int KIT = FA_KEYS * 8 / 512, PIT = FA_PROWS * 8 / 512, VIT = (FA_KEYS / 2) * 8 / 512;
-  static_assert(FA_KEYS * 8 % 512 == 0 && FA_PROWS * 8 % 512 == 0 && (FA_KEYS / 2) * 8 % 512 == 0, "staging");
-  u32x4 sk[KIT], sp[PIT], sv0[VIT], sv1[VIT];
+  constexpr int KIT = FA_KEYS * 8 / 512, VIT = (FA_KEYS / 2) * 8 / 512;
+  static_assert(FA_KEYS * 8 % 512 == 0 && FA_PROWS % 64 == 0 && (FA_KEYS / 2) * 8 % 512 == 0, "staging");
+  u32x4 sk[KIT], sv0[VIT], sv1[VIT];
   const u32x4 z4 = (u32x4){0u, 0u, 0u, 0u};
 #pragma unroll
   for (int it = 0; it < VIT; ++it) {   // V rows: two keys x one 16-B chunk (zero past key_hi: p = 0 x finite)
@@ -708,21 +718,11 @@ __global__ __launch_bounds__(512, 1) void full_attention_bf16_kernel(
                         : z4;
   }
 #pragma unroll
-  for (int it = 0; it < PIT; ++it) {   // P rows pb0 .. (zero outside [0, p_rows): they reach masked scores only)
-    const int idx = tid + 512 * it, r = idx >> 3, ch = idx & 7, prow = pb0 + r;
-    sp[it] = prow >= 0 && prow < p_rows ? *reinterpret_cast<const u32x4*>(P + (size_t)prow * p_ld + h * 64 + ch * 8)
-                                        : z4;
-  }
-#pragma unroll
   for (int it = 0; it < KIT; ++it) {
     const int idx = tid + 512 * it;
     *reinterpret_cast<u32x4*>(kr + sw128(idx >> 3, idx & 7)) = sk[it];
   }
-#pragma unroll
-  for (int it = 0; it < PIT; ++it) {
-    const int idx = tid + 512 * it;
-    *reinterpret_cast<u32x4*>(pl + sw128(idx >> 3, idx & 7)) = sp[it];
-  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the P rows (LDS-DMA) have landed
   __syncthreads();
 
   const int i0 = wq * 16;
