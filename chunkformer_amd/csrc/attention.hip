@@ -244,6 +244,9 @@ CFM_DEV unsigned pack_bf16x2_a(float a, float b) {
   return __builtin_bit_cast(unsigned, (b2){(bf16)a, (bf16)b});
 }
 CFM_DEV int sw128(int row, int ch) { return row * 128 + ((ch ^ ((row >> 1) & 7)) << 4); }
+#ifndef RING_KPF
+#define RING_KPF 1   // ring kernel, interior chunks: next tile's K fragments read before this tile's skew
+#endif
 #ifndef ATTN_STORE16
 #define ATTN_STORE16 1   // ring kernel output as 16-B stores after permlane swaps (A/B: 0 = 8-B stores)
 #endif
@@ -407,6 +410,19 @@ __global__ __launch_bounds__(512, 1) void chunk_attention_ring_kernel(
         f32x4 S[NTT][4];
         f32x4 band_next = (f32x4){0.f, 0.f, 0.f, 0.f};
         float mx = -INFINITY;
+        // RING_KPF (interior chunks): tile t + 1's K fragments are read right after tile t's band
+        // MFMAs, so their LDS latency overlaps tile t's skew round trip
+        bf16x8 kf_next[4][2];
+        auto load_kf = [&](int t, bf16x8 (&kf)[4][2]) {
+#pragma unroll
+          for (int st = 0; st < 4; ++st) {
+            const char* kb_ = kr + ring16(jb + 64 * t + 16 * st) * 128;
+#pragma unroll
+            for (int s = 0; s < 2; ++s) kf[st][s] = *reinterpret_cast<const bf16x8*>(kb_ + frag_lane[s]);
+          }
+        };
+        constexpr bool KPF = RING_KPF && !MASK;
+        if constexpr (KPF) load_kf(0, kf_next);
 #pragma unroll
         for (int t = 0; t < NTT; ++t) {
           const int j0 = jb + 64 * t;
@@ -429,11 +445,11 @@ __global__ __launch_bounds__(512, 1) void chunk_attention_ring_kernel(
 #pragma unroll
             for (int s = 0; s < 2; ++s) pf[pt][s] = *reinterpret_cast<const bf16x8*>(pb_ + frag_lane[s]);
           }
+          if constexpr (KPF) {
 #pragma unroll
-          for (int st = 0; st < 4; ++st) {
-            const char* kb_ = kr + ring16(j0 + 16 * st) * 128;
-#pragma unroll
-            for (int s = 0; s < 2; ++s) kf[st][s] = *reinterpret_cast<const bf16x8*>(kb_ + frag_lane[s]);
+            for (int st = 0; st < 4; ++st) { kf[st][0] = kf_next[st][0]; kf[st][1] = kf_next[st][1]; }
+          } else {
+            load_kf(t, kf);
           }
           // band^T[P row kb0 + 16pt + 4g + rr][query fr], pt = 0..4 (80 rows for 64 keys + 15 skew); the
           // two 32-key halves use subtiles 0-2 and 2-4 -> scratch[query][band pos] (16 x 48 bf16 per wave)
@@ -450,6 +466,9 @@ __global__ __launch_bounds__(512, 1) void chunk_attention_ring_kernel(
             band[pt] = a;
           }
           band_next = band[4];
+          if constexpr (KPF) {
+            if (t + 1 < NTT) load_kf(t + 1, kf_next);
+          }
 #pragma unroll
           for (int hh = 0; hh < 2; ++hh) {
 #pragma unroll
