@@ -610,7 +610,8 @@ __global__ __launch_bounds__(512, 1) void chunk_attention_ring_kernel(
 // returns -1 when the shape is not eligible for the ring kernel
 int chunk_attention_masked_bf16(const bf16* q, const bf16* kv, int kv_rows, const bf16* P, int p_rows,
                                 const float* pos_u, const float* pos_v, const int32_t* desc, int n_chunks, int H,
-                                int C, int W, bf16* out, hipStream_t st, int diag, int p_ld, int reuse) {
+                                int C, int W, bf16* out, hipStream_t st, int diag, int p_ld, int reuse,
+                                int min_chunks) {
   if (p_ld <= 0) p_ld = H * 64;
   // W <= 320: a query's scores are 5 tiles of 64 keys held in registers (exact softmax)
   if (C <= 0 || C > 64 || (C % 16) || (W & 1) || W > 320 || W + C > RING || p_rows > RING || n_chunks <= 0) return -1;
@@ -621,7 +622,7 @@ int chunk_attention_masked_bf16(const bf16* q, const bf16* kv, int kv_rows, cons
   // one block per CU (CUs / H runs per head), each a balanced run of >= 2 chunks: a small launch (an
   // endless_decode segment at tbd 1800: 199 chunks) still fills every CU (was: runs of >= NCH chunks,
   // rounded to pairs -- 200 blocks on 256 CUs there)
-  const int gx = max(1, min(n_cu / max(H, 1), n_chunks / 2));
+  const int gx = max(1, min(n_cu / max(H, 1), n_chunks / max(2, min_chunks)));
   const int nch = (n_chunks + gx - 1) / gx;
   const dim3 grid(gx, H);
 #define RING_L(DG_, NT_)                                                                                             \

@@ -377,7 +377,7 @@ struct ModelT : public cfm_model {
           if (r == -1 && masked && use_ring_attention && dk == 64)
             r = chunk_attention_masked_bf16(w.q, w.kv, kv_rows, w.P + (size_t)l * d, p_rows, Lw.pu, Lw.pv,
                                             attd, natt, H, C, hh[PH_L] + C + hh[PH_R], w.ao, st, attn_diag, p_ld,
-                                            tune.attn_reuse);
+                                            tune.attn_reuse, tune.attn_min_chunks);
           else if (w.vt) {   // head_dim 128 (4-head d=512): V^T copy, then the band / score / P.V kernel
             KCHK(vt_transpose_bf16(w.kv, kv_rows, H, w.vt, w.vt_ld, st));
             r = chunk_attention_masked_a128(w.q, w.kv, kv_rows, w.vt, w.vt_ld, w.P + (size_t)l * d, p_rows, p_ld,
@@ -704,7 +704,8 @@ cfm_status cfm_model_set_option(cfm_model* m, const char* key, int64_t value) {
         {"conv_dma", &m->tune.conv_dma},   {"dw2_seg", &m->tune.dw2_seg},   {"nt_sites", &m->tune.nt_sites},
         {"fe_fuse_dw2", &m->tune.fe_fuse_dw2},
         {"attn128_var", &m->tune.attn128_var}, {"attn_q32", &m->tune.attn_q32},
-        {"gemm_big_min", &m->tune.big_min_tiles}};
+        {"gemm_big_min", &m->tune.big_min_tiles}, {"wsp_small_div", &m->tune.wsp_small_div},
+        {"attn_min_chunks", &m->tune.attn_min_chunks}};
     for (auto& k : knobs)
       if (!std::strcmp(key, k.first)) { *k.second = (int)value; return CFM_OK; }
   }
