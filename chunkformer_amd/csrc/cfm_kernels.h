@@ -35,8 +35,9 @@ struct EpiArgs {
   int wst = 1;                   // K = 512 weight-stationary kernel ("gemm_wst")
   int small_tiles = 0;           // force the 128 x 128 kernel (cfm_op_gemm A/B)
   int big_min_tiles = 0;         // 256 x 256 kernel only from this many tiles (fewer: the 128 x 128 kernel)
-  int wsp_small_div = 1;         // weight-stationary kernel below 32k rows: grid = CUs / this (leaves CUs to
-                                 // the other streams of a pipelined caller)
+  int wsp_small_div = 1;         // weight-stationary kernel below wsp_small_rows rows: grid = CUs / this
+                                 // (leaves CUs to the other streams of a pipelined caller)
+  int wsp_small_rows = 32768;
   // DW2 (front-end pw1 + ReLU + dw2, K = N = 512 weight-stationary only): dw2 taps tap-major [9][N]
   // f32, bias [N]; the pw1 rows are (window, t2 < t2n, f2 < 19); out = dw2 rows (window, t3 < t3n, f3 < 9)
   const float* dw_w = nullptr;
@@ -68,12 +69,14 @@ struct Tuning {
   int nt_sites = 8;   // SITE_FFN2
   int big_min_tiles = 0;         // 256 x 256 tiles only from this many tiles ("gemm_big_min"; small launches:
                                  // an endless segment's 12.7k rows are 100 tiles of 256 x 256 for 256 CUs)
-  int wsp_small_div = 1;         // "wsp_small_div" (see EpiArgs)
+  int wsp_small_div = 1;         // "wsp_small_div" / "wsp_small_rows" (see EpiArgs)
+  int wsp_small_rows = 32768;
   int attn_min_chunks = 2;       // ring attention: chunks per block at least this ("attn_min_chunks")
   void apply(EpiArgs& e, int site = 0) const {
     e.diag = gemm_diag;
     e.big_min_tiles = big_min_tiles;
     e.wsp_small_div = wsp_small_div;
+    e.wsp_small_rows = wsp_small_rows;
     e.wst = gemm_wst;
     e.store_mode = (nt_sites & site) ? 2 : store_mode;
     e.col_group = col_group;

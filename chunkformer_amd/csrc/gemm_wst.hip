@@ -801,7 +801,7 @@ static int launch_wst(const bf16* A, int lda, const bf16* W, int ldw, int M, int
   int n_cu = cu_count() / 8 * 8;
   // small launches in a pipelined caller (endless_decode's segments): fewer workgroups, each taking
   // more row tiles per weight-tile fill, and CUs left to the other streams' kernels
-  if (ep.wsp_small_div > 1 && M < 32768) n_cu = max(8 * (N >> 8), n_cu / ep.wsp_small_div / 8 * 8);
+  if (ep.wsp_small_div > 1 && M < ep.wsp_small_rows) n_cu = max(8 * (N >> 8), n_cu / ep.wsp_small_div / 8 * 8);
   // buffer descriptors are built per 64-row tile on 64-bit bases (offsets inside one tile stay
   // below 64 rows x ld), so outputs past 2 GiB (a 980-minute batch's FFN hidden: 3 GB) stay here
 #define WSP_LAUNCH(D) hipLaunchKernelGGL((gemm_wsp_kernel<EPI, ACT, D>), dim3(n_cu), dim3(256), 0, st, A, lda, W, ldw, M, N, ep)

@@ -705,6 +705,7 @@ cfm_status cfm_model_set_option(cfm_model* m, const char* key, int64_t value) {
         {"fe_fuse_dw2", &m->tune.fe_fuse_dw2},
         {"attn128_var", &m->tune.attn128_var}, {"attn_q32", &m->tune.attn_q32},
         {"gemm_big_min", &m->tune.big_min_tiles}, {"wsp_small_div", &m->tune.wsp_small_div},
+        {"wsp_small_rows", &m->tune.wsp_small_rows},
         {"attn_min_chunks", &m->tune.attn_min_chunks}};
     for (auto& k : knobs)
       if (!std::strcmp(key, k.first)) { *k.second = (int)value; return CFM_OK; }
