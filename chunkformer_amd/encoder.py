@@ -16,6 +16,7 @@ torch's current stream.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import weakref
 from typing import Dict, List, Optional, Tuple
@@ -72,6 +73,7 @@ class ChunkFormerEncoder:
         # with the other group's, which hides its own roofline (FFN w1 0.37 ms -> 0.29 ms at half the rows)
         self.stream_split = 1
         self.split_min_chunks = 1024
+        self._native_opts: dict = {}
         self._split_streams: List[torch.cuda.Stream] = []
         self._split_ws: List[Optional[torch.Tensor]] = []
         # destroy the native handle when this object is collected or at interpreter exit (a finalizer
@@ -88,6 +90,26 @@ class ChunkFormerEncoder:
             setattr(self, key, int(value))
             return
         _lib.check(_lib.cfm_model_set_option(self._h, key.encode(), int(value)))
+        self._native_opts[key] = int(value)
+
+    # the native options' values before any set_option (csrc/cfm_kernels.h Tuning)
+    _NATIVE_DEFAULTS = {"wsp_small_div": 1, "wsp_small_rows": 32768, "attn_min_chunks": 2}
+
+    @contextlib.contextmanager
+    def scoped_options(self, **opts):
+        """Native options for the duration of a with-block (launch parameters only: results are the
+        same), then the previous values; options the caller set explicitly are left alone."""
+        keep = {k: self._native_opts.get(k, self._NATIVE_DEFAULTS[k]) for k in opts}
+        explicit = {k for k in opts if k in self._native_opts}
+        for k, v in opts.items():
+            if k not in explicit:
+                _lib.check(_lib.cfm_model_set_option(self._h, k.encode(), int(v)))
+        try:
+            yield
+        finally:
+            for k in opts:
+                if k not in explicit:
+                    _lib.check(_lib.cfm_model_set_option(self._h, k.encode(), int(keep[k])))
 
     # ------------------------------------------------------------------ helpers
     def _workspace(self, nbytes: int) -> torch.Tensor:

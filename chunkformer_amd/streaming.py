@@ -149,6 +149,14 @@ class EndlessGraphRunner:
         return ids, (eo if self.want_out else None), eo.shape[0]
 
 
+# Launch parameters while several segments are in flight (each launch then shares the chip with the
+# other streams' kernels): the K = 512 weight-stationary GEMMs of a segment (< 32k rows) on a quarter
+# of the CUs (each workgroup then takes 4x the row tiles per weight-tile fill), ring attention runs of
+# >= 16 chunks per workgroup.  tbd 1800, 16 h (same box): graph pipeline 22.2 -> 23.9 M frames/s, eager
+# pipeline 22.2 -> 23.3 M; tbd 7200 segments (45k rows) are not affected.
+PIPELINE_OPTS = {"wsp_small_div": 4, "attn_min_chunks": 16}
+
+
 class EndlessPipeline:
     """endless_decode's segments with `depth` in flight (MI355X streams, no graph): segment k runs on
     stream k % depth and its encoder layer l waits only for segment k - 1's layer l (the attention /
@@ -189,7 +197,11 @@ class EndlessPipeline:
     def run(self, xs_dev: torch.Tensor, segs):
         """Returns (per-segment CTC ids of the kept rows, per-segment kept encoder rows or None,
         index of the cache pair holding the caches after the last segment); the tensors are ready on
-        the caller's current stream."""
+        the caller's current stream.  Launch parameters for segments in flight: PIPELINE_OPTS."""
+        with self.enc.scoped_options(**PIPELINE_OPTS):
+            return self._run(xs_dev, segs)
+
+    def _run(self, xs_dev: torch.Tensor, segs):
         enc, C, L, R = self.enc, self.C, self.L, self.R
         nb, d = enc.cfg.num_blocks, enc.cfg.d_model
         self.att[0].zero_()
@@ -356,7 +368,12 @@ class EndlessGraphPipeline:
 
     def run(self, xs_dev: torch.Tensor, segs):
         """Returns (per-segment CTC ids of the kept rows, per-segment kept encoder rows or None, index of
-        the cache pair holding the caches after the last segment), ready on the caller's stream."""
+        the cache pair holding the caches after the last segment), ready on the caller's stream.
+        Launch parameters for segments in flight: PIPELINE_OPTS (baked into the captured graphs)."""
+        with self.enc.scoped_options(**PIPELINE_OPTS):
+            return self._run(xs_dev, segs)
+
+    def _run(self, xs_dev: torch.Tensor, segs):
         enc, C, L, R, D = self.enc, self.C, self.L, self.R, self.depth
         d = enc.cfg.d_model
         self.replayed = 0
