@@ -123,6 +123,25 @@ def test_golden_utterances_inside_bench_batch(large, dtype, minutes):
         assert total >= 0.99
 
 
+@pytest.mark.parametrize("opts", [{"wsp_small_div": 4, "attn_min_chunks": 16},
+                                  {"wsp_small_div": 2, "wsp_small_rows": 1 << 30, "attn_min_chunks": 64},
+                                  {"wsp_small_div": 8, "wsp_small_rows": 1 << 30}])
+def test_launch_parameters_bit_identical(large, opts):
+    """The pipelined endless_decode's launch parameters (streaming.PIPELINE_OPTS: fewer workgroups for
+    the weight-stationary GEMMs, longer attention runs) only regroup the same per-row / per-chunk
+    work: a 30-min masked batch is bit-identical to the default launches (here forced at every size)."""
+    g, _, models = large
+    enc = models["bf16"]
+    xs, _ = _embedded_batch(g, 30, enc.device)
+    lens = torch.tensor([x.shape[0] for x in xs], dtype=torch.int32)
+    ref = enc.forward_parallel_chunk(xs, lens, 64, 128, 128)[0].clone()
+    with enc.scoped_options(**opts):
+        out = enc.forward_parallel_chunk(xs, lens, 64, 128, 128)[0]
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)
+    assert torch.equal(enc.forward_parallel_chunk(xs, lens, 64, 128, 128)[0], ref)   # restored
+
+
 @pytest.mark.parametrize("dtype,minutes,parts", [("bf16", 240, 2), ("fp32", 60, 3)])
 def test_stream_split_bit_identical(large, dtype, minutes, parts):
     """forward_parallel_chunk runs a large masked batch as utterance groups on separate streams,
