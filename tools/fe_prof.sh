@@ -1,3 +1,5 @@
+# PMC passes (wave states, LDS instructions / bank conflicts, VALU) over one encoder layer of the bench
+# workload (tools/layer_bench.py), for the front-end kernels.  bash tools/fe_prof.sh  (via gpurun)
 set -e
 cd /tmp && export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
