@@ -44,8 +44,7 @@ struct RnntDev {
   const float* embed;                     // [V, E]
   const float* wg[RNNT_MAXL];             // [(in_l + H), 4H]: W_ih^T rows then W_hh^T rows
   const float* bg[RNNT_MAXL];             // [4H] b_ih + b_hh
-  const float *wp, *bp;                   // [H, P], [P]
-  const float *wpj, *bpj;                 // [P, J], [J]
+  const float *wp, *bp;                   // [H, J], [J]: projection and pred_ffn composed (P = J)
   const float *wo, *bo;                   // [J, Vp] (zero-padded columns), [Vp] (padding -inf)
   int V, Vp, E, H, nl, P, J, blank;
 };
@@ -117,8 +116,7 @@ CFM_DEV void predictor(const RnntDev& w, int tok, const float* h, const float* c
     __syncthreads();
     in = H;
   }
-  matvec(w.wp, H, w.P, xin, w.bp, pvec, red, tid);
-  matvec(w.wpj, w.P, w.J, pvec, w.bpj, pj, red, tid);
+  matvec(w.wp, H, w.J, xin, w.bp, pj, red, tid);   // composed projection + pred_ffn (cfm_rnnt_create)
 }
 
 __global__ __launch_bounds__(RNNT_NT) void rnnt_greedy_kernel(RnntDev w, const float* __restrict__ enc_proj,
@@ -243,8 +241,8 @@ __global__ __launch_bounds__(RNNT_NT) void rnnt_greedy_kernel(RnntDev w, const f
 // through ONE CU per emission.  rnnt_grid_kernel runs G workgroups per utterance instead; each owns a
 // fixed slice of every matrix-vector product's outputs (LSTM units with their four gates, projection
 // and pred_ffn outputs, vocabulary columns), stored block-major so a workgroup's slice is one
-// contiguous, coalesced stream.  The phases of an emission (nl LSTM layers, projection, pred_ffn, the
-// joint's candidates) are separated by grid barriers on per-utterance flag words; the shared vectors
+// contiguous, coalesced stream.  The phases of an emission (nl LSTM layers, the composed projection +
+// pred_ffn, the joint's candidates) are separated by grid barriers on per-utterance flag words; the shared vectors
 // (h / c state slots, projection and pred_ffn outputs, per-workgroup argmax candidates) live in the
 // workspace.  Every workgroup reduces the candidates in the same order, so all of them take the same
 // decisions and leave the loop together.  A barrier that does not complete within ~2^21 polls sets
@@ -256,7 +254,7 @@ constexpr int RG_MAXG = 256;   // workgroups per utterance
 struct RnntGrid {
   const float4* wg[RNNT_MAXL];  // per layer, block-major [K_l][n_b] slices of gate quads (i, f, g, o of a unit)
   const float4* bg[RNNT_MAXL];  // [H] gate-quad biases (b_ih + b_hh)
-  const float4 *wp, *wpj, *wo;  // block-major slices of the projection, pred_ffn, ffn_out float4 columns
+  const float4 *wp, *wo;        // block-major slices of the composed projection + pred_ffn and ffn_out columns
   int G;
 };
 
@@ -437,15 +435,13 @@ __global__ __launch_bounds__(RG_NT) void rnnt_grid_kernel(RnntDev w, RnntGrid gw
   auto sync = [&]() { return rg_barrier<ATOM>(flags, G, part, ++epoch, err, lflag); };
 
   // this workgroup's output ranges and weight slices
-  int u0, nu, pg0, pn, jg0, jn, v0, nv;
+  int u0, nu, pg0, pn, v0, nv;
   rg_range(H, G, part, u0, nu);
-  rg_range(P >> 2, G, part, pg0, pn);
-  rg_range(J >> 2, G, part, jg0, jn);
+  rg_range(P >> 2, G, part, pg0, pn);   // (P = J: the composed projection + pred_ffn)
   rg_range(w.Vp >> 2, G, part, v0, nv);
   const float4* sl_wp = gw.wp + (size_t)H * pg0;
-  const float4* sl_wpj = gw.wpj + (size_t)P * jg0;
   const float4* sl_wo = gw.wo + (size_t)J * v0;
-  float4* wcache = reinterpret_cast<float4*>(lds + rnnt_grid_lds_bytes(w) / 4);   // [layers][wp][wpj][wo]
+  float4* wcache = reinterpret_cast<float4*>(lds + rnnt_grid_lds_bytes(w) / 4);   // [layers][wp][wo]
   if constexpr (LDSW) {
     float4* c = wcache;
     auto copy = [&](const float4* src, size_t n4) {
@@ -459,8 +455,6 @@ __global__ __launch_bounds__(RG_NT) void rnnt_grid_kernel(RnntDev w, RnntGrid gw
     }
     copy(sl_wp, (size_t)H * pn);
     sl_wp = c - (size_t)H * pn;
-    copy(sl_wpj, (size_t)P * jn);
-    sl_wpj = c - (size_t)P * jn;
     copy(sl_wo, (size_t)J * nv);
     sl_wo = c - (size_t)J * nv;
     __syncthreads();
@@ -502,19 +496,7 @@ __global__ __launch_bounds__(RG_NT) void rnnt_grid_kernel(RnntDev w, RnntGrid gw
       __syncthreads();
       const int g0 = pg0, n = pn;
       const float4* b4 = reinterpret_cast<const float4*>(w.bp);
-      rg_matvec(sl_wp, H, n, x, red, [&](int jj, float4 a) {
-        const float4 b = b4[g0 + jj];
-        float* o = pvec + 4 * (g0 + jj);
-        sh_st<ATOM>(o, a.x + b.x); sh_st<ATOM>(o + 1, a.y + b.y); sh_st<ATOM>(o + 2, a.z + b.z); sh_st<ATOM>(o + 3, a.w + b.w);
-      });
-      if (!sync()) return false;
-    }
-    {
-      rg_fetch<ATOM>(x, pvec, P);
-      __syncthreads();
-      const int g0 = jg0, n = jn;
-      const float4* b4 = reinterpret_cast<const float4*>(w.bpj);
-      rg_matvec(sl_wpj, P, n, x, red, [&](int jj, float4 a) {
+      rg_matvec(sl_wp, H, n, x, red, [&](int jj, float4 a) {   // composed projection + pred_ffn
         const float4 b = b4[g0 + jj];
         float* o = pj + 4 * (g0 + jj);
         sh_st<ATOM>(o, a.x + b.x); sh_st<ATOM>(o + 1, a.y + b.y); sh_st<ATOM>(o + 2, a.z + b.z); sh_st<ATOM>(o + 3, a.w + b.w);
@@ -657,7 +639,7 @@ struct cfm_rnnt {
   cfm::RnntGrid gw{};
   std::vector<std::vector<float>> host_wg;    // [(in_l + H)][4H] transposed gate weights per layer
   std::vector<std::vector<float>> host_bg;    // [4H]
-  std::vector<float> host_wp, host_wpj, host_wo;   // [H][P], [P][J], [J][Vp]
+  std::vector<float> host_wp, host_wo;   // [H][J] (projection + pred_ffn composed), [J][Vp]
   ~cfm_rnnt() {
     (void)hipSetDevice(device);
     if (dev_mem) (void)hipFree(dev_mem);
@@ -733,7 +715,6 @@ int rnnt_grid_build(cfm_rnnt* h) {
     });
   };
   put(cols(h->host_wp, H, w.P), &h->gw.wp);
-  put(cols(h->host_wpj, w.P, w.J), &h->gw.wpj);
   put(cols(h->host_wo, w.J, w.Vp), &h->gw.wo);
   if (hipSetDevice(h->device) != hipSuccess || hipMalloc(&h->grid_mem, img.size() * 4) != hipSuccess ||
       hipMemcpy(h->grid_mem, img.data(), img.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
@@ -805,14 +786,34 @@ cfm_status cfm_rnnt_create(const cfm_rnnt_config* cfg, const cfm_tensor_view* we
       h->host_wg.push_back(std::move(a));
       h->host_bg.push_back(std::move(bias));
     }
-    h->host_wp = transpose(get("predictor.projection.weight", (int64_t)P * H), P, H, P);
-    img.put(h->host_wp, &w.wp);
+    // projection (predictor.py:204) and the joint's pred_ffn (joint.py:86) are consecutive Linear
+    // layers with nothing between them: composed once here (f64 products, f32 result) into one
+    // [J, H] matrix, so an emission's predictor runs one matrix-vector product fewer (and the
+    // multi-CU search one grid barrier fewer)
+    const float* wpm = get("predictor.projection.weight", (int64_t)P * H);
     const float* bp = get("predictor.projection.bias", P);
-    img.put(std::vector<float>(bp, bp + P), &w.bp);
-    h->host_wpj = transpose(get("joint.pred_ffn.weight", (int64_t)J * P), J, P, J);
-    img.put(h->host_wpj, &w.wpj);
+    const float* wpjm = get("joint.pred_ffn.weight", (int64_t)J * P);
     const float* bpj = get("joint.pred_ffn.bias", J);
-    img.put(std::vector<float>(bpj, bpj + J), &w.bpj);
+    std::vector<float> wc((size_t)J * H), bc(J);
+    {
+      std::vector<double> row(H);
+      for (int j = 0; j < J; ++j) {
+        std::fill(row.begin(), row.end(), 0.0);
+        double b = bpj[j];
+        for (int q = 0; q < P; ++q) {
+          const double a = wpjm[(size_t)j * P + q];
+          const float* src = wpm + (size_t)q * H;
+          for (int k = 0; k < H; ++k) row[k] += a * src[k];
+          b += a * bp[q];
+        }
+        for (int k = 0; k < H; ++k) wc[(size_t)j * H + k] = (float)row[k];
+        bc[j] = (float)b;
+      }
+    }
+    w.P = J;   // the composed product's width: pvec is the pred_ffn output
+    h->host_wp = transpose(wc.data(), J, H, J);   // [H][J]
+    img.put(h->host_wp, &w.wp);
+    img.put(bc, &w.bp);
     h->host_wo = transpose(get("joint.ffn_out.weight", (int64_t)V * J), V, J, w.Vp);
     img.put(h->host_wo, &w.wo);
     const float* bo = get("joint.ffn_out.bias", V);
