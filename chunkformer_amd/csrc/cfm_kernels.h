@@ -57,6 +57,8 @@ struct Tuning {
   int conv_dot2 = 2;             // conv module: bf16 dot2 kernel in half-chunk blocks (1: one block per chunk, 0: per-tap f32)
   int conv_dma = 1;              // conv module: LDS-DMA window staging (0: register staging)
   int dw2_seg = 4;               // front-end dw2: row segments per walk
+  int fe_conv = 1;               // bf16 front-end conv0+dw1: 1 = position-stationary (dw1 on VALU), 2 + k = channel-
+                                 // stationary with dw1 on MFMA
   int fe_fuse_dw2 = 1;           // front-end: pw1 + ReLU + dw2 in one weight-stationary GEMM (bf16; bench A/B
                                  // 50.85 -> 50.15 ms/step, 3 interleaved pairs; 0 = pw1 GEMM + fe_dw2_kernel)
   int attn128_var = 1;           // head_dim 128 attention kernel variant (A/B)
@@ -159,9 +161,11 @@ template <typename T>
 int frontend_conv0_dw(const float* feats, const float* const* tab, int step, const int32_t* meta, int meta_stride,
                       int nwin, int W,
                       const float* cmvn_mean, const float* cmvn_istd, const float* w0, const float* b0,
-                      const float* w1, const float* b1, const float* wpack, int d, T* out, hipStream_t st);
+                      const float* w1, const float* b1, const float* wpack, const float* wfrag, int d, T* out,
+                      hipStream_t st, int var = 1);
 // per-channel [w0 taps 0..8 | w1 taps 0..8 | b0 | b1 | pad 2] (FE_WPACK floats) for the bf16 MFMA front-end
 constexpr int FE_WPACK = 24;
+constexpr int FE2_NFRAG = 23;   // per-lane 16-B fragments of one 32-channel tile (channel-stationary front-end)
 template <typename T>
 int frontend_dw2(const T* in, int nwin, int T2, int d, const float* w, const float* b, T* out, hipStream_t st,
                  int seg = 4);

@@ -243,6 +243,234 @@ __global__ __launch_bounds__(256, 3) void fe_conv0_dw_mfma_kernel(const float* _
   }
 }
 
+// bf16 mode, channel-stationary (the default, "fe_conv" 2): dw1 on MFMA as well.  Each wave owns
+// 32 channels for a run of FE2_POS-position chunks, so its weights are loop-invariant registers.
+//  - conv0 is computed transposed, X^T[channel][position] = W0 . im2col (A = the wave's W0 rows with
+//    b0 at k = 9, B = the position's conv0 patch), so its accumulator has the position on the lane
+//    and 16 channels in registers;
+//  - ReLU + bf16 rounding (autocast rounds conv0's output to bf16 too) turn registers 8t..8t+7 into
+//    the B operand of k-step t of a second 32x32x16 MFMA with no lane movement: k = 8h + j holds
+//    channel 16t + 8(j>>2) + 4h + (j&3);
+//  - dw1 is that MFMA against a diagonal A (row c: w1[c][s] at its own channel's k), accumulated
+//    over the 9 taps on top of a b1-seeded accumulator.
+// Per tap and 32x32 tile: 3 MFMAs (96 cycles) and 16 packed VALU ops (8 cvt_pk + 8 pk_max_i16),
+// against 1 MFMA and 32 f32 VALU ops (max + fma per value) in the kernel above.
+// conv0 patches are built once per chunk as bf16 im2col rows in LDS (taps 0..7 in the "lo" image,
+// tap 8 + 1.0 + zeros in the "hi" image, 16 B each, even and odd conv0 columns in separate planes so
+// the 32 lanes of a tap read consecutive 16-B slots), so a tap's B fragment is one ds_read_b128 at a
+// constant offset.  The next chunk's input rows are loaded into registers while this chunk computes.
+#ifndef FE2_POS_DEF
+#define FE2_POS_DEF 256
+#endif
+#ifndef FE2_STG
+#define FE2_STG 2   // output staging buffers per wave (2: a tile's outputs leave during the next tile)
+#endif
+constexpr int FE2_POS = FE2_POS_DEF;                                  // dw1 positions per chunk
+constexpr int FE2_T1ROWS = 2 * ((FE_F2 - 1 + FE2_POS - 1) / FE_F2) + 3;   // conv0 rows a chunk can touch
+constexpr int FE2_XROWS = 2 * FE2_T1ROWS + 1;                         // input rows behind them
+constexpr int FE2_SLOTS = (FE_F1 + 1) / 2;                            // conv0 columns per parity plane
+constexpr int FE2_IMG = 2 * FE2_T1ROWS * FE2_SLOTS * 16;              // one image (lo or hi), bytes
+constexpr int FE2_OPITCH = 80;                                        // output staging row (32 ch bf16 + pad)
+constexpr int FE2_NQ = FE2_XROWS * (FE_F0 / 4);                        // float4 loads per chunk
+constexpr int FE2_QPT = (FE2_NQ + 255) / 256;                         // ... per thread
+typedef short short2v __attribute__((ext_vector_type(2)));
+typedef float f32x2v __attribute__((ext_vector_type(2)));
+typedef bf16 bf16x2v __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ unsigned fe2_relu_pk(float a, float b) {
+  const bf16x2v pr = __builtin_convertvector((f32x2v){a, b}, bf16x2v);   // one v_cvt_pk_bf16_f32
+  short2v v = __builtin_bit_cast(short2v, pr);
+  v = __builtin_elementwise_max(v, (short2v){0, 0});   // v_pk_max_i16: a negative bf16 is a negative int16
+  return __builtin_bit_cast(unsigned, v);
+}
+
+__global__ __launch_bounds__(256, 2) void fe_conv0_dw_mfma2_kernel(const float* __restrict__ feats,
+                                                                const float* const* __restrict__ tab, int step,
+                                                                const int32_t* __restrict__ meta, int meta_stride,
+                                                                int W, int T2, const float* __restrict__ cm,
+                                                                const float* __restrict__ ci,
+                                                                const float* __restrict__ wfrag, int d,
+                                                                bf16* __restrict__ out, int nch) {
+  __shared__ __attribute__((aligned(16))) char im2col[2 * FE2_IMG];
+  // the chunk's input rows (f32, CMVN applied) while im2col is built; then the waves' output staging
+  constexpr int XBYTES = FE2_XROWS * FE_F0 * 4, OBYTES = FE2_STG * 4 * 32 * FE2_OPITCH;   // output staging
+  __shared__ __attribute__((aligned(16))) char xstage[XBYTES > OBYTES ? XBYTES : OBYTES];
+  __shared__ __attribute__((aligned(16))) float cmvn[2][FE_F0];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wv = tid >> 6, h = lane >> 5, n = lane & 31;
+  if (cm && tid < 2 * FE_F0) cmvn[tid / FE_F0][tid % FE_F0] = (tid < FE_F0 ? cm : ci)[tid % FE_F0];
+  const int win = blockIdx.z;
+  const int P = T2 * FE_F2;
+  const int ct = blockIdx.y * 4 + wv;   // this wave's 32-channel tile (waves past d only help build)
+  const bool active = ct * 32 < d;
+  // loop-invariant operands (host-built per-lane fragments, model.hip), loaded first so their latency
+  // overlaps the first chunk's input loads: W0 rows (+ b0 at k = 9), the diagonal dw1 fragments, the
+  // b1 seed
+  bf16x8 a0, a1[9][2];
+  f32x16 seed;
+  {
+    const u32x4* fr = reinterpret_cast<const u32x4*>(wfrag) + (size_t)(active ? ct : 0) * FE2_NFRAG * 64 + lane;
+    a0 = __builtin_bit_cast(bf16x8, fr[0]);
+#pragma unroll
+    for (int s = 0; s < 9; ++s)
+#pragma unroll
+      for (int t = 0; t < 2; ++t) a1[s][t] = __builtin_bit_cast(bf16x8, fr[(1 + 2 * s + t) * 64]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const f32x4 v = __builtin_bit_cast(f32x4, fr[(19 + i) * 64]);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) seed[4 * i + r] = v[r];
+    }
+  }
+  const float* xsrc = window_rows(feats, tab, step, meta + (size_t)win * meta_stride);
+  const int nvalid = min(meta[(size_t)win * meta_stride + PM_NVALID], W);
+  const int nck = (P + FE2_POS - 1) / FE2_POS;
+  const int c_beg = blockIdx.x * nch, c_end = min(c_beg + nch, nck);
+  f32x4 pv[FE2_QPT];   // a chunk's input rows in flight; rows at or past nvalid are padding (zeros before CMVN)
+  auto prefetch = [&](int c) {
+    const int r0 = 4 * ((c * FE2_POS) / FE_F2);
+#pragma unroll
+    for (int i = 0; i < FE2_QPT; ++i) {
+      const int q = tid + 256 * i, r = q / (FE_F0 / 4), gr = r0 + r;
+      pv[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      if (q < FE2_NQ && gr < nvalid)
+        pv[i] = *reinterpret_cast<const f32x4*>(xsrc + (size_t)gr * FE_F0 + 4 * (q % (FE_F0 / 4)));
+    }
+  };
+  if (c_beg < c_end) prefetch(c_beg);
+  const unsigned long long obase = (unsigned long long)(out + (size_t)win * P * d);
+  const unsigned long long obu = ((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(obase >> 32)) << 32) |
+                                 (unsigned)__builtin_amdgcn_readfirstlane((unsigned)obase);
+  const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)obu, (short)0, __builtin_amdgcn_readfirstlane(P * d * 2), 0x00020000);
+  char* os = xstage + wv * 32 * FE2_OPITCH;   // this wave's staging; its second buffer 4 waves further on
+  const f32x16 zero = {};
+  for (int c = c_beg; c < c_end; ++c) {
+    const int p0 = c * FE2_POS, t2a = p0 / FE_F2;
+    __syncthreads();   // the previous chunk's waves are done with im2col and the output staging
+    {
+      float* xs = reinterpret_cast<float*>(xstage);
+#pragma unroll
+      for (int i = 0; i < FE2_QPT; ++i) {
+        const int q = tid + 256 * i;
+        if (q < FE2_NQ) {
+          f32x4 x = pv[i];
+          if (cm) {   // CMVN after padding (cmvn.py:32-43 on the padded window)
+            const int f = 4 * (q % (FE_F0 / 4));
+            x = (x - *reinterpret_cast<const f32x4*>(&cmvn[0][f])) * *reinterpret_cast<const f32x4*>(&cmvn[1][f]);
+          }
+          *reinterpret_cast<f32x4*>(xs + 4 * q) = x;
+        }
+      }
+    }
+    __syncthreads();
+    // im2col of conv0 rows 2*t2a .. 2*t2a + FE2_T1ROWS - 1; slot (row, parity, i) = column 2i + parity.
+    // One thread per (row, i): input columns 4i .. 4i+4 of three rows give both parities' patches.
+    for (int idx = tid; idx < FE2_T1ROWS * FE2_SLOTS; idx += 256) {
+      const int tl = idx / FE2_SLOTS, i = idx - tl * FE2_SLOTS;
+      const float* xr = reinterpret_cast<const float*>(xstage) + (2 * tl) * FE_F0 + 4 * i;
+      f32x4 A[3];
+      float E[3];
+#pragma unroll
+      for (int a = 0; a < 3; ++a) {
+        A[a] = *reinterpret_cast<const f32x4*>(xr + a * FE_F0);
+        E[a] = i + 1 < FE2_SLOTS ? xr[a * FE_F0 + 4] : 0.f;   // column 4i+4 (odd parity only)
+      }
+      const bf16x8 lo0 = {(bf16)A[0][0], (bf16)A[0][1], (bf16)A[0][2], (bf16)A[1][0],
+                          (bf16)A[1][1], (bf16)A[1][2], (bf16)A[2][0], (bf16)A[2][1]};
+      const bf16x8 hi0 = {(bf16)A[2][2], (bf16)1.f, (bf16)0.f, (bf16)0.f, (bf16)0.f, (bf16)0.f, (bf16)0.f, (bf16)0.f};
+      const int s0 = (tl * FE2_SLOTS + i) * 16, s1 = ((FE2_T1ROWS + tl) * FE2_SLOTS + i) * 16;
+      *reinterpret_cast<bf16x8*>(im2col + s0) = lo0;
+      *reinterpret_cast<bf16x8*>(im2col + FE2_IMG + s0) = hi0;
+      if (2 * i + 1 < FE_F1) {
+        const bf16x8 lo1 = {(bf16)A[0][2], (bf16)A[0][3], (bf16)E[0], (bf16)A[1][2],
+                            (bf16)A[1][3], (bf16)E[1], (bf16)A[2][2], (bf16)A[2][3]};
+        const bf16x8 hi1 = {(bf16)E[2], (bf16)1.f, (bf16)0.f, (bf16)0.f, (bf16)0.f, (bf16)0.f, (bf16)0.f, (bf16)0.f};
+        *reinterpret_cast<bf16x8*>(im2col + s1) = lo1;
+        *reinterpret_cast<bf16x8*>(im2col + FE2_IMG + s1) = hi1;
+      }
+    }
+    __syncthreads();
+    if (c + 1 < c_end) prefetch(c + 1);   // lands under this chunk's MFMAs
+    if (!active) continue;
+    const int pend = min(p0 + FE2_POS, P);
+    // tile pt's patches: tap (u, v) = conv0 position (2 t2 + u, 2 f2 + v) of the lane's position
+    auto patch_base = [&](int pt) {
+      const int pos = min(pt + n, P - 1);   // positions past P are computed and dropped at the store
+      const int t2 = pos / FE_F2, f2 = pos - t2 * FE_F2;
+      return im2col + h * FE2_IMG + ((2 * (t2 - t2a)) * FE2_SLOTS + f2) * 16;
+    };
+    auto tap_off = [](int s) { return ((((s % 3) & 1) * FE2_T1ROWS + s / 3) * FE2_SLOTS + ((s % 3) >> 1)) * 16; };
+    auto ld = [&](const char* xb, int s) { return *reinterpret_cast<const bf16x8*>(xb + tap_off(s)); };
+    // the staged outputs of tile pt leave as 64-B row pieces (4 lanes per position)
+    auto flush = [&](const char* sb, int pt) {
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int pl = (lane >> 2) + 16 * k, ch = lane & 3;
+        const u32x4 v = *reinterpret_cast<const u32x4*>(sb + pl * FE2_OPITCH + ch * 16);
+#ifndef CFM_FE_DIAG_NOSTORE
+        __builtin_amdgcn_raw_buffer_store_b128(v, ors, (unsigned)(((pt + pl) * d + ct * 32 + ch * 8) * 2), 0, 0);
+#else
+        asm volatile("" ::"v"(v));
+#endif
+      }
+    };
+    bf16x8 pb[9];
+    {
+      const char* xb = patch_base(p0);
+#pragma unroll
+      for (int s = 0; s < 9; ++s) pb[s] = ld(xb, s);
+    }
+    int it = 0;
+    for (int pt = p0; pt < pend; pt += 32, ++it) {
+      // the next tile's patches are read into pb as its registers free up (tap t's patch is last
+      // used when conv0 of tap t is issued, in loop step t - 1), so they arrive under this tile's
+      // MFMAs; the previous tile's staged outputs leave in step 1
+      const char* xbn = patch_base(pt + 32 < pend ? pt + 32 : pt);
+      char* sb = os + (FE2_STG == 2 ? (it & 1) : 0) * (4 * 32 * FE2_OPITCH);
+      f32x16 y = seed;
+      f32x16 acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, pb[0], zero, 0, 0, 0);
+#pragma unroll
+      for (int s = 0; s < 9; ++s) {
+        f32x16 nxt;
+        if (s + 1 < 9) nxt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, pb[s + 1], zero, 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);   // conv0 of tap s+1 runs under tap s's VALU work
+        u32x4 r0, r1;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          r0[q] = fe2_relu_pk(acc[2 * q], acc[2 * q + 1]);
+          r1[q] = fe2_relu_pk(acc[8 + 2 * q], acc[9 + 2 * q]);
+        }
+        y = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1[s][0], __builtin_bit_cast(bf16x8, r0), y, 0, 0, 0);
+        y = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1[s][1], __builtin_bit_cast(bf16x8, r1), y, 0, 0, 0);
+        if (FE2_STG == 2 && s == 1 && it > 0) flush(os + ((it - 1) & 1) * (4 * 32 * FE2_OPITCH), pt - 32);
+        if (s == 3) {
+#pragma unroll
+          for (int t = 0; t < 4; ++t) pb[t] = ld(xbn, t);
+        }
+        if (s == 7) {
+#pragma unroll
+          for (int t = 4; t < 9; ++t) pb[t] = ld(xbn, t);
+        }
+        // one tap at a time (left alone, the scheduler hoists all nine conv0 MFMAs and spills)
+        __builtin_amdgcn_sched_barrier(0);
+        if (s + 1 < 9) acc = nxt;
+      }
+      // y: lane (h, position n), register r -> channel (r&3) + 8(r>>2) + 4h; staged [32 pos][32 ch]
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const bf16x2v lo = __builtin_convertvector((f32x2v){y[4 * g], y[4 * g + 1]}, bf16x2v);
+        const bf16x2v hi = __builtin_convertvector((f32x2v){y[4 * g + 2], y[4 * g + 3]}, bf16x2v);
+        const unsigned long long u = (unsigned long long)__builtin_bit_cast(unsigned, lo) |
+                                     ((unsigned long long)__builtin_bit_cast(unsigned, hi) << 32);
+        *reinterpret_cast<unsigned long long*>(sb + n * FE2_OPITCH + (8 * g + 4 * h) * 2) = u;
+      }
+      if (FE2_STG == 1) flush(sb, pt);
+    }
+    if (FE2_STG == 2 && it > 0) flush(os + ((it - 1) & 1) * (4 * 32 * FE2_OPITCH), pend - 1 - ((pend - 1 - p0) % 32));
+  }
+}
+
 // dw2: [win][T2][19][d] -> [win][T3][9][d], depthwise 3x3 stride 2 + bias (no activation), taps
 // tap-major w[9][d].  One thread per (window, f3, 8 channels, row segment) walks down its
 // FE_DW2_SEG-th of the window's output rows: input row 2*t3+2 is kept in registers for the next
@@ -304,7 +532,8 @@ template <typename T>
 int frontend_conv0_dw(const float* feats, const float* const* tab, int step, const int32_t* meta, int meta_stride,
                       int nwin, int W,
                       const float* cmvn_mean, const float* cmvn_istd, const float* w0, const float* b0,
-                      const float* w1, const float* b1, const float* wpack, int d, T* out, hipStream_t st) {
+                      const float* w1, const float* b1, const float* wpack, const float* wfrag, int d, T* out,
+                      hipStream_t st, int var) {
   if (nwin <= 0) return 0;
   const int T1 = (W - 3) / 2 + 1, T2 = (T1 - 3) / 2 + 1;
   if (T2 <= 0 || d % FE_CG) return (int)hipErrorInvalidValue;
@@ -312,6 +541,13 @@ int frontend_conv0_dw(const float* feats, const float* const* tab, int step, con
   if constexpr (std::is_same<T, bf16>::value) {
     // one window's dw1 output is addressed by 32-bit byte offsets (buffer stores)
     if (d % 64 || (size_t)T2 * FE_F2 * d * sizeof(bf16) >= ((size_t)1 << 31)) return (int)hipErrorInvalidValue;
+    if (var >= 2 && wfrag) {
+      const int nck = (T2 * FE_F2 + FE2_POS - 1) / FE2_POS, nch = std::max(1, var - 1);   // var 2 + k: k+1 chunks
+      hipLaunchKernelGGL(fe_conv0_dw_mfma2_kernel, dim3((nck + nch - 1) / nch, (d + 127) / 128, nwin), dim3(256), 0,
+                         st, feats, tab, step, meta, meta_stride, W, T2, cmvn_mean, cmvn_istd, wfrag, d, out, nch);
+      CFM_CHECK_LAUNCH();
+      return 0;
+    }
     hipLaunchKernelGGL(fe_conv0_dw_mfma_kernel, dim3((T2 * FE_F2 + FE_POS_BLOCK - 1) / FE_POS_BLOCK, nwin), dim3(256),
                        0, st, feats, tab, step, meta, meta_stride, W, T2, cmvn_mean, cmvn_istd, wpack, d, out);
   } else {
@@ -339,10 +575,10 @@ int frontend_dw2(const T* in, int nwin, int T2, int d, const float* w, const flo
 
 template int frontend_conv0_dw<float>(const float*, const float* const*, int, const int32_t*, int, int, int, const float*,
                                       const float*,
-                                      const float*, const float*, const float*, const float*, const float*, int, float*, hipStream_t);
+                                      const float*, const float*, const float*, const float*, const float*, const float*, int, float*, hipStream_t, int);
 template int frontend_conv0_dw<bf16>(const float*, const float* const*, int, const int32_t*, int, int, int, const float*,
                                      const float*,
-                                     const float*, const float*, const float*, const float*, const float*, int, bf16*, hipStream_t);
+                                     const float*, const float*, const float*, const float*, const float*, const float*, int, bf16*, hipStream_t, int);
 template int frontend_dw2<float>(const float*, int, int, int, const float*, const float*, float*, hipStream_t, int);
 template int frontend_dw2<bf16>(const bf16*, int, int, int, const float*, const float*, bf16*, hipStream_t, int);
 

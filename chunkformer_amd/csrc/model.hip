@@ -72,7 +72,7 @@ struct LayerW {
 };
 
 struct FrontW {
-  float *cm = nullptr, *ci = nullptr, *w0, *b0, *w1, *b1, *w2, *b2, *b_pw1, *b_pw2, *b_out, *wpack;
+  float *cm = nullptr, *ci = nullptr, *w0, *b0, *w1, *b1, *w2, *b2, *b_pw1, *b_pw2, *b_out, *wpack, *wfrag = nullptr;
   void *pw1, *pw2, *wout;
   float *an_w, *an_b;
   void* ctc_w = nullptr;
@@ -286,7 +286,7 @@ struct ModelT : public cfm_model {
       const int ng = std::min(G, nwin - g0);
       PROF(PC_FE_CONV, frontend_conv0_dw<T>(feats, feats_tab, 8 * C, meta + (size_t)g0 * PLAN_REC, PLAN_REC, ng, Wn,
                                 fe.cm, fe.ci, fe.w0, fe.b0,
-                                fe.w1, fe.b1, fe.wpack, d, w.feA, st));
+                                fe.w1, fe.b1, fe.wpack, fe.wfrag, d, w.feA, st, tune.fe_conv));
       EpiArgs e1 = E(SITE_FE); e1.bias = fe.b_pw1; e1.out = w.feB; e1.ldo = d;
       T* dw2_rows = w.feA;   // the pw2 GEMM's input
       if constexpr (std::is_same<T, bf16>::value) {
@@ -546,6 +546,37 @@ static cfm_status build_model(const cfm_config& cfg, const HostW& hw, int device
         w[(size_t)c * FE_WPACK + 19] = bb[c];
       }
       put_f32(w.data(), w.size(), &F.wpack);
+      // the channel-stationary kernel's per-lane MFMA fragments ("fe_conv" >= 2), [tile][FE2_NFRAG][64 lanes]
+      // x 16 B: W0 rows + b0 (bf16), the diagonal dw1 fragments of the 9 taps x 2 k-steps (bf16), the b1
+      // seed in accumulator order (f32)
+      if (d % 32 == 0) {
+        std::vector<uint32_t> fr((size_t)(d / 32) * FE2_NFRAG * 64 * 4, 0u);
+        auto bf = [](float x) { return (uint32_t)bf16_bits_rne(x); };
+        for (int ct = 0; ct < d / 32; ++ct)
+          for (int lane = 0; lane < 64; ++lane) {
+            const int h = lane >> 5, n = lane & 31, c = ct * 32 + n;
+            auto slot = [&](int q) { return &fr[(((size_t)ct * FE2_NFRAG + q) * 64 + lane) * 4]; };
+            uint16_t a0[8];
+            for (int j = 0; j < 8; ++j) {
+              const int k = 8 * h + j;
+              a0[j] = (uint16_t)bf(k < 9 ? a[c * 9 + k] : k == 9 ? ab[c] : 0.f);
+            }
+            std::memcpy(slot(0), a0, 16);
+            const bool own = h == ((n >> 2) & 1);
+            const int town = n >> 4, j0 = (n & 3) + 4 * ((n >> 3) & 1);
+            for (int sp = 0; sp < 9; ++sp)
+              for (int t = 0; t < 2; ++t) {
+                uint16_t a1[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+                if (own && t == town) a1[j0] = (uint16_t)bf(b[c * 9 + sp]);
+                std::memcpy(slot(1 + 2 * sp + t), a1, 16);
+              }
+            for (int r = 0; r < 16; ++r) {
+              const float v = bb[ct * 32 + (r & 3) + 8 * (r >> 2) + 4 * h];
+              std::memcpy(slot(19 + r / 4) + (r & 3), &v, 4);
+            }
+          }
+        put_f32(reinterpret_cast<const float*>(fr.data()), fr.size(), &F.wfrag);
+      }
     }
     put_T(vec(E + "embed.conv.3.weight", (int64_t)d * d), &F.pw1);
     put_f32(hw.get(E + "embed.conv.3.bias", d), d, &F.b_pw1);
@@ -702,7 +733,7 @@ cfm_status cfm_model_set_option(cfm_model* m, const char* key, int64_t value) {
         {"gemm_diag", &m->tune.gemm_diag}, {"gemm_wst", &m->tune.gemm_wst},   {"store_mode", &m->tune.store_mode},
         {"col_group", &m->tune.col_group}, {"attn_reuse", &m->tune.attn_reuse}, {"conv_dot2", &m->tune.conv_dot2},
         {"conv_dma", &m->tune.conv_dma},   {"dw2_seg", &m->tune.dw2_seg},   {"nt_sites", &m->tune.nt_sites},
-        {"fe_fuse_dw2", &m->tune.fe_fuse_dw2},
+        {"fe_fuse_dw2", &m->tune.fe_fuse_dw2}, {"fe_conv", &m->tune.fe_conv},
         {"attn128_var", &m->tune.attn128_var}, {"attn_q32", &m->tune.attn_q32},
         {"gemm_big_min", &m->tune.big_min_tiles}, {"wsp_small_div", &m->tune.wsp_small_div},
         {"wsp_small_rows", &m->tune.wsp_small_rows},
