@@ -548,7 +548,8 @@ static cfm_status build_model(const cfm_config& cfg, const HostW& hw, int device
       put_f32(w.data(), w.size(), &F.wpack);
       // the channel-stationary kernel's per-lane MFMA fragments ("fe_conv" >= 2), [tile][FE2_NFRAG][64 lanes]
       // x 16 B: W0 rows + b0 (bf16), the diagonal dw1 fragments of the 9 taps x 2 k-steps (bf16), the b1
-      // seed in accumulator order (f32)
+      // seed in accumulator order (f32).  W0 and b0 are scaled by 2^-24 and w1 by 2^24 (exact), so conv0's
+      // accumulator carries 2^-24 x its value: the ReLU can then be a clamp to [0, 1] (frontend.hip FE2_CLAMP)
       if (d % 32 == 0) {
         std::vector<uint32_t> fr((size_t)(d / 32) * FE2_NFRAG * 64 * 4, 0u);
         auto bf = [](float x) { return (uint32_t)bf16_bits_rne(x); };
@@ -559,7 +560,7 @@ static cfm_status build_model(const cfm_config& cfg, const HostW& hw, int device
             uint16_t a0[8];
             for (int j = 0; j < 8; ++j) {
               const int k = 8 * h + j;
-              a0[j] = (uint16_t)bf(k < 9 ? a[c * 9 + k] : k == 9 ? ab[c] : 0.f);
+              a0[j] = (uint16_t)bf(std::ldexp(k < 9 ? a[c * 9 + k] : k == 9 ? ab[c] : 0.f, -24));
             }
             std::memcpy(slot(0), a0, 16);
             const bool own = h == ((n >> 2) & 1);
@@ -567,7 +568,7 @@ static cfm_status build_model(const cfm_config& cfg, const HostW& hw, int device
             for (int sp = 0; sp < 9; ++sp)
               for (int t = 0; t < 2; ++t) {
                 uint16_t a1[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-                if (own && t == town) a1[j0] = (uint16_t)bf(b[c * 9 + sp]);
+                if (own && t == town) a1[j0] = (uint16_t)bf(std::ldexp(b[c * 9 + sp], 24));
                 std::memcpy(slot(1 + 2 * sp + t), a1, 16);
               }
             for (int r = 0; r < 16; ++r) {
