@@ -278,13 +278,15 @@ typedef float f32x2v __attribute__((ext_vector_type(2)));
 typedef bf16 bf16x2v __attribute__((ext_vector_type(2)));
 
 #ifndef FE2_CLAMP
-#define FE2_CLAMP 0   // 1: ReLU as the clamp modifier of the conversion (see fe2_relu_pk)
+#define FE2_CLAMP 1   // ReLU as the clamp modifier of the conversion (see fe2_relu_pk); 0: v_pk_max_i16
 #endif
 __device__ __forceinline__ unsigned fe2_relu_pk(float a, float b) {
 #if FE2_CLAMP
   // W0 and b0 enter the fragments scaled by 2^-24 and w1 by 2^24 (exact: powers of two), so conv0's
   // accumulator is the true value times 2^-24 and, for |conv0| < 2^24, the conversion's clamp to
-  // [0, 1] is exactly the ReLU: one instruction per pair instead of two
+  // [0, 1] is exactly the ReLU: one instruction per pair instead of two (saturation to [0, 1], NaN to 0,
+  // probed on gfx950: tools/probe/cvt_clamp.hip).  Front-end conv0 outputs of CMVN-normalised
+  // features are orders of magnitude below 2^24.
   unsigned u;
   asm("v_cvt_pk_bf16_f32 %0, %1, %2 clamp" : "=v"(u) : "v"(a), "v"(b));
   return u;

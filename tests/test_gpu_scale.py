@@ -217,10 +217,11 @@ def test_frontend_window_groups_forced(large):
 
 @pytest.mark.parametrize("minutes", [1, 240])
 def test_frontend_conv_kernels_agree(large, minutes):
-    """bf16 conv0 + ReLU + dw1: the channel-stationary kernel (fe_conv 3: dw1 on MFMA, conv0's ReLU
-    output rounded to bf16 as autocast does, 2 chunks per block) and the position-stationary one
-    (fe_conv 1, the default: dw1 in f32 on the VALU) both stay at the golden's bf16 bar and agree
-    with each other to bf16 rounding (1 minute: partial last blocks; 240 minutes: the bench batch)."""
+    """bf16 conv0 + ReLU + dw1: the channel-stationary kernel (fe_conv 3, the default: dw1 on MFMA,
+    conv0's ReLU output rounded to bf16 as autocast does, the ReLU as the conversion's clamp on
+    2^-24-scaled values) and the position-stationary one (fe_conv 1: dw1 in f32 on the VALU) both
+    stay at the golden's bf16 bar and agree with each other to bf16 rounding (1 minute: partial last
+    blocks; 240 minutes: the bench batch)."""
     g, _, models = large
     enc = models["bf16"]
     xs, pos = _embedded_batch(g, minutes, enc.device)
@@ -232,7 +233,7 @@ def test_frontend_conv_kernels_agree(large, minutes):
             out, _, nch, _, _, _ = enc.forward_parallel_chunk(xs, lens, 64, 128, 128)
             outs[v] = out.float()
     finally:
-        enc.set_option("fe_conv", 1)   # the default
+        enc.set_option("fe_conv", 3)   # the default
     torch.cuda.synchronize()
     gstart = np.cumsum([0] + g["nchunks"].tolist())
     for v in (1, 3):

@@ -139,13 +139,21 @@ def test_configs2_980min_world8_golden():
     # golden utterances against the reference's rows
     gnch = g["nchunks"].tolist()
     gstart = np.cumsum([0] + [n * C for n in gnch])
+    agree = []
     for k, u in enumerate(pos):
         exp = g["out"].reshape(-1, LARGE.d_model)[gstart[k]: gstart[k] + outs[u].shape[0]]
         o = outs[u].cpu().numpy()
         rel = float(np.linalg.norm(o - exp) / np.linalg.norm(exp))
         assert rel <= 2e-2, (k, rel)
         ei = g["ids"].reshape(-1)[gstart[k]: gstart[k] + outs[u].shape[0]]
-        assert (ids[u].cpu().numpy() == ei).mean() >= 0.99
+        m = (g["top2"][..., 0] - g["top2"][..., 1]).reshape(-1)[gstart[k]: gstart[k] + outs[u].shape[0]]
+        i = ids[u].cpu().numpy()
+        # the bars of test_golden_utterances_inside_bench_batch: ids equal wherever the reference's top-2
+        # margin exceeds 5e-2, >= 99% agreement over the golden frames (one near-tie flip is 1.4% of the
+        # 6 s utterance's 74 frames, so the 99% bar is the aggregate one)
+        np.testing.assert_array_equal(i[m > 5e-2], ei[m > 5e-2])
+        agree.append(i == ei)
+    assert np.concatenate(agree).mean() >= 0.99
     # every utterance against the unsharded run of the same batch
     ref, rid = _unsharded(enc, xs, lens, C, L, R)
     worst, agree = 0.0, []
