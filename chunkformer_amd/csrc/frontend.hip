@@ -303,7 +303,7 @@ __global__ __launch_bounds__(256, 2) void fe_conv0_dw_mfma2_kernel(const float* 
                                                                 int W, int T2, const float* __restrict__ cm,
                                                                 const float* __restrict__ ci,
                                                                 const float* __restrict__ wfrag, int d,
-                                                                bf16* __restrict__ out, int nch) {
+                                                                bf16* __restrict__ out) {
   __shared__ __attribute__((aligned(16))) char im2col[2 * FE2_IMG];
   // the chunk's input rows (f32, CMVN applied) while im2col is built; then the waves' output staging
   constexpr int XBYTES = FE2_XROWS * FE_F0 * 4, OBYTES = FE2_STG * 4 * 32 * FE2_OPITCH;   // output staging
@@ -338,7 +338,8 @@ __global__ __launch_bounds__(256, 2) void fe_conv0_dw_mfma2_kernel(const float* 
   const float* xsrc = window_rows(feats, tab, step, meta + (size_t)win * meta_stride);
   const int nvalid = min(meta[(size_t)win * meta_stride + PM_NVALID], W);
   const int nck = (P + FE2_POS - 1) / FE2_POS;
-  const int c_beg = blockIdx.x * nch, c_end = min(c_beg + nch, nck);
+  // the window's chunks split evenly over the gridDim.x workgroups of its row (counts differ by <= 1)
+  const int c_beg = (int)((long long)blockIdx.x * nck / gridDim.x), c_end = (int)((long long)(blockIdx.x + 1) * nck / gridDim.x);
   f32x4 pv[FE2_QPT];   // a chunk's input rows in flight; rows at or past nvalid are padding (zeros before CMVN)
   auto prefetch = [&](int c) {
     const int r0 = 4 * ((c * FE2_POS) / FE_F2);
@@ -555,9 +556,11 @@ int frontend_conv0_dw(const float* feats, const float* const* tab, int step, con
     // one window's dw1 output is addressed by 32-bit byte offsets (buffer stores)
     if (d % 64 || (size_t)T2 * FE_F2 * d * sizeof(bf16) >= ((size_t)1 << 31)) return (int)hipErrorInvalidValue;
     if (var >= 2 && wfrag) {
-      const int nck = (T2 * FE_F2 + FE2_POS - 1) / FE2_POS, nch = std::max(1, var - 1);   // var 2 + k: k+1 chunks
-      hipLaunchKernelGGL(fe_conv0_dw_mfma2_kernel, dim3((nck + nch - 1) / nch, (d + 127) / 128, nwin), dim3(256), 0,
-                         st, feats, tab, step, meta, meta_stride, W, T2, cmvn_mean, cmvn_istd, wfrag, d, out, nch);
+      // "fe_conv" 2 + k: about k + 1 chunks of FE2_POS positions per workgroup, balanced per window
+      const int nck = (T2 * FE_F2 + FE2_POS - 1) / FE2_POS, nch = std::max(1, var - 1);
+      const int nb = (nck + nch - 1) / nch;
+      hipLaunchKernelGGL(fe_conv0_dw_mfma2_kernel, dim3(nb, (d + 127) / 128, nwin), dim3(256), 0, st, feats, tab, step,
+                         meta, meta_stride, W, T2, cmvn_mean, cmvn_istd, wfrag, d, out);
       CFM_CHECK_LAUNCH();
       return 0;
     }

@@ -79,9 +79,10 @@ void cfm_model_destroy(cfm_model* m);
  *                   0 = the generic per-block kernel (A/B testing)
  *   "fe_fuse_dw2"   1 (default) = bf16 front-end pw1 + ReLU + dw2 in one weight-stationary GEMM,
  *                   0 = pw1 GEMM + the separate dw2 kernel (bit-identical; A/B testing)
- *   "fe_conv"       bf16 conv0 + ReLU + dw1: 3 (default) = channel-stationary, dw1 on MFMA with
- *                   conv0's ReLU output rounded to bf16 (as autocast does), 2 chunks of 256 positions
- *                   per workgroup (2 + k: k + 1 chunks); 1 = position-stationary, dw1 in f32 on the VALU
+ *   "fe_conv"       bf16 conv0 + ReLU + dw1: 6 (default) = channel-stationary, dw1 on MFMA with
+ *                   conv0's ReLU output rounded to bf16 (as autocast does), about 5 chunks of 256
+ *                   positions per workgroup, balanced per window (2 + k: about k + 1 chunks);
+ *                   1 = position-stationary, dw1 in f32 on the VALU
  * (all per-model kernel options: struct Tuning in chunkformer_amd/csrc/cfm_kernels.h, keyed in
  *  cfm_model_set_option, chunkformer_amd/csrc/model.hip) */
 cfm_status cfm_model_set_option(cfm_model* m, const char* key, int64_t value);
