@@ -269,7 +269,12 @@ constexpr int FE2_POS = FE2_POS_DEF;                                  // dw1 pos
 constexpr int FE2_T1ROWS = 2 * ((FE_F2 - 1 + FE2_POS - 1) / FE_F2) + 3;   // conv0 rows a chunk can touch
 constexpr int FE2_XROWS = 2 * FE2_T1ROWS + 1;                         // input rows behind them
 constexpr int FE2_SLOTS = (FE_F1 + 1) / 2;                            // conv0 columns per parity plane
-constexpr int FE2_IMG = 2 * FE2_T1ROWS * FE2_SLOTS * 16;              // one image (lo or hi), bytes
+// slot of conv0 row t1, column pair i within a parity plane: each pair of rows is padded by 11 slots
+// so that one dw1 row (2 conv0 rows) spans 51 = 3 (mod 16) slots and 16 consecutive positions fall in
+// 16 different 16-B bank groups even across a row boundary (18 -> 0: +33 slots)
+__host__ __device__ constexpr int fe2_slot(int t1, int i) { return t1 * FE2_SLOTS + (t1 >> 1) * 11 + i; }
+constexpr int FE2_PLANE = fe2_slot(FE2_T1ROWS - 1, FE2_SLOTS - 1) + 1;  // slots per parity plane
+constexpr int FE2_IMG = 2 * FE2_PLANE * 16;                           // one image (lo or hi), bytes
 constexpr int FE2_OPITCH = 80;                                        // output staging row (32 ch bf16 + pad)
 constexpr int FE2_NQ = FE2_XROWS * (FE_F0 / 4);                        // float4 loads per chunk
 constexpr int FE2_QPT = (FE2_NQ + 255) / 256;                         // ... per thread
@@ -393,7 +398,7 @@ __global__ __launch_bounds__(256, 2) void fe_conv0_dw_mfma2_kernel(const float* 
       const bf16x8 lo0 = {(bf16)A[0][0], (bf16)A[0][1], (bf16)A[0][2], (bf16)A[1][0],
                           (bf16)A[1][1], (bf16)A[1][2], (bf16)A[2][0], (bf16)A[2][1]};
       const bf16x8 hi0 = {(bf16)A[2][2], (bf16)1.f, (bf16)0.f, (bf16)0.f, (bf16)0.f, (bf16)0.f, (bf16)0.f, (bf16)0.f};
-      const int s0 = (tl * FE2_SLOTS + i) * 16, s1 = ((FE2_T1ROWS + tl) * FE2_SLOTS + i) * 16;
+      const int s0 = fe2_slot(tl, i) * 16, s1 = (FE2_PLANE + fe2_slot(tl, i)) * 16;
       *reinterpret_cast<bf16x8*>(im2col + s0) = lo0;
       *reinterpret_cast<bf16x8*>(im2col + FE2_IMG + s0) = hi0;
       if (2 * i + 1 < FE_F1) {
@@ -412,9 +417,11 @@ __global__ __launch_bounds__(256, 2) void fe_conv0_dw_mfma2_kernel(const float* 
     auto patch_base = [&](int pt) {
       const int pos = min(pt + n, P - 1);   // positions past P are computed and dropped at the store
       const int t2 = pos / FE_F2, f2 = pos - t2 * FE_F2;
-      return im2col + h * FE2_IMG + ((2 * (t2 - t2a)) * FE2_SLOTS + f2) * 16;
+      return im2col + h * FE2_IMG + (fe2_slot(2 * (t2 - t2a), 0) + f2) * 16;
     };
-    auto tap_off = [](int s) { return ((((s % 3) & 1) * FE2_T1ROWS + s / 3) * FE2_SLOTS + ((s % 3) >> 1)) * 16; };
+    // tap (u, v): conv0 row 2 t2 + u (fe2_slot(2 t2 + u, i) - fe2_slot(2 t2, i) = fe2_slot(u, 0)), parity
+    // plane v & 1, pair f2 + (v >> 1)
+    auto tap_off = [](int s) { return (((s % 3) & 1) * FE2_PLANE + fe2_slot(s / 3, 0) + ((s % 3) >> 1)) * 16; };
     auto ld = [&](const char* xb, int s) { return *reinterpret_cast<const bf16x8*>(xb + tap_off(s)); };
     // the staged outputs of tile pt leave as 64-B row pieces (4 lanes per position)
     auto flush = [&](const char* sb, int pt) {
