@@ -22,6 +22,7 @@ CLASSES = [
     ("gemm_wsp_kernel<5, 1,", "frontend_pw1_dw2 (fused)"), ("gemm_wsp_kernelILi5ELi1E", "frontend_pw1_dw2 (fused)"),
     ("gemm_wsp_kernel<0, 1,", "frontend_pw_gemm"), ("gemm_wsp_kernel<3, 0,", "qkv_gemm"),
     ("gemm_wsp_kernel<4, 0,", "pw1_glu_gemm"), ("gemm_wsp_kernel<0, 0,", "plain_gemm_k512 (out_proj / pw2)"),
+    ("fe_conv0_dw_mfma2_kernel", "frontend_conv0_dw"),
     ("fe_conv0_dw_mfma_kernel", "frontend_conv0_dw"),
     ("fe_dw2_kernel", "frontend_dw2"),
     ("chunk_attention_ring_kernel", "chunk_attention"),
