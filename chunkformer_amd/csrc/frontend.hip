@@ -262,6 +262,9 @@ __global__ __launch_bounds__(256, 3) void fe_conv0_dw_mfma_kernel(const float* _
 #ifndef FE2_POS_DEF
 #define FE2_POS_DEF 256
 #endif
+#ifndef FE2_WAVES
+#define FE2_WAVES 4   // waves (32-channel tiles) per workgroup sharing one im2col build: 4 (2 workgroups per CU) or 8
+#endif
 #ifndef FE2_STG
 #define FE2_STG 2   // output staging buffers per wave (2: a tile's outputs leave during the next tile)
 #endif
@@ -277,7 +280,8 @@ constexpr int FE2_PLANE = fe2_slot(FE2_T1ROWS - 1, FE2_SLOTS - 1) + 1;  // slots
 constexpr int FE2_IMG = 2 * FE2_PLANE * 16;                           // one image (lo or hi), bytes
 constexpr int FE2_OPITCH = 80;                                        // output staging row (32 ch bf16 + pad)
 constexpr int FE2_NQ = FE2_XROWS * (FE_F0 / 4);                        // float4 loads per chunk
-constexpr int FE2_QPT = (FE2_NQ + 255) / 256;                         // ... per thread
+constexpr int FE2_NT = 64 * FE2_WAVES;                                // threads per workgroup
+constexpr int FE2_QPT = (FE2_NQ + FE2_NT - 1) / FE2_NT;               // ... per thread
 typedef short short2v __attribute__((ext_vector_type(2)));
 typedef float f32x2v __attribute__((ext_vector_type(2)));
 typedef bf16 bf16x2v __attribute__((ext_vector_type(2)));
@@ -302,7 +306,7 @@ __device__ __forceinline__ unsigned fe2_relu_pk(float a, float b) {
   return __builtin_bit_cast(unsigned, v);
 }
 
-__global__ __launch_bounds__(256, 2) void fe_conv0_dw_mfma2_kernel(const float* __restrict__ feats,
+__global__ __launch_bounds__(FE2_NT, 8 / FE2_WAVES) void fe_conv0_dw_mfma2_kernel(const float* __restrict__ feats,
                                                                 const float* const* __restrict__ tab, int step,
                                                                 const int32_t* __restrict__ meta, int meta_stride,
                                                                 int W, int T2, const float* __restrict__ cm,
@@ -311,7 +315,7 @@ __global__ __launch_bounds__(256, 2) void fe_conv0_dw_mfma2_kernel(const float* 
                                                                 bf16* __restrict__ out) {
   __shared__ __attribute__((aligned(16))) char im2col[2 * FE2_IMG];
   // the chunk's input rows (f32, CMVN applied) while im2col is built; then the waves' output staging
-  constexpr int XBYTES = FE2_XROWS * FE_F0 * 4, OBYTES = FE2_STG * 4 * 32 * FE2_OPITCH;   // output staging
+  constexpr int XBYTES = FE2_XROWS * FE_F0 * 4, OBYTES = FE2_STG * FE2_WAVES * 32 * FE2_OPITCH;   // output staging
   __shared__ __attribute__((aligned(16))) char xstage[XBYTES > OBYTES ? XBYTES : OBYTES];
   __shared__ __attribute__((aligned(16))) float cmvn[2][FE_F0];
   const int tid = threadIdx.x;
@@ -319,7 +323,7 @@ __global__ __launch_bounds__(256, 2) void fe_conv0_dw_mfma2_kernel(const float* 
   if (cm && tid < 2 * FE_F0) cmvn[tid / FE_F0][tid % FE_F0] = (tid < FE_F0 ? cm : ci)[tid % FE_F0];
   const int win = blockIdx.z;
   const int P = T2 * FE_F2;
-  const int ct = blockIdx.y * 4 + wv;   // this wave's 32-channel tile (waves past d only help build)
+  const int ct = blockIdx.y * FE2_WAVES + wv;   // this wave's 32-channel tile (waves past d only help build)
   const bool active = ct * 32 < d;
   // loop-invariant operands (host-built per-lane fragments, model.hip), loaded first so their latency
   // overlaps the first chunk's input loads: W0 rows (+ b0 at k = 9), the diagonal dw1 fragments, the
@@ -350,7 +354,7 @@ __global__ __launch_bounds__(256, 2) void fe_conv0_dw_mfma2_kernel(const float* 
     const int r0 = 4 * ((c * FE2_POS) / FE_F2);
 #pragma unroll
     for (int i = 0; i < FE2_QPT; ++i) {
-      const int q = tid + 256 * i, r = q / (FE_F0 / 4), gr = r0 + r;
+      const int q = tid + FE2_NT * i, r = q / (FE_F0 / 4), gr = r0 + r;
       pv[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
       if (q < FE2_NQ && gr < nvalid)
         pv[i] = *reinterpret_cast<const f32x4*>(xsrc + (size_t)gr * FE_F0 + 4 * (q % (FE_F0 / 4)));
@@ -362,7 +366,7 @@ __global__ __launch_bounds__(256, 2) void fe_conv0_dw_mfma2_kernel(const float* 
                                  (unsigned)__builtin_amdgcn_readfirstlane((unsigned)obase);
   const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(
       (void*)obu, (short)0, __builtin_amdgcn_readfirstlane(P * d * 2), 0x00020000);
-  char* os = xstage + wv * 32 * FE2_OPITCH;   // this wave's staging; its second buffer 4 waves further on
+  char* os = xstage + wv * 32 * FE2_OPITCH;   // this wave's staging; its second buffer FE2_WAVES waves further on
   const f32x16 zero = {};
   for (int c = c_beg; c < c_end; ++c) {
     const int p0 = c * FE2_POS, t2a = p0 / FE_F2;
@@ -371,7 +375,7 @@ __global__ __launch_bounds__(256, 2) void fe_conv0_dw_mfma2_kernel(const float* 
       float* xs = reinterpret_cast<float*>(xstage);
 #pragma unroll
       for (int i = 0; i < FE2_QPT; ++i) {
-        const int q = tid + 256 * i;
+        const int q = tid + FE2_NT * i;
         if (q < FE2_NQ) {
           f32x4 x = pv[i];
           if (cm) {   // CMVN after padding (cmvn.py:32-43 on the padded window)
@@ -385,7 +389,7 @@ __global__ __launch_bounds__(256, 2) void fe_conv0_dw_mfma2_kernel(const float* 
     __syncthreads();
     // im2col of conv0 rows 2*t2a .. 2*t2a + FE2_T1ROWS - 1; slot (row, parity, i) = column 2i + parity.
     // One thread per (row, i): input columns 4i .. 4i+4 of three rows give both parities' patches.
-    for (int idx = tid; idx < FE2_T1ROWS * FE2_SLOTS; idx += 256) {
+    for (int idx = tid; idx < FE2_T1ROWS * FE2_SLOTS; idx += FE2_NT) {
       const int tl = idx / FE2_SLOTS, i = idx - tl * FE2_SLOTS;
       const float* xr = reinterpret_cast<const float*>(xstage) + (2 * tl) * FE_F0 + 4 * i;
       f32x4 A[3];
@@ -448,7 +452,7 @@ __global__ __launch_bounds__(256, 2) void fe_conv0_dw_mfma2_kernel(const float* 
       // used when conv0 of tap t is issued, in loop step t - 1), so they arrive under this tile's
       // MFMAs; the previous tile's staged outputs leave in step 1
       const char* xbn = patch_base(pt + 32 < pend ? pt + 32 : pt);
-      char* sb = os + (FE2_STG == 2 ? (it & 1) : 0) * (4 * 32 * FE2_OPITCH);
+      char* sb = os + (FE2_STG == 2 ? (it & 1) : 0) * (FE2_WAVES * 32 * FE2_OPITCH);
       f32x16 y = seed;
       f32x16 acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, pb[0], zero, 0, 0, 0);
 #pragma unroll
@@ -464,7 +468,7 @@ __global__ __launch_bounds__(256, 2) void fe_conv0_dw_mfma2_kernel(const float* 
         }
         y = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1[s][0], __builtin_bit_cast(bf16x8, r0), y, 0, 0, 0);
         y = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1[s][1], __builtin_bit_cast(bf16x8, r1), y, 0, 0, 0);
-        if (FE2_STG == 2 && s == 1 && it > 0) flush(os + ((it - 1) & 1) * (4 * 32 * FE2_OPITCH), pt - 32);
+        if (FE2_STG == 2 && s == 1 && it > 0) flush(os + ((it - 1) & 1) * (FE2_WAVES * 32 * FE2_OPITCH), pt - 32);
         if (s == 3) {
 #pragma unroll
           for (int t = 0; t < 4; ++t) pb[t] = ld(xbn, t);
@@ -488,7 +492,8 @@ __global__ __launch_bounds__(256, 2) void fe_conv0_dw_mfma2_kernel(const float* 
       }
       if (FE2_STG == 1) flush(sb, pt);
     }
-    if (FE2_STG == 2 && it > 0) flush(os + ((it - 1) & 1) * (4 * 32 * FE2_OPITCH), pend - 1 - ((pend - 1 - p0) % 32));
+    if (FE2_STG == 2 && it > 0)
+      flush(os + ((it - 1) & 1) * (FE2_WAVES * 32 * FE2_OPITCH), pend - 1 - ((pend - 1 - p0) % 32));
   }
 }
 
@@ -566,7 +571,8 @@ int frontend_conv0_dw(const float* feats, const float* const* tab, int step, con
       // "fe_conv" 2 + k: about k + 1 chunks of FE2_POS positions per workgroup, balanced per window
       const int nck = (T2 * FE_F2 + FE2_POS - 1) / FE2_POS, nch = std::max(1, var - 1);
       const int nb = (nck + nch - 1) / nch;
-      hipLaunchKernelGGL(fe_conv0_dw_mfma2_kernel, dim3(nb, (d + 127) / 128, nwin), dim3(256), 0, st, feats, tab, step,
+      hipLaunchKernelGGL(fe_conv0_dw_mfma2_kernel, dim3(nb, (d + 32 * FE2_WAVES - 1) / (32 * FE2_WAVES), nwin), dim3(FE2_NT),
+                         0, st, feats, tab, step,
                          meta, meta_stride, W, T2, cmvn_mean, cmvn_istd, wfrag, d, out);
       CFM_CHECK_LAUNCH();
       return 0;
