@@ -266,7 +266,7 @@ __global__ __launch_bounds__(256, 3) void fe_conv0_dw_mfma_kernel(const float* _
 #define FE2_WAVES 4   // waves (32-channel tiles) per workgroup sharing one im2col build: 4 (2 workgroups per CU) or 8
 #endif
 #ifndef FE2_STG
-#define FE2_STG 2   // output staging buffers per wave (2: a tile's outputs leave during the next tile)
+#define FE2_STG 1   // output staging buffers per wave (2: a tile's outputs leave during the next tile; 2.709 vs 2.688 ms)
 #endif
 constexpr int FE2_POS = FE2_POS_DEF;                                  // dw1 positions per chunk
 constexpr int FE2_T1ROWS = 2 * ((FE_F2 - 1 + FE2_POS - 1) / FE_F2) + 3;   // conv0 rows a chunk can touch
