@@ -107,7 +107,9 @@ cfm_rnnt_error = _sig("cfm_rnnt_error", I32, P, P, I32)
 # include/cfm_ops.h
 cfm_op_gemm = _sig("cfm_op_gemm", I32, I32, I32, I32, P, I32, P, I32, I32, I32, I32, P, ctypes.c_float, P, I32, I32, P,
                    I32, P, I32, P, I32, P)
-EXPORTED_OPS = ["cfm_op_gemm"]
+cfm_op_gemm_rowln = _sig("cfm_op_gemm_rowln", I32, P, I32, P, I32, I32, I32, P, ctypes.c_float, P, P, P,
+                         ctypes.c_float, P, P, P, P, P, P, P, P, P, P, P, ctypes.c_float, I32, P)
+EXPORTED_OPS = ["cfm_op_gemm", "cfm_op_gemm_rowln"]
 
 EXPORTED = ["cfm_version", "cfm_last_error", "cfm_model_create", "cfm_model_destroy", "cfm_model_set_option",
             "cfm_plan_masked", "cfm_plan_masked_ex", "cfm_plan_padded", "cfm_workspace_bytes_masked", "cfm_workspace_bytes_padded",

@@ -38,6 +38,7 @@ struct EpiArgs {
   int wsp_small_div = 1;         // weight-stationary kernel below wsp_small_rows rows: grid = CUs / this
                                  // (leaves CUs to the other streams of a pipelined caller)
   int wsp_small_rows = 32768;
+  int n512 = 0;                  // N = 512, K >= 1024: the full-row 128 x 512 kernel (gemm_rowln.hip, plain form)
   // DW2 (front-end pw1 + ReLU + dw2, K = N = 512 weight-stationary only): dw2 taps tap-major [9][N]
   // f32, bias [N]; the pw1 rows are (window, t2 < t2n, f2 < 19); out = dw2 rows (window, t3 < t3n, f3 < 9)
   const float* dw_w = nullptr;
@@ -47,6 +48,37 @@ struct EpiArgs {
 
 int gemm_bf16_wst(int epi, int act, const bf16* A, int lda, const bf16* W, int ldw, int M, int N, int K,
                   const EpiArgs& ep, hipStream_t st);
+
+// Row-owning GEMM with the sub-block's residual add and LayerNorm(s) in its epilogue (gemm_rowln.hip),
+// N = 512, K % 64 == 0, bf16 operands.  With v = bf16(A . W^T + bias) per row:
+//   xn = x + a1 * y1mask[row] * y1 + alpha * accmask[row] * v     (fmaf, y1 term first; y1 optional)
+//   y_out = v (bf16)                                              (optional: a deferred branch)
+//   one LayerNorm (g2 == null):  x_out = xn;          z = LN(xn; g1, b1)
+//   two LayerNorms:              x_out = LN(xn; g1, b1); z = LN(x_out; g2, b2)
+//   h_out = bf16(z) (rows with hmask 0 -> 0)  or  f_out = z (f32);  x_out may alias x
+// (encoder_layer.py:155-248: the four branch outputs of a layer and the LayerNorm that follows each)
+struct RowLnArgs {
+  const float* bias = nullptr;
+  float alpha = 1.f;
+  const uint8_t* accmask = nullptr;
+  const float* x = nullptr;
+  const bf16* y1 = nullptr;
+  float a1 = 1.f;
+  const uint8_t* y1mask = nullptr;
+  bf16* y_out = nullptr;
+  float* x_out = nullptr;
+  const float *g1 = nullptr, *b1 = nullptr, *g2 = nullptr, *b2 = nullptr;
+  bf16* h_out = nullptr;
+  float* f_out = nullptr;
+  const uint8_t* hmask = nullptr;
+  bf16* ybuf = nullptr;   // [M, 512] bf16 scratch for v when y_out is null (the LayerNorm reads it back)
+  float eps = 1e-5f;
+  int diag = 0;   // timing diagnostics (cfm_op_gemm_rowln variant, CFM_GEMM_DIAG builds): 1 = GEMM only, no LayerNorm
+  int nt = 0;     // plain form: non-temporal y_out stores
+};
+// -1 = not eligible (shape / alignment, K < 512); otherwise a hipError_t.  With g1 == null the same
+// kernel is a plain GEMM: y_out = bf16(acc + bias) or f_out = alpha (acc + bias) (the N = 512 GEMMs of K >= 2048)
+int gemm_rowln_bf16(const bf16* A, int lda, const bf16* W, int ldw, int M, int K, const RowLnArgs& ra, hipStream_t st);
 
 enum { SITE_QKV = 1, SITE_OPROJ = 2, SITE_PW2 = 4, SITE_FFN2 = 8, SITE_FFN1 = 16, SITE_PW1 = 32, SITE_FE = 64 };
 
@@ -74,6 +106,12 @@ struct Tuning {
   int wsp_small_div = 1;         // "wsp_small_div" / "wsp_small_rows" (see EpiArgs)
   int wsp_small_rows = 32768;
   int attn_min_chunks = 2;       // ring attention: chunks per block at least this ("attn_min_chunks")
+  // "gemm_n512": N = 512, K >= 1024 GEMMs on full-row 128 x 512 tiles (gemm_rowln.hip plain form; in the
+  // 240-min step FFN w2 8.20 -> 9.87 ms/step, so off: its A ring is one K-step deep, 160 KiB of LDS)
+  int gemm_n512 = 0;
+  // "ln_fuse": bf16, d = 512: the residual adds and LayerNorms in the four N = 512 GEMMs of a layer (gemm_rowln.hip;
+  // correct, but 47.3 -> 51.9 ms/step in the 240-min step: off, the LayerNorm kernels of norm.hip run)
+  int ln_fuse = 0;
   void apply(EpiArgs& e, int site = 0) const {
     e.diag = gemm_diag;
     e.big_min_tiles = big_min_tiles;
@@ -82,6 +120,7 @@ struct Tuning {
     e.wst = gemm_wst;
     e.store_mode = (nt_sites & site) ? 2 : store_mode;
     e.col_group = col_group;
+    e.n512 = gemm_n512;
   }
 };
 

@@ -348,13 +348,39 @@ struct ModelT : public cfm_model {
         PROF(PC_FFN2, gemm<T>(EPI_STORE, ACT_NONE, w.hid, ff, (const T*)w2, ff, rows, d, ff, e, st)); }
       return CFM_OK;
     };
+    // Fused form (bf16, d = 512, "ln_fuse"): each N = 512 GEMM of the layer owns whole rows
+    // (gemm_rowln.hip) and applies the residual add and the LayerNorm(s) after it in its epilogue, with
+    // the same deferrals as the LayerNorm kernels below: FFN_mac w2 writes y_mac and h = LN_mha(x + 0.5
+    // y_mac) but not x; linear_out writes x += 0.5 y_mac + y_att and h = LN_conv; pointwise_conv2 writes
+    // y_conv and h = LN_ff(x + y_conv) but not x; FFN w2 writes x = LN_fin(x + y_conv + 0.5 y_ffn) and
+    // h = LN_ffm of the next layer (or the after_norm output)
+    bool fused = false;
+    if constexpr (sizeof(T) == 2) fused = tune.ln_fuse && d == 512;
+    auto rowln = [&](int cls, const T* Ain, int K, const void* Wm, const RowLnArgs& a) -> int {
+      int r = -1;
+      if constexpr (sizeof(T) == 2) PROF(cls, (r = gemm_rowln_bf16(Ain, K, (const bf16*)Wm, K, rows, K, a, st), r < 0 ? 0 : r));
+      return r;
+    };
+    auto ln_args = [&](const float* bias, float alpha, const float* g1, const float* b1) {
+      RowLnArgs a; a.bias = bias; a.alpha = alpha; a.x = w.x; a.g1 = g1; a.b1 = b1; a.eps = eps;
+      if constexpr (sizeof(T) == 2) a.h_out = w.h;
+      return a;
+    };
     for (int l = std::max(0, stage_lo); l < nl && l <= stage_hi; ++l) {
       const LayerW& Lw = layers[l];
+      if (fused) {   // macaron FFN: w1 + SiLU, then w2 -> y_mac, h = LN_mha(x + 0.5 y_mac)
+        { EpiArgs e = E(SITE_FFN1); e.bias = Lw.b_ff1m; e.out = w.hid; e.ldo = ff;
+          PROF(PC_FFN1, gemm<T>(EPI_STORE, ACT_SILU, w.h, d, (const T*)Lw.ff1m, d, rows, ff, d, e, st)); }
+        RowLnArgs a = ln_args(Lw.b_ff2m, 0.5f, Lw.ln_mha_w, Lw.ln_mha_b);
+        if constexpr (sizeof(T) == 2) a.y_out = w.y;
+        if (rowln(PC_FFN2, w.hid, ff, Lw.ff2m, a) < 0) return set_error(CFM_ERR_RUNTIME, "fused FFN w2 not eligible");
+      } else {
       // macaron FFN (x 0.5)
       { const cfm_status fs = ffn(Lw.ff1m, Lw.b_ff1m, Lw.ff2m, Lw.b_ff2m, w.y); if (fs != CFM_OK) return fs; }
       // MHSA (x + 0.5 y_ffm is not stored: the conv LayerNorm re-applies it)
       { ResidAdd<T> r = resid(w.y, 0.5f, nullptr); r.defer = true;
         PROF(PC_LN, layernorm<T>(w.x, r, rows, d, Lw.ln_mha_w, Lw.ln_mha_b, eps, w.h, nullptr, st)); }
+      }
       if (aci) {
         if (stream) PROF(PC_CACHE, att_cache_in_hl<T>(aci + l * att_ls, H, L, dk, w.kv, st));
         else PROF(PC_CACHE, att_cache_in<T>(aci + l * att_ls, L, 2 * d, w.kv, st));
@@ -396,17 +422,44 @@ struct ModelT : public cfm_model {
         KCHK(r);
         prof_end(PC_ATTN, st, pb_);
       }
+      if (fused) {   // linear_out: x += 0.5 y_mac + y_att (stored), h = LN_conv(x)
+        RowLnArgs a = ln_args(Lw.b_o, 1.f, Lw.ln_conv_w, Lw.ln_conv_b);
+        a.y1 = reinterpret_cast<const bf16*>(w.y); a.a1 = 0.5f; a.x_out = w.x;
+        a.ybuf = reinterpret_cast<bf16*>(w.y2);
+        a.hmask = (masked || stream) ? nullptr : rmask;
+        if (rowln(PC_OPROJ, w.ao, d, Lw.wo, a) < 0) return set_error(CFM_ERR_RUNTIME, "fused linear_out not eligible");
+      } else {
       { EpiArgs e = E(SITE_OPROJ); e.bias = Lw.b_o; e.out = w.y2; e.ldo = d;
         PROF(PC_OPROJ, gemm<T>(EPI_STORE, ACT_NONE, w.ao, d, (const T*)Lw.wo, d, rows, d, d, e, st)); }
       // convolution module: x += 0.5 y_ffm + y_attn, stored
       PROF(PC_LN, layernorm<T>(w.x, resid2(w.y, 0.5f, nullptr, w.y2, 1.f, nullptr), rows, d, Lw.ln_conv_w, Lw.ln_conv_b,
                                eps, w.h, (masked || stream) ? nullptr : rmask, st));
+      }
       if (cci) PROF(PC_CACHE, cnn_cache_in<T>(cci + l * cnn_ls, d, 7, w.glu, st));
       { EpiArgs e = E(SITE_PW1); e.bias = Lw.b_pw1; e.out = w.glu; e.ldo = d; e.row_off = gluoff;
         PROF(PC_PW1, gemm<T>(EPI_GLU, ACT_NONE, w.h, d, (const T*)Lw.pw1, d, rows, 2 * d, d, e, st)); }
       if (cci && cco) PROF(PC_CACHE, cnn_cache_out<T>(w.glu, cache_start, d, 7, cco + l * cnn_ls, st));
       PROF(PC_CONV, conv_dw_ln_silu<T>(w.glu, convd, nconv, d, Lw.dw_t, Lw.b_dw, Lw.cn_w, Lw.cn_b, eps, w.cv, st,
                                         tune.conv_dot2, tune.conv_dma));
+      if (fused) {   // pointwise_conv2 -> y_conv, h = LN_ff(x + y_conv) (x not stored)
+        RowLnArgs a = ln_args(Lw.b_pw2, 1.f, Lw.ln_ff_w, Lw.ln_ff_b);
+        a.accmask = rmask;
+        if constexpr (sizeof(T) == 2) a.y_out = w.y;
+        if (rowln(PC_PW2, w.cv, d, Lw.pw2, a) < 0) return set_error(CFM_ERR_RUNTIME, "fused pointwise_conv2 not eligible");
+        // FFN: w1 + SiLU, then w2: x = LN_fin(x + y_conv + 0.5 y_ffn), h = next LN_ffm (or after_norm -> out)
+        { EpiArgs e = E(SITE_FFN1); e.bias = Lw.b_ff1; e.out = w.hid; e.ldo = ff;
+          PROF(PC_FFN1, gemm<T>(EPI_STORE, ACT_SILU, w.h, d, (const T*)Lw.ff1, d, rows, ff, d, e, st)); }
+        RowLnArgs f = ln_args(Lw.b_ff2, 0.5f, Lw.ln_fin_w, Lw.ln_fin_b);
+        f.y1 = reinterpret_cast<const bf16*>(w.y); f.a1 = 1.f; f.y1mask = rmask;
+        f.ybuf = reinterpret_cast<bf16*>(w.y2);
+        if (l + 1 < nl) {
+          f.x_out = w.x; f.g2 = layers[l + 1].ln_ffm_w; f.b2 = layers[l + 1].ln_ffm_b;
+        } else {
+          f.g2 = fe.an_w; f.b2 = fe.an_b; f.h_out = nullptr; f.f_out = out;
+        }
+        if (rowln(PC_FFN2, w.hid, ff, Lw.ff2, f) < 0) return set_error(CFM_ERR_RUNTIME, "fused FFN w2 not eligible");
+        continue;
+      }
       { EpiArgs e = E(SITE_PW2); e.bias = Lw.b_pw2; e.out = w.y; e.ldo = d;
         PROF(PC_PW2, gemm<T>(EPI_STORE, ACT_NONE, w.cv, d, (const T*)Lw.pw2, d, rows, d, d, e, st)); }
       // FFN (x 0.5); x + y_conv is not stored: norm_final re-applies it
@@ -738,7 +791,8 @@ cfm_status cfm_model_set_option(cfm_model* m, const char* key, int64_t value) {
         {"attn128_var", &m->tune.attn128_var}, {"attn_q32", &m->tune.attn_q32},
         {"gemm_big_min", &m->tune.big_min_tiles}, {"wsp_small_div", &m->tune.wsp_small_div},
         {"wsp_small_rows", &m->tune.wsp_small_rows},
-        {"attn_min_chunks", &m->tune.attn_min_chunks}};
+        {"attn_min_chunks", &m->tune.attn_min_chunks}, {"ln_fuse", &m->tune.ln_fuse},
+        {"gemm_n512", &m->tune.gemm_n512}};
     for (auto& k : knobs)
       if (!std::strcmp(key, k.first)) { *k.second = (int)value; return CFM_OK; }
   }
@@ -873,12 +927,30 @@ cfm_status cfm_op_gemm(int32_t dtype, int32_t epi, int32_t act, const void* A, i
   e.rowmask = rowmask; e.d = d; e.small_tiles = variant & 1; e.diag = (variant >> 8) & 0xff;
   e.store_mode = (variant >> 16) & 3;
   if ((variant >> 18) & 7) e.wst = ((variant >> 18) & 7) == 7 ? 0 : (variant >> 18) & 7;
+  if ((variant >> 21) & 1) e.n512 = 1;
   int r;
   if (dtype == CFM_DTYPE_F32)
     r = gemm<float>(epi, act, (const float*)A, lda, (const float*)W, ldw, M, N, K, e, (hipStream_t)stream);
   else
     r = gemm<bf16>(epi, act, (const bf16*)A, lda, (const bf16*)W, ldw, M, N, K, e, (hipStream_t)stream);
   if (r) return set_error(CFM_ERR_RUNTIME, std::string("gemm: ") + hipGetErrorString((hipError_t)r));
+  return CFM_OK;
+}
+
+cfm_status cfm_op_gemm_rowln(const void* A, int32_t lda, const void* W, int32_t ldw, int32_t M, int32_t K,
+                             const float* bias, float alpha, const uint8_t* accmask, const float* x, const void* y1,
+                             float a1, const uint8_t* y1mask, void* y_out, float* x_out, const float* g1,
+                             const float* b1, const float* g2, const float* b2, void* h_out, float* f_out,
+                             const uint8_t* hmask, void* ybuf, float eps, int32_t variant, cfm_stream stream) {
+  RowLnArgs a;
+  a.diag = variant;
+  a.ybuf = (bf16*)ybuf;
+  a.bias = bias; a.alpha = alpha; a.accmask = accmask; a.x = x; a.y1 = (const bf16*)y1; a.a1 = a1; a.y1mask = y1mask;
+  a.y_out = (bf16*)y_out; a.x_out = x_out; a.g1 = g1; a.b1 = b1; a.g2 = g2; a.b2 = b2; a.h_out = (bf16*)h_out;
+  a.f_out = h_out ? nullptr : f_out; a.hmask = hmask; a.eps = eps;
+  const int r = gemm_rowln_bf16((const bf16*)A, lda, (const bf16*)W, ldw, M, K, a, (hipStream_t)stream);
+  if (r == -1) return set_error(CFM_ERR_VALUE, "gemm_rowln: shape or arguments not eligible");
+  if (r) return set_error(CFM_ERR_RUNTIME, std::string("gemm_rowln: ") + hipGetErrorString((hipError_t)r));
   return CFM_OK;
 }
 
