@@ -505,6 +505,11 @@ def main():
                        "heads": cfg.n_heads, "head_dim": cfg.head_dim,
                        "pieces_rank0": len(mine), "chunks_rank0": n_chunks, "frames_total": int(total_frames),
                        "parallelism": f"dp{world} ({'plan_shards: LPT pieces, halo cuts' if sharded else 'LPT utterance sharding'})"},
+            # ranks vs physical GPUs: world > devices is a gloo rehearsal of the multi-rank path on one GPU
+            # (the ranks share it), not a scaling measurement
+            "devices": min(world, ndev),
+            "backend": (dist.get_backend() if world > 1 else None),
+            "rehearsal": world > ndev,
             "roofline": {"bound": "mfma", "kernel": roof_name,
                          "achieved": round(achieved, 1) if achieved else None, "peak": peak, "unit": "TFLOP/s",
                          "frac": round(achieved / peak, 4) if achieved else None, "traffic": traffic,

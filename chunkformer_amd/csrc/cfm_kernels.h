@@ -90,7 +90,9 @@ struct Tuning {
   int conv_dma = 1;              // conv module: LDS-DMA window staging (0: register staging)
   int dw2_seg = 4;               // front-end dw2: row segments per walk
   int fe_conv = 6;               // bf16 front-end conv0+dw1: 1 = position-stationary (dw1 on VALU), 2 + k = channel-
-                                 // stationary with dw1 on MFMA, ~k + 1 chunks per workgroup (2.74 vs 3.10 ms/step)
+                                 // stationary with dw1 on MFMA, ~k + 1 chunks per workgroup (2.74 vs 3.10 ms/step);
+                                 // its ReLU is a clamp valid for |conv0| < 2^24 (NaN -> 0): models without CMVN
+                                 // are created with 1 (build_model)
   int fe_fuse_dw2 = 1;           // front-end: pw1 + ReLU + dw2 in one weight-stationary GEMM (bf16; bench A/B
                                  // 50.85 -> 50.15 ms/step, 3 interleaved pairs; 0 = pw1 GEMM + fe_dw2_kernel)
   int attn128_var = 1;           // head_dim 128 attention kernel variant (A/B)

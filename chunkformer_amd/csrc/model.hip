@@ -737,6 +737,11 @@ static cfm_status build_model(const cfm_config& cfg, const HostW& hw, int device
   } catch (const std::string& e) {
     return set_error(CFM_ERR_VALUE, e);
   }
+  // the channel-stationary front-end (fe_conv >= 2) applies conv0's ReLU as the bf16 conversion's clamp on
+  // values scaled by 2^-24: exact while |conv0| < 2^24, which CMVN-normalised features keep by orders of
+  // magnitude; without CMVN the raw features are not bounded by construction, so such a model keeps the
+  // position-stationary kernel (fe_conv 1: an f32 max, no saturation).  Neither propagates a NaN input.
+  if (!cfg.has_cmvn) M->tune.fe_conv = 1;
   HIPC(hipSetDevice(device));
   HIPC(hipMalloc(&M->dev_mem, img.size()));
   HIPC(hipMemcpy(M->dev_mem, img.data(), img.size(), hipMemcpyHostToDevice));

@@ -413,6 +413,9 @@ __global__ __launch_bounds__(RG_NT) void rnnt_grid_kernel(RnntDev w, RnntGrid gw
                                                           int32_t* __restrict__ out) {
   extern __shared__ float lds[];
   const int tid = threadIdx.x;
+  // an error word set before the launch (option grid_force_error, tests of the caller's fallback): every
+  // workgroup leaves before its first barrier
+  if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
   const int G = gw.G, utt = blockIdx.x / G, part = blockIdx.x - utt * G;
   const int H = w.H, J = w.J, P = w.P, E = w.E, nl = w.nl;
   const int r0 = row_start[utt], T = row_len[utt];
@@ -634,6 +637,7 @@ struct cfm_rnnt {
   int grid_blocks = 32;                       // 0: always one workgroup per utterance
   int grid_lds = 1;                           // cache the grid path's weight slices in LDS when they fit
   int grid_atomic = 1;                        // exchanged vectors by agent-scope atomics, no cache-wide fences
+  int grid_force_error = 0;                   // test hook: the grid search starts with its error word set
   int n_cu = 0;
   void* grid_mem = nullptr;
   cfm::RnntGrid gw{};
@@ -864,14 +868,22 @@ cfm_status cfm_rnnt_set_option(cfm_rnnt* h, const char* key, int64_t value) {
     h->grid_atomic = value != 0;
     return CFM_OK;
   }
+  if (std::string(key) == "grid_force_error") {
+    h->grid_force_error = value != 0;
+    return CFM_OK;
+  }
   return set_error(CFM_ERR_VALUE, std::string("unknown rnnt option ") + key);
 }
 
 int32_t cfm_rnnt_grid_blocks(const cfm_rnnt* h, int32_t B) {
   if (!h || B <= 0 || h->grid_blocks <= 0 || B > RG_MAXB || (int64_t)B * h->grid_blocks > h->n_cu) return 0;
+  const int G = h->grid_blocks;
   // the joint's per-workgroup candidates reuse the z block: <= 64 column groups per workgroup, J >= 128
-  if ((h->w.Vp / 4 + h->grid_blocks - 1) / h->grid_blocks > 64 || h->w.J < 128) return 0;
-  return h->grid_blocks;
+  if ((h->w.Vp / 4 + G - 1) / G > 64 || h->w.J < 128) return 0;
+  // rg_matvec gives every output column of a slice its own thread: the LSTM units (ceil(H / G)) and the
+  // composed projection's column quads (ceil(P / 4 / G)) of one workgroup must fit in its RG_NT threads
+  if ((h->w.H + G - 1) / G > RG_NT || (h->w.P / 4 + G - 1) / G > RG_NT) return 0;
+  return G;
 }
 
 int32_t cfm_rnnt_error(const cfm_rnnt* h, const void* ws, int32_t rows) {
@@ -908,32 +920,43 @@ cfm_status cfm_rnnt_greedy(const cfm_rnnt* h, const float* enc, int32_t rows, co
     unsigned long long* bars = (unsigned long long*)(gbase + (size_t)RG_MAXB * per * 4);
     int* err = (int*)((char*)bars + (size_t)RG_MAXB * RG_MAXG * 8);
     if (hipMemsetAsync(scratch, 0, (size_t)B * per * 4, st) != hipSuccess ||
-        hipMemsetAsync(bars, 0, (size_t)RG_MAXB * RG_MAXG * 8 + 256, st) != hipSuccess)
+        hipMemsetAsync(bars, 0, (size_t)RG_MAXB * RG_MAXG * 8 + 256, st) != hipSuccess ||
+        (h->grid_force_error && hipMemsetAsync(err, 1, 1, st) != hipSuccess))
       return set_error(CFM_ERR_RUNTIME, "rnnt: workspace memset");
     // the largest workgroup's weight slices (float4s): cached in LDS when they fit beside the work area
     const RnntDev& w = h->w;
     auto cdiv = [&](int a) { return (size_t)((a + G - 1) / G); };
     size_t slice4 = 0;
     for (int l = 0, in = w.E; l < w.nl; ++l, in = w.H) slice4 += (size_t)(in + w.H) * cdiv(w.H);
-    slice4 += (size_t)w.H * cdiv(w.P / 4) + (size_t)w.P * cdiv(w.J / 4) + (size_t)w.J * cdiv(w.Vp / 4);
+    slice4 += (size_t)w.H * cdiv(w.P / 4) + (size_t)w.J * cdiv(w.Vp / 4);   // what the kernel copies: wp, wo
     const size_t work = rnnt_grid_lds_bytes(w);
     const bool cache = h->grid_lds && work + slice4 * 16 <= 160 * 1024;
     const size_t glds = work + (cache ? slice4 * 16 : 0);
-    auto launch = [&](auto kern) -> bool {
+    // 0 = launched, 1 = the kernel cannot hold a workgroup on a CU at this LDS size (one-workgroup path instead),
+    // -1 = error.  The grid barriers need all B * G workgroups resident at once: B * G <= CUs is checked by
+    // cfm_rnnt_grid_blocks, one workgroup per CU by the occupancy query; a barrier that still times out (CUs
+    // held by another stream's kernels) sets the error word and RNNTGreedy.greedy_packed reruns the search on
+    // the one-workgroup kernel
+    auto launch = [&](auto kern) -> int {
       if (glds > 64 * 1024 &&
           hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)glds) != hipSuccess)
-        return false;
+        return -1;
+      int per_cu = 0;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, RG_NT, glds) != hipSuccess) return -1;
+      if (per_cu < 1) return 1;
       hipLaunchKernelGGL(kern, dim3(B * G), dim3(RG_NT), glds, st, h->w, h->gw, scratch, (int)per, bars, err, proj,
                          row_start, row_len, n_steps, out);
-      return true;
+      return 0;
     };
     const bool atom = h->grid_atomic != 0;
-    const bool okl = cache ? (atom ? launch(rnnt_grid_kernel<true, true>) : launch(rnnt_grid_kernel<true, false>))
-                           : (atom ? launch(rnnt_grid_kernel<false, true>) : launch(rnnt_grid_kernel<false, false>));
-    if (!okl) return set_error(CFM_ERR_RUNTIME, "rnnt: dynamic LDS attribute");
-    const hipError_t ge = hipGetLastError();
-    if (ge != hipSuccess) return set_error(CFM_ERR_RUNTIME, std::string("rnnt_grid_kernel: ") + hipGetErrorString(ge));
-    return CFM_OK;
+    const int okl = cache ? (atom ? launch(rnnt_grid_kernel<true, true>) : launch(rnnt_grid_kernel<true, false>))
+                          : (atom ? launch(rnnt_grid_kernel<false, true>) : launch(rnnt_grid_kernel<false, false>));
+    if (okl < 0) return set_error(CFM_ERR_RUNTIME, "rnnt: dynamic LDS attribute / occupancy query");
+    if (okl == 0) {
+      const hipError_t ge = hipGetLastError();
+      if (ge != hipSuccess) return set_error(CFM_ERR_RUNTIME, std::string("rnnt_grid_kernel: ") + hipGetErrorString(ge));
+      return CFM_OK;
+    }
   }
   const size_t lds = rnnt_lds_bytes(h->w);
   if (lds > 64 * 1024 &&

@@ -137,6 +137,7 @@ class RNNTGreedy:
             _lib.check(_lib.cfm_rnnt_create(ctypes.byref(c), views, len(names), self.device.index or 0,
                                             ctypes.byref(h)))
         self._h = h
+        self.grid_fallbacks = 0   # searches the multi-CU kernel left early (barrier timeout), rerun on one workgroup
         self._finalizer = weakref.finalize(self, _lib.cfm_rnnt_destroy, ctypes.c_void_p(h.value))
 
     def set_option(self, key: str, value: int) -> None:
@@ -173,11 +174,23 @@ class RNNTGreedy:
                                         int(n_steps), out.data_ptr(), ws.data_ptr(), nbytes,
                                         torch.cuda.current_stream(self.device).cuda_stream))
         self._keep = (rs_d, rl_d, ws)   # alive until the stream consumed them
-        if self.grid_blocks(B):
-            # the multi-CU search stops early if a grid barrier timed out: never return a partial result
+        G = self.grid_blocks(B)
+        if G:
+            # the multi-CU search stops early if a grid barrier timed out (its workgroups were not all resident:
+            # CUs held by another stream's kernels): never return that partial result, run the search again
+            # on the one-workgroup kernel, which needs no co-residency
             torch.cuda.current_stream(self.device).synchronize()
             if int(_lib.cfm_rnnt_error(self._h, ws.data_ptr(), rows)) != 0:
-                raise RuntimeError("cfm_rnnt_greedy: multi-CU search barrier timed out")
+                self.grid_fallbacks += 1
+                self.set_option("grid_blocks", 0)
+                try:
+                    out.zero_()
+                    _lib.check(_lib.cfm_rnnt_greedy(self._h, enc.data_ptr(), rows, rs_d.data_ptr(), rl_d.data_ptr(),
+                                                    B, int(n_steps), out.data_ptr(), ws.data_ptr(), nbytes,
+                                                    torch.cuda.current_stream(self.device).cuda_stream))
+                    torch.cuda.current_stream(self.device).synchronize()
+                finally:
+                    self.set_option("grid_blocks", G)
         return out
 
     @torch.no_grad()

@@ -210,3 +210,42 @@ def test_grid_search_equals_one_workgroup(G, B):
         out = dec.greedy_packed(enc, starts, lens, 4).cpu()
         assert (ref != 0).any() and (ref == 0).any()
         np.testing.assert_array_equal(out.numpy(), ref.numpy())
+
+
+def test_grid_slices_wider_than_a_workgroup_use_one_workgroup():
+    """with G workgroups per utterance every LSTM unit (ceil(H / G)) and projection column quad of a
+    workgroup's slice needs a thread of its own (rg_matvec); a small vocabulary with H = 640 at G = 2 would
+    give 320 > 256 units per workgroup.  cfm_rnnt_grid_blocks refuses it (0: the one-workgroup kernel), and
+    the decisions are the one-workgroup kernel's."""
+    from chunkformer_amd.transducer import RNNTConfig, RNNTGreedy, synthetic_transducer_state_dict
+    c = RNNTConfig(vocab=200, hidden=640, num_layers=1, embed_size=128, pred_out=256, join_dim=256)
+    dec = RNNTGreedy(c, synthetic_transducer_state_dict(c, 3, blank_bias=4.0), "cuda")
+    gen = torch.Generator().manual_seed(5)
+    enc = torch.randn(90, c.enc_dim, generator=gen).cuda()
+    dec.set_option("grid_blocks", 0)
+    ref = dec.greedy_packed(enc, [0], [90], 3).cpu()
+    for G in (1, 2):
+        dec.set_option("grid_blocks", G)
+        assert dec.grid_blocks(1) == 0
+        np.testing.assert_array_equal(dec.greedy_packed(enc, [0], [90], 3).cpu().numpy(), ref.numpy())
+    dec.set_option("grid_blocks", 3)   # ceil(640 / 3) = 214 units per workgroup: the grid kernel runs
+    assert dec.grid_blocks(1) == 3
+    np.testing.assert_array_equal(dec.greedy_packed(enc, [0], [90], 3).cpu().numpy(), ref.numpy())
+
+
+def test_grid_barrier_error_falls_back_to_one_workgroup():
+    """A multi-CU search that left early (its error word set: a grid barrier that timed out because other
+    kernels held CUs) is rerun on the one-workgroup kernel, not returned and not raised."""
+    from chunkformer_amd.transducer import RNNTConfig, RNNTGreedy, synthetic_transducer_state_dict
+    c = RNNTConfig(vocab=1001, hidden=256, num_layers=1, embed_size=128, pred_out=256, join_dim=384)
+    dec = RNNTGreedy(c, synthetic_transducer_state_dict(c, 7, blank_bias=5.0), "cuda")
+    gen = torch.Generator().manual_seed(11)
+    enc = torch.randn(300, c.enc_dim, generator=gen).cuda()
+    dec.set_option("grid_blocks", 0)
+    ref = dec.greedy_packed(enc, [0], [300], 4).cpu()
+    dec.set_option("grid_blocks", 32)
+    dec.set_option("grid_force_error", 1)
+    out = dec.greedy_packed(enc, [0], [300], 4).cpu()
+    dec.set_option("grid_force_error", 0)
+    assert dec.grid_fallbacks == 1 and dec.grid_blocks(1) == 32
+    np.testing.assert_array_equal(out.numpy(), ref.numpy())

@@ -152,6 +152,9 @@ def test_configs2_980min_world8_golden():
         # margin exceeds 5e-2, >= 99% agreement over the golden frames (one near-tie flip is 1.4% of the
         # 6 s utterance's 74 frames, so the 99% bar is the aggregate one)
         np.testing.assert_array_equal(i[m > 5e-2], ei[m > 5e-2])
+        # and a per-utterance floor: at most 2% of an utterance's ids (one flip for the 6 s one),
+        # so a regression confined to one shard cannot hide in the aggregate
+        assert int((i != ei).sum()) <= max(1, int(0.02 * len(i))), (k, int((i != ei).sum()), len(i))
         agree.append(i == ei)
     assert np.concatenate(agree).mean() >= 0.99
     # every utterance against the unsharded run of the same batch
