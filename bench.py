@@ -57,7 +57,7 @@ from chunkformer_amd.encoder import ChunkFormerEncoder  # noqa: E402
 from chunkformer_amd.weights import synthetic_state_dict  # noqa: E402
 
 METRIC = "audio-frames/sec (80-dim fbank) through encoder, chunkformer-large chunk=64, 1/2/4/8 GPU"
-PEAK_TFLOPS = {"bf16": 2500.0, "fp32": 157.3}   # MI355X dense MFMA peaks (MI355X_MICROARCH.md)
+PEAK_TFLOPS = {"bf16": 2500.0, "fp16": 2500.0, "fp32": 157.3}   # MI355X dense MFMA peaks (MI355X_MICROARCH.md)
 MEASURED_BF16_CEILING = 1833.8   # TFLOP/s, tools/mfma_peak.hip on this pool
 HIPBLASLT_W1 = 706.8             # TFLOP/s, hipBLASLt M=182080 N=2048 K=512 bf16
 C, L, R = 64, 128, 128
@@ -267,7 +267,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp16", "fp32"])
     ap.add_argument("--minutes", type=float, default=None,
                     help="audio minutes: per GPU for masked (240), of the whole batch for sharded (980)")
     ap.add_argument("--no-gather-logp", action="store_true", help="sharded: skip the bf16 log-prob all-gather")
@@ -381,7 +381,8 @@ def main():
     d_, ff_ = cfg.d_model, cfg.ffn_dim
     roof_cls = "ffn_w1_gemm"
     roof_name = ("ffn_w1_gemm (gemm_wsp_kernel<EPI_STORE,SiLU>: K=512 weight-stationary bf16 MFMA)"
-                 if args.dtype == "bf16" else "ffn_w1_gemm (gemm_kernel<float,EPI_STORE,SiLU>)")
+                 if args.dtype == "bf16" else f"ffn_w1_gemm (gemm_kernel<{'_Float16' if args.dtype == 'fp16' else 'float'},"
+                 "EPI_STORE,SiLU>)")
     # per step: one w_1 launch per layer and utterance group (enc.stream_split groups of the batch run
     # on their own streams, so a launch covers rows / groups rows); totals over the timed launches
     # (two FFNs per layer: the macaron and the final one)

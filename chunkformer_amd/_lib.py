@@ -30,7 +30,7 @@ PI32 = ctypes.POINTER(ctypes.c_int32)
 PI64 = ctypes.POINTER(ctypes.c_int64)
 
 CFM_OK, CFM_ERR_VALUE, CFM_ERR_ASSERT, CFM_ERR_RUNTIME = 0, 1, 2, 3
-DTYPE_F32, DTYPE_BF16 = 0, 1
+DTYPE_F32, DTYPE_BF16, DTYPE_F16 = 0, 1, 2
 PLAN_HEADER = 16
 PLAN_REC = 8
 

@@ -209,6 +209,8 @@ template int chunk_attention<float>(const float*, const float*, int, const float
                                     const int32_t*, int, int, int, float*, hipStream_t, int);
 template int chunk_attention<bf16>(const bf16*, const bf16*, int, const bf16*, int, const float*, const float*,
                                    const int32_t*, int, int, int, bf16*, hipStream_t, int);
+template int chunk_attention<f16>(const f16*, const f16*, int, const f16*, int, const float*, const float*,
+                                   const int32_t*, int, int, int, f16*, hipStream_t, int);
 
 
 

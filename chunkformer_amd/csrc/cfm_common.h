@@ -1,9 +1,10 @@
 // Common device/host helpers for the gfx950 (CDNA4) ChunkFormer kernels.
 //
-// Element type T of every activation/weight stream is either `float` (parity
-// mode: exact-f32 MFMA v_mfma_f32_16x16x4_f32) or `bf16` (fast mode:
-// v_mfma_f32_16x16x32_bf16).  Accumulation, softmax and LayerNorm statistics
-// are always f32.  Both operand types share ONE fragment abstraction: a lane
+// Element type T of every activation/weight stream is `float` (parity
+// mode: exact-f32 MFMA v_mfma_f32_16x16x4_f32), `bf16` (fast mode:
+// v_mfma_f32_16x16x32_bf16) or `f16` (the reference's --autocast_dtype fp16:
+// v_mfma_f32_16x16x32_f16 on the generic kernels).  Accumulation, softmax and
+// LayerNorm statistics are always f32.  Both operand types share ONE fragment abstraction: a lane
 // holds 8 consecutive K elements of its row (A) / column (B); for bf16 that is
 // one 16x16x32 MFMA, for f32 eight 16x16x4 MFMAs (instruction e consumes
 // element e of every lane: k = 8*(lane>>4) + e).  Any consistent K permutation
@@ -17,6 +18,8 @@
 
 typedef __bf16 bf16;
 typedef bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16;
+typedef f16 f16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x8 __attribute__((ext_vector_type(8)));
@@ -36,12 +39,15 @@ CFM_DEV void sfor(F&& f) {
 template <typename T> struct Frag;
 template <> struct Frag<float> { typedef f32x8 type; };
 template <> struct Frag<bf16> { typedef bf16x8 type; };
+template <> struct Frag<f16> { typedef f16x8 type; };
 
 CFM_DEV float to_f32(float x) { return x; }
 CFM_DEV float to_f32(bf16 x) { return (float)x; }
+CFM_DEV float to_f32(f16 x) { return (float)x; }
 template <typename T> CFM_DEV T from_f32(float x);
 template <> CFM_DEV float from_f32<float>(float x) { return x; }
 template <> CFM_DEV bf16 from_f32<bf16>(float x) { return (bf16)x; }
+template <> CFM_DEV f16 from_f32<f16>(float x) { return (f16)x; }
 
 // 16x16 output tile += A(16 x 32) * B(32 x 16) expressed on 8-element fragments
 CFM_DEV f32x4 mma16(const f32x8& a, const f32x8& b, f32x4 acc) {
@@ -51,6 +57,9 @@ CFM_DEV f32x4 mma16(const f32x8& a, const f32x8& b, f32x4 acc) {
 }
 CFM_DEV f32x4 mma16(const bf16x8& a, const bf16x8& b, f32x4 acc) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc, 0, 0, 0);
+}
+CFM_DEV f32x4 mma16(const f16x8& a, const f16x8& b, f32x4 acc) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, acc, 0, 0, 0);
 }
 
 // load 8 consecutive elements (16 B for bf16, 32 B for f32)
@@ -71,6 +80,11 @@ CFM_DEV void load8(const bf16* p, float* x) {
 #pragma unroll
   for (int q = 0; q < 8; ++q) x[q] = (float)a[q];
 }
+CFM_DEV void load8(const f16* p, float* x) {
+  const f16x8 a = *reinterpret_cast<const f16x8*>(p);
+#pragma unroll
+  for (int q = 0; q < 8; ++q) x[q] = (float)a[q];
+}
 CFM_DEV void store8(float* p, const float* x) {
   *reinterpret_cast<f32x4*>(p) = (f32x4){x[0], x[1], x[2], x[3]};
   *reinterpret_cast<f32x4*>(p + 4) = (f32x4){x[4], x[5], x[6], x[7]};
@@ -80,6 +94,12 @@ CFM_DEV void store8(bf16* p, const float* x) {
 #pragma unroll
   for (int q = 0; q < 8; ++q) v[q] = (bf16)x[q];
   *reinterpret_cast<bf16x8*>(p) = v;
+}
+CFM_DEV void store8(f16* p, const float* x) {
+  f16x8 v;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) v[q] = (f16)x[q];
+  *reinterpret_cast<f16x8*>(p) = v;
 }
 
 template <typename T> CFM_DEV typename Frag<T>::type zero8() {

@@ -38,23 +38,22 @@ template <int VPL> struct VecIO<float, VPL> {
     }
   }
 };
-template <int VPL> struct VecIO<bf16, VPL> {
-  static CFM_DEV void load(const bf16* p, float (&v)[VPL]) {
+template <typename H, int VPL> struct VecIO16 {   // bf16 / f16 streams
+  typedef H h2 __attribute__((ext_vector_type(2)));
+  static CFM_DEV void load(const H* p, float (&v)[VPL]) {
 #pragma unroll
     for (int e = 0; e < VPL; e += 2) {
-      typedef bf16 b2 __attribute__((ext_vector_type(2)));
-      const b2 t = *reinterpret_cast<const b2*>(p + e);
+      const h2 t = *reinterpret_cast<const h2*>(p + e);
       v[e] = (float)t[0]; v[e + 1] = (float)t[1];
     }
   }
-  static CFM_DEV void store(bf16* p, const float (&v)[VPL]) {
+  static CFM_DEV void store(H* p, const float (&v)[VPL]) {
 #pragma unroll
-    for (int e = 0; e < VPL; e += 2) {
-      typedef bf16 b2 __attribute__((ext_vector_type(2)));
-      *reinterpret_cast<b2*>(p + e) = (b2){(bf16)v[e], (bf16)v[e + 1]};
-    }
+    for (int e = 0; e < VPL; e += 2) *reinterpret_cast<h2*>(p + e) = (h2){(H)v[e], (H)v[e + 1]};
   }
 };
+template <int VPL> struct VecIO<bf16, VPL> : VecIO16<bf16, VPL> {};
+template <int VPL> struct VecIO<f16, VPL> : VecIO16<f16, VPL> {};
 
 template <typename T, int VPL>
 __global__ __launch_bounds__(256) void conv_dw_ln_silu_kernel(const T* __restrict__ glu, const int32_t* __restrict__ desc,
@@ -417,5 +416,7 @@ template int conv_dw_ln_silu<float>(const float*, const int32_t*, int, int, cons
                                     const float*, float, float*, hipStream_t, int, int);
 template int conv_dw_ln_silu<bf16>(const bf16*, const int32_t*, int, int, const float*, const float*, const float*,
                                    const float*, float, bf16*, hipStream_t, int, int);
+template int conv_dw_ln_silu<f16>(const f16*, const int32_t*, int, int, const float*, const float*, const float*,
+                                   const float*, float, f16*, hipStream_t, int, int);
 
 }  // namespace cfm

@@ -608,7 +608,11 @@ template int frontend_conv0_dw<float>(const float*, const float* const*, int, co
 template int frontend_conv0_dw<bf16>(const float*, const float* const*, int, const int32_t*, int, int, int, const float*,
                                      const float*,
                                      const float*, const float*, const float*, const float*, const float*, const float*, int, bf16*, hipStream_t, int);
+template int frontend_conv0_dw<f16>(const float*, const float* const*, int, const int32_t*, int, int, int, const float*,
+                                     const float*,
+                                     const float*, const float*, const float*, const float*, const float*, const float*, int, f16*, hipStream_t, int);
 template int frontend_dw2<float>(const float*, int, int, int, const float*, const float*, float*, hipStream_t, int);
 template int frontend_dw2<bf16>(const bf16*, int, int, int, const float*, const float*, bf16*, hipStream_t, int);
+template int frontend_dw2<f16>(const f16*, int, int, int, const float*, const float*, f16*, hipStream_t, int);
 
 }  // namespace cfm

@@ -106,8 +106,8 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const T* __restrict__ A, i
         const int ra_ = wm * 64 + i * 16 + fr, rb_ = wn * 64 + i * 16 + fr;
         if constexpr (sizeof(T) == 2) {
           const int ch = s * 4 + g;
-          af[i] = *reinterpret_cast<const bf16x8*>(as + swz(ra_, ch));
-          bfr[i] = *reinterpret_cast<const bf16x8*>(ws + swz(rb_, ch));
+          af[i] = *reinterpret_cast<const typename Frag<T>::type*>(as + swz(ra_, ch));
+          bfr[i] = *reinterpret_cast<const typename Frag<T>::type*>(ws + swz(rb_, ch));
         } else {
           f32x4 lo = *reinterpret_cast<const f32x4*>(as + swz(ra_, 2 * g));
           f32x4 hi = *reinterpret_cast<const f32x4*>(as + swz(ra_, 2 * g + 1));
@@ -204,7 +204,7 @@ int gemm_bf16_big(int epi, int act, const bf16* A, int lda, const bf16* W, int l
 template <typename T>
 int gemm(int epi, int act, const T* A, int lda, const T* W, int ldw, int M, int N, int K, const EpiArgs& ep,
          hipStream_t st) {
-  if constexpr (sizeof(T) == 2) {
+  if constexpr (std::is_same<T, bf16>::value) {
     if (!ep.small_tiles) {
       const int r = gemm_bf16_big(epi, act, A, lda, W, ldw, M, N, K, ep, st);
       if (r != -1) return r;
@@ -225,5 +225,6 @@ int gemm(int epi, int act, const T* A, int lda, const T* W, int ldw, int M, int 
 
 template int gemm<float>(int, int, const float*, int, const float*, int, int, int, int, const EpiArgs&, hipStream_t);
 template int gemm<bf16>(int, int, const bf16*, int, const bf16*, int, int, int, int, const EpiArgs&, hipStream_t);
+template int gemm<f16>(int, int, const f16*, int, const f16*, int, int, int, int, const EpiArgs&, hipStream_t);
 
 }  // namespace cfm

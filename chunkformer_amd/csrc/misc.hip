@@ -175,17 +175,24 @@ int log_softmax_rows(float* logits, int M, int V, int write_logp, int32_t* ids, 
 
 template int pos_table<float>(int, int, int, float*, hipStream_t);
 template int pos_table<bf16>(int, int, int, bf16*, hipStream_t);
+template int pos_table<f16>(int, int, int, f16*, hipStream_t);
 template int att_cache_in<float>(const float*, int, int, float*, hipStream_t);
 template int att_cache_in<bf16>(const float*, int, int, bf16*, hipStream_t);
+template int att_cache_in<f16>(const float*, int, int, f16*, hipStream_t);
 template int att_cache_out<float>(const float*, int, int, int, float*, hipStream_t);
 template int att_cache_out<bf16>(const bf16*, int, int, int, float*, hipStream_t);
+template int att_cache_out<f16>(const f16*, int, int, int, float*, hipStream_t);
 template int att_cache_in_hl<float>(const float*, int, int, int, float*, hipStream_t);
 template int att_cache_in_hl<bf16>(const float*, int, int, int, bf16*, hipStream_t);
+template int att_cache_in_hl<f16>(const float*, int, int, int, f16*, hipStream_t);
 template int att_cache_out_hl<float>(const float*, int, int, int, int, float*, hipStream_t);
 template int att_cache_out_hl<bf16>(const bf16*, int, int, int, int, float*, hipStream_t);
+template int att_cache_out_hl<f16>(const f16*, int, int, int, int, float*, hipStream_t);
 template int cnn_cache_in<float>(const float*, int, int, float*, hipStream_t);
 template int cnn_cache_in<bf16>(const float*, int, int, bf16*, hipStream_t);
+template int cnn_cache_in<f16>(const float*, int, int, f16*, hipStream_t);
 template int cnn_cache_out<float>(const float*, int, int, int, float*, hipStream_t);
 template int cnn_cache_out<bf16>(const bf16*, int, int, int, float*, hipStream_t);
+template int cnn_cache_out<f16>(const f16*, int, int, int, float*, hipStream_t);
 
 }  // namespace cfm

@@ -199,7 +199,7 @@ struct ModelT : public cfm_model {
   };
   // the head_dim 128 attention kernel's V^T buffer is needed (bf16 masked batch)
   bool uses_vt(const int32_t* h) const {
-    return sizeof(T) == 2 && h[PH_KIND] == 1 && use_ring_attention && cfg.d_model == 128 * cfg.n_heads &&
+    return std::is_same<T, bf16>::value && h[PH_KIND] == 1 && use_ring_attention && cfg.d_model == 128 * cfg.n_heads &&
            attention_a128_eligible(h[PH_C], h[PH_L] + h[PH_C] + h[PH_R], h[PH_PROWS], 128);
   }
 
@@ -246,7 +246,7 @@ struct ModelT : public cfm_model {
   size_t ctc_ws_bytes(int rows) const override {
     return align_up((size_t)rows * cfg.vocab * sizeof(float)) + align_up((size_t)rows * cfg.d_model * sizeof(T)) + 4096;
   }
-  bool fused_ctc_ok() const { return sizeof(T) == 2 && use_fused_ctc && ctc_argmax_eligible(cfg.vocab, cfg.d_model); }
+  bool fused_ctc_ok() const { return std::is_same<T, bf16>::value && use_fused_ctc && ctc_argmax_eligible(cfg.vocab, cfg.d_model); }
   size_t ctc_ids_ws_bytes(int rows) const override { return fused_ctc_ok() ? 0 : ctc_ws_bytes(rows); }
 
   cfm_status encode(const float* feats, const int32_t* plan_dev, const int32_t* hh, const float* aci, const float* cci,
@@ -355,15 +355,15 @@ struct ModelT : public cfm_model {
     // y_conv and h = LN_ff(x + y_conv) but not x; FFN w2 writes x = LN_fin(x + y_conv + 0.5 y_ffn) and
     // h = LN_ffm of the next layer (or the after_norm output)
     bool fused = false;
-    if constexpr (sizeof(T) == 2) fused = tune.ln_fuse && d == 512;
+    if constexpr (std::is_same<T, bf16>::value) fused = tune.ln_fuse && d == 512;
     auto rowln = [&](int cls, const T* Ain, int K, const void* Wm, const RowLnArgs& a) -> int {
       int r = -1;
-      if constexpr (sizeof(T) == 2) PROF(cls, (r = gemm_rowln_bf16(Ain, K, (const bf16*)Wm, K, rows, K, a, st), r < 0 ? 0 : r));
+      if constexpr (std::is_same<T, bf16>::value) PROF(cls, (r = gemm_rowln_bf16(Ain, K, (const bf16*)Wm, K, rows, K, a, st), r < 0 ? 0 : r));
       return r;
     };
     auto ln_args = [&](const float* bias, float alpha, const float* g1, const float* b1) {
       RowLnArgs a; a.bias = bias; a.alpha = alpha; a.x = w.x; a.g1 = g1; a.b1 = b1; a.eps = eps;
-      if constexpr (sizeof(T) == 2) a.h_out = w.h;
+      if constexpr (std::is_same<T, bf16>::value) a.h_out = w.h;
       return a;
     };
     for (int l = std::max(0, stage_lo); l < nl && l <= stage_hi; ++l) {
@@ -372,7 +372,7 @@ struct ModelT : public cfm_model {
         { EpiArgs e = E(SITE_FFN1); e.bias = Lw.b_ff1m; e.out = w.hid; e.ldo = ff;
           PROF(PC_FFN1, gemm<T>(EPI_STORE, ACT_SILU, w.h, d, (const T*)Lw.ff1m, d, rows, ff, d, e, st)); }
         RowLnArgs a = ln_args(Lw.b_ff2m, 0.5f, Lw.ln_mha_w, Lw.ln_mha_b);
-        if constexpr (sizeof(T) == 2) a.y_out = w.y;
+        if constexpr (std::is_same<T, bf16>::value) a.y_out = w.y;
         if (rowln(PC_FFN2, w.hid, ff, Lw.ff2m, a) < 0) return set_error(CFM_ERR_RUNTIME, "fused FFN w2 not eligible");
       } else {
       // macaron FFN (x 0.5)
@@ -395,7 +395,7 @@ struct ModelT : public cfm_model {
         int r = -1;
         hipEvent_t pb_;
         prof_begin(PC_ATTN, st, &pb_);
-        if constexpr (sizeof(T) == 2) {
+        if constexpr (std::is_same<T, bf16>::value) {
           if (masked && use_ring_attention && dk == 64 && tune.attn_q32)
             r = chunk_attention_masked_q32(w.q, w.kv, kv_rows, w.P + (size_t)l * d, p_rows, p_ld, Lw.pu, Lw.pv, attd,
                                            natt, H, C, hh[PH_L] + C + hh[PH_R], w.ao, st,
@@ -444,7 +444,7 @@ struct ModelT : public cfm_model {
       if (fused) {   // pointwise_conv2 -> y_conv, h = LN_ff(x + y_conv) (x not stored)
         RowLnArgs a = ln_args(Lw.b_pw2, 1.f, Lw.ln_ff_w, Lw.ln_ff_b);
         a.accmask = rmask;
-        if constexpr (sizeof(T) == 2) a.y_out = w.y;
+        if constexpr (std::is_same<T, bf16>::value) a.y_out = w.y;
         if (rowln(PC_PW2, w.cv, d, Lw.pw2, a) < 0) return set_error(CFM_ERR_RUNTIME, "fused pointwise_conv2 not eligible");
         // FFN: w1 + SiLU, then w2: x = LN_fin(x + y_conv + 0.5 y_ffn), h = next LN_ffm (or after_norm -> out)
         { EpiArgs e = E(SITE_FFN1); e.bias = Lw.b_ff1; e.out = w.hid; e.ldo = ff;
@@ -481,7 +481,7 @@ struct ModelT : public cfm_model {
                  hipStream_t st) const override {
     if (!fe.ctc_w) return set_error(CFM_ERR_ASSERT, "model has no CTC head (vocab == 0)");
     const int d = cfg.d_model, V = cfg.vocab;
-    if constexpr (sizeof(T) == 2) {
+    if constexpr (std::is_same<T, bf16>::value) {
       // ids only: the fused argmax head (ctc.hip) keeps every logit in registers
       if (!logp && ids && fused_ctc_ok()) {
         int r;
@@ -563,6 +563,7 @@ static cfm_status build_model(const cfm_config& cfg, const HostW& hw, int device
     T* p = reinterpret_cast<T*>(img.data() + off);
     for (size_t i = 0; i < src.size(); ++i) {
       if constexpr (sizeof(T) == 4) p[i] = src[i];
+      else if constexpr (std::is_same<T, f16>::value) p[i] = (f16)src[i];   // round-to-nearest-even (host)
       else {   // round-to-nearest-even f32 -> bf16 (host)
         uint32_t u;
         std::memcpy(&u, &src[i], 4);
@@ -775,6 +776,7 @@ cfm_status cfm_model_create(const cfm_config* cfg, const cfm_tensor_view* weight
   for (int i = 0; i < n; ++i) hw.m[weights[i].name] = {weights[i].data, weights[i].numel};
   if (cfg->compute_dtype == CFM_DTYPE_F32) return build_model<float>(*cfg, hw, device, out);
   if (cfg->compute_dtype == CFM_DTYPE_BF16) return build_model<bf16>(*cfg, hw, device, out);
+  if (cfg->compute_dtype == CFM_DTYPE_F16) return build_model<f16>(*cfg, hw, device, out);
   return set_error(CFM_ERR_VALUE, "unknown compute dtype");
 }
 
@@ -936,6 +938,8 @@ cfm_status cfm_op_gemm(int32_t dtype, int32_t epi, int32_t act, const void* A, i
   int r;
   if (dtype == CFM_DTYPE_F32)
     r = gemm<float>(epi, act, (const float*)A, lda, (const float*)W, ldw, M, N, K, e, (hipStream_t)stream);
+  else if (dtype == CFM_DTYPE_F16)
+    r = gemm<f16>(epi, act, (const f16*)A, lda, (const f16*)W, ldw, M, N, K, e, (hipStream_t)stream);
   else
     r = gemm<bf16>(epi, act, (const bf16*)A, lda, (const bf16*)W, ldw, M, N, K, e, (hipStream_t)stream);
   if (r) return set_error(CFM_ERR_RUNTIME, std::string("gemm: ") + hipGetErrorString((hipError_t)r));

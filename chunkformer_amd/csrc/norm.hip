@@ -34,8 +34,6 @@ CFM_DEV void ln_row(float (&v)[VPL], int d, const float* w, const float* b, floa
 }
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
-typedef bf16 bf16x2 __attribute__((ext_vector_type(2)));
-typedef bf16 bf16x4 __attribute__((ext_vector_type(4)));
 // VPL is 2 (d=128), 4 (d=256) or 8 (d=512): vector width min(VPL, 4) elements
 template <int VPL>
 CFM_DEV void load_row(const float* p, float (&v)[VPL]) {
@@ -61,29 +59,32 @@ CFM_DEV void store_row(float* p, const float (&v)[VPL]) {
     }
   }
 }
-template <int VPL>
-CFM_DEV void store_row(bf16* p, const float (&v)[VPL]) {
+template <typename H, int VPL, typename = std::enable_if_t<sizeof(H) == 2>>
+CFM_DEV void store_row(H* p, const float (&v)[VPL]) {   // bf16 / f16 rows
+  typedef H h2 __attribute__((ext_vector_type(2)));
+  typedef H h4 __attribute__((ext_vector_type(4)));
   if constexpr (VPL == 2) {
-    *reinterpret_cast<bf16x2*>(p) = (bf16x2){(bf16)v[0], (bf16)v[1]};
+    *reinterpret_cast<h2*>(p) = (h2){(H)v[0], (H)v[1]};
   } else {
 #pragma unroll
     for (int e = 0; e < VPL; e += 4) {
-      __builtin_nontemporal_store((bf16x4){(bf16)v[e], (bf16)v[e + 1], (bf16)v[e + 2], (bf16)v[e + 3]},
-                                  reinterpret_cast<bf16x4*>(p + e));
+      __builtin_nontemporal_store((h4){(H)v[e], (H)v[e + 1], (H)v[e + 2], (H)v[e + 3]}, reinterpret_cast<h4*>(p + e));
     }
   }
 }
 
-template <int VPL>
-CFM_DEV void load_row(const bf16* p, float (&v)[VPL]) {
+template <typename H, int VPL, typename = std::enable_if_t<sizeof(H) == 2>>
+CFM_DEV void load_row(const H* p, float (&v)[VPL]) {
+  typedef H h2 __attribute__((ext_vector_type(2)));
+  typedef H h4 __attribute__((ext_vector_type(4)));
   if constexpr (VPL == 2) {
-    const bf16x2 t = *reinterpret_cast<const bf16x2*>(p);
+    const h2 t = *reinterpret_cast<const h2*>(p);
     v[0] = (float)t[0]; v[1] = (float)t[1];
   } else {
 #pragma unroll
     for (int e = 0; e < VPL; e += 4) {
       // the branch outputs y are read once, here: non-temporal (A/B: LayerNorms 8.59 -> 8.14 ms/step)
-      const bf16x4 t = __builtin_nontemporal_load(reinterpret_cast<const bf16x4*>(p + e));
+      const h4 t = __builtin_nontemporal_load(reinterpret_cast<const h4*>(p + e));
       v[e] = (float)t[0]; v[e + 1] = (float)t[1]; v[e + 2] = (float)t[2]; v[e + 3] = (float)t[3];
     }
   }
@@ -94,12 +95,12 @@ CFM_DEV void load_row(const bf16* p, float (&v)[VPL]) {
 template <typename TY, int VPL>
 CFM_DEV void resid_terms(float (&v)[VPL], const ResidAdd<TY>& ra, int row, int lane) {
   float yv[VPL];
-  load_row<VPL>(ra.y + (size_t)row * (VPL * 64) + lane * VPL, yv);
+  load_row(ra.y + (size_t)row * (VPL * 64) + lane * VPL, yv);
   const float a = ra.alpha * (ra.ymask ? (float)ra.ymask[row] : 1.f);
 #pragma unroll
   for (int e = 0; e < VPL; ++e) v[e] = fmaf(a, yv[e], v[e]);
   if (ra.y2) {
-    load_row<VPL>(ra.y2 + (size_t)row * (VPL * 64) + lane * VPL, yv);
+    load_row(ra.y2 + (size_t)row * (VPL * 64) + lane * VPL, yv);
     const float a2 = ra.alpha2 * (ra.ymask2 ? (float)ra.ymask2[row] : 1.f);
 #pragma unroll
     for (int e = 0; e < VPL; ++e) v[e] = fmaf(a2, yv[e], v[e]);
@@ -109,7 +110,7 @@ template <typename TY, int VPL>
 CFM_DEV void resid_add(float (&v)[VPL], float* xp, const ResidAdd<TY>& ra, int row, int lane) {
   if (!ra.y) return;
   resid_terms<TY, VPL>(v, ra, row, lane);
-  if (!ra.defer) store_row<VPL>(xp, v);
+  if (!ra.defer) store_row(xp, v);
 }
 
 template <typename T, int VPL>
@@ -122,14 +123,14 @@ __global__ __launch_bounds__(256) void ln_kernel(float* __restrict__ x, ResidAdd
   constexpr int d = VPL * 64;
   float v[VPL];
   float* xp = x + (size_t)row * d + lane * VPL;
-  load_row<VPL>(xp, v);
+  load_row(xp, v);
   resid_add<T, VPL>(v, xp, ra, row, lane);
   ln_row<VPL>(v, d, w, b, eps, lane);
   if (rowmask && !rowmask[row]) {
 #pragma unroll
     for (int e = 0; e < VPL; ++e) v[e] = 0.f;
   }
-  store_row<VPL>(out + (size_t)row * d + lane * VPL, v);
+  store_row(out + (size_t)row * d + lane * VPL, v);
 }
 
 template <typename TY, typename TO, int VPL>
@@ -143,12 +144,12 @@ __global__ __launch_bounds__(256) void ln2_kernel(float* __restrict__ x, ResidAd
   constexpr int d = VPL * 64;
   float v[VPL];
   float* xp = x + (size_t)row * d + lane * VPL;
-  load_row<VPL>(xp, v);
+  load_row(xp, v);
   if (ra.y) resid_terms<TY, VPL>(v, ra, row, lane);
   ln_row<VPL>(v, d, w1, b1, eps, lane);
-  store_row<VPL>(xp, v);
+  store_row(xp, v);
   if (w2) ln_row<VPL>(v, d, w2, b2, eps, lane);
-  store_row<VPL>(out + (size_t)row * d + lane * VPL, v);
+  store_row(out + (size_t)row * d + lane * VPL, v);
 }
 
 template <typename T>
@@ -190,13 +191,19 @@ template int layernorm<float>(float*, const ResidAdd<float>&, int, int, const fl
                               const uint8_t*, hipStream_t);
 template int layernorm<bf16>(float*, const ResidAdd<bf16>&, int, int, const float*, const float*, float, bf16*,
                              const uint8_t*, hipStream_t);
+template int layernorm<f16>(float*, const ResidAdd<f16>&, int, int, const float*, const float*, float, f16*,
+                             const uint8_t*, hipStream_t);
 template int layernorm2<float>(float*, const ResidAdd<float>&, int, int, const float*, const float*, const float*,
                                const float*, float, float*, hipStream_t);
 template int layernorm2<bf16>(float*, const ResidAdd<bf16>&, int, int, const float*, const float*, const float*,
                               const float*, float, bf16*, hipStream_t);
+template int layernorm2<f16>(float*, const ResidAdd<f16>&, int, int, const float*, const float*, const float*,
+                              const float*, float, f16*, hipStream_t);
 template int layernorm2_f32<float>(float*, const ResidAdd<float>&, int, int, const float*, const float*, const float*,
                                    const float*, float, float*, hipStream_t);
 template int layernorm2_f32<bf16>(float*, const ResidAdd<bf16>&, int, int, const float*, const float*, const float*,
+                                  const float*, float, float*, hipStream_t);
+template int layernorm2_f32<f16>(float*, const ResidAdd<f16>&, int, int, const float*, const float*, const float*,
                                   const float*, float, float*, hipStream_t);
 
 }  // namespace cfm

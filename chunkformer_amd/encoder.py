@@ -27,7 +27,8 @@ from . import _lib
 from .config import EncoderConfig
 from .weights import check_state_dict
 
-_DTYPES = {"fp32": _lib.DTYPE_F32, "float32": _lib.DTYPE_F32, "bf16": _lib.DTYPE_BF16, "bfloat16": _lib.DTYPE_BF16}
+_DTYPES = {"fp32": _lib.DTYPE_F32, "float32": _lib.DTYPE_F32, "bf16": _lib.DTYPE_BF16, "bfloat16": _lib.DTYPE_BF16,
+           "fp16": _lib.DTYPE_F16, "float16": _lib.DTYPE_F16}
 
 
 def calc_length(T: int) -> int:
@@ -48,7 +49,7 @@ class ChunkFormerEncoder:
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         if dtype not in _DTYPES:
             raise ValueError(f"dtype must be one of {list(_DTYPES)}")
-        self.dtype = "bf16" if _DTYPES[dtype] == _lib.DTYPE_BF16 else "fp32"
+        self.dtype = {_lib.DTYPE_F32: "fp32", _lib.DTYPE_BF16: "bf16", _lib.DTYPE_F16: "fp16"}[_DTYPES[dtype]]
         self.num_blocks = cfg.num_blocks
         self.attention_heads = cfg.n_heads
         self._output_size = cfg.d_model

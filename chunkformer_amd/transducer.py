@@ -106,6 +106,80 @@ def synthetic_transducer_state_dict(c: RNNTConfig, seed: int = 0, blank_bias: fl
     return sd
 
 
+def with_emission_memory(sd: Dict[str, torch.Tensor], c: RNNTConfig, frame_dirs: torch.Tensor,
+                         frame_bias: torch.Tensor, tokens: List[int], forget: float = 0.3, write: float = 0.5,
+                         suppress: float = 40.0, token_gain: float = 4.0, blank_logit: float = 2.0,
+                         rest_scale: float = 0.1) -> "OrderedDict[str, torch.Tensor]":
+    """Reshape seeded transducer weights so greedy search behaves like a trained transducer: a frame
+    emits the few tokens it carries, one per step, then blank.  Test-fixture recipe
+    (tests/golden/gen_golden.py gen_rnnt_memory); every tensor keeps its reference shape.
+
+    * token k (tokens[k], k < K) has joint unit 1 + k: enc_ffn row = frame_dirs[k], bias
+      frame_bias[k], so its logit token_gain * tanh(frame_dirs[k] . x + frame_bias[k] - memory_k)
+      depends on the frame;
+    * the predictor keeps a decaying memory of each emitted token: LSTM layer 0 unit k writes
+      `write` when its input is tokens[k] (one-hot embedding column k) and every unit keeps `forget`
+      of its cell per predictor step; layer 1 unit k and projection row k pass it through, and
+      pred_ffn row 1 + k subtracts suppress x memory_k — a token just emitted is off for the next
+      few steps, so the frame moves on to its next token or to blank;
+    * blank's logit is the constant `blank_logit`; the seeded rows of the remaining joint units
+      are scaled by `rest_scale` (small frame- and state-dependent perturbations) and every other
+      token has bias -8."""
+    sd = OrderedDict((k, v.clone()) for k, v in sd.items())
+    K, H = len(tokens), c.hidden
+    assert K + 1 <= min(c.join_dim, H, c.embed_size, c.pred_out)
+    big = 10.0
+    emb = sd["predictor.embed.weight"]
+    emb[:, :K] = 0.0
+    for k, t in enumerate(tokens):
+        emb[t, k] = 1.0
+    for layer in range(c.num_layers):
+        wih, whh = sd[f"predictor.rnn.weight_ih_l{layer}"], sd[f"predictor.rnn.weight_hh_l{layer}"]
+        bih, bhh = sd[f"predictor.rnn.bias_ih_l{layer}"], sd[f"predictor.rnn.bias_hh_l{layer}"]
+        for k in range(K):
+            gi, gf, gg, go = k, H + k, 2 * H + k, 3 * H + k     # gate rows i, f, g, o of unit k
+            for r in (gi, gf, gg, go):
+                wih[r].zero_()
+                whh[r].zero_()
+                bhh[r] = 0.0
+            bih[go] = big
+            if layer == 0:        # i: open on tokens[k] only; f: keep `forget`; g: write `write`
+                wih[gi, k] = 2 * big
+                bih[gi] = -big
+                bih[gf] = math.log(forget / (1 - forget))
+                bih[gg] = math.atanh(write)
+            else:                 # pass-through of the layer below's unit k
+                bih[gi] = big
+                bih[gf] = -big
+                wih[gg, k] = 1.0
+                bih[gg] = 0.0
+    proj_w, proj_b = sd["predictor.projection.weight"], sd["predictor.projection.bias"]
+    proj_w[:K].zero_()
+    proj_b[:K] = 0.0
+    for k in range(K):
+        proj_w[k, k] = 1.0
+    ew, eb = sd["joint.enc_ffn.weight"], sd["joint.enc_ffn.bias"]
+    pw, pb = sd["joint.pred_ffn.weight"], sd["joint.pred_ffn.bias"]
+    ow, ob = sd["joint.ffn_out.weight"], sd["joint.ffn_out.bias"]
+    ow *= rest_scale
+    ob.fill_(-8.0)
+    ob[c.blank] = blank_logit
+    for u in range(K + 1):
+        ew[u].zero_()
+        eb[u] = 0.0
+        pw[u].zero_()
+        pb[u] = 0.0
+        ow[:, u] = 0.0
+    for k, t in enumerate(tokens):
+        u = 1 + k
+        ew[u] = frame_dirs[k].to(ew.dtype)
+        eb[u] = float(frame_bias[k])
+        pw[u, k] = -suppress
+        ow[t, u] = token_gain
+        ob[t] = 0.0
+    return sd
+
+
 class RNNTGreedy:
     """The transducer greedy search on libcfm (cfm_rnnt_*): predictor LSTM + joint + argmax loop in
     one persistent kernel — one workgroup per utterance for batches, `grid_blocks` workgroups per

@@ -34,7 +34,8 @@ extern "C" {
 #endif
 
 typedef enum { CFM_OK = 0, CFM_ERR_VALUE = 1, CFM_ERR_ASSERT = 2, CFM_ERR_RUNTIME = 3 } cfm_status;
-typedef enum { CFM_DTYPE_F32 = 0, CFM_DTYPE_BF16 = 1 } cfm_dtype;
+/* F16: the reference decoder's --autocast_dtype fp16 (chunkformer_model.py:709-743) */
+typedef enum { CFM_DTYPE_F32 = 0, CFM_DTYPE_BF16 = 1, CFM_DTYPE_F16 = 2 } cfm_dtype;
 
 /* encoder_conf subset (encoder.py:36-70) + CTC output_dim (init_model.py:73) */
 typedef struct {
@@ -47,7 +48,7 @@ typedef struct {
   int32_t vocab;          /* CTC output_dim, 0 = no CTC head */
   float norm_eps;         /* 1e-5 */
   int32_t has_cmvn;       /* global_cmvn present */
-  int32_t compute_dtype;  /* cfm_dtype: F32 = exact-f32 MFMA parity mode, BF16 = bf16 MFMA, f32 accumulate */
+  int32_t compute_dtype;  /* cfm_dtype: F32 = exact-f32 MFMA parity mode, BF16 / F16 = 16-bit MFMA, f32 accumulate */
 } cfm_config;
 
 /* one state_dict tensor, by reference key name, host f32 contiguous */

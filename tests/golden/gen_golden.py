@@ -381,18 +381,53 @@ def gen_endless_tbd(path, cfg=SMALL, seed=1):
                         ids=ids.numpy().astype(np.int32), att=ac.numpy(), cnn=cc.numpy())
 
 
+PEAK_SECTORS, PEAK_BLANK, PEAK_SCALE, PEAK_REST = 16, 0.8, 2.0, 0.1
+
+
+def peaked_ctc_head(out, sd, sectors=PEAK_SECTORS, blank=PEAK_BLANK, scale=PEAK_SCALE, rest=PEAK_REST):
+    """A peaked ctc_lo for a random-weight encoder, standing in for a trained head.
+
+    Scaling the seeded head does not make it peaked in the sense that matters: its argmax margins
+    and the logit error of a bf16 encoder grow together (the seeded encoder's frames share one
+    dominant direction, |x - mean| / |x| ~ 0.3, and the top-2 rows of a random V=1024 head nearly
+    tie).  A trained head reads the directions the frames vary along, so this one does: token rows
+    are `sectors` unit directions in the whitened plane of the reference outputs' two leading
+    principal components (centred on their mean, which the bias removes), the blank row wins
+    inside radius `blank`, and every other row is the seeded row x `rest` with bias -8.  All the
+    logits are scaled by `scale`.  Returns (rows, w_rows, bias) for with_fixture_ctc_head."""
+    x = out.reshape(-1, out.shape[-1]).double()
+    mu = x.mean(0)
+    _, s, vh = torch.linalg.svd(x - mu, full_matrices=False)
+    sig = s / x.shape[0] ** 0.5
+    th = torch.arange(sectors, dtype=torch.float64) * (2 * np.pi / sectors)
+    d = torch.cos(th)[:, None] * vh[0] / sig[0] + torch.sin(th)[:, None] * vh[1] / sig[1]
+    V = sd["ctc.ctc_lo.weight"].shape[0]
+    rows = torch.cat([torch.tensor([0]), 1 + torch.arange(sectors) * ((V - 1) // sectors)])
+    w_rows = torch.cat([torch.zeros(1, x.shape[1], dtype=torch.float64), scale * d]).float()
+    bias = torch.full((V,), -8.0)
+    bias[rows[1:]] = (-(scale * d) @ mu).float()
+    bias[0] = scale * blank
+    return rows.numpy().astype(np.int32), w_rows.numpy(), bias.numpy()
+
+
 def gen_small256(path, seed=2):
     """The reference's shipped small recipes (examples/asr/ctc/conf/chunkformer-ctc-small-libri-100h.yaml:5-8,
     likewise the rnnt-small and libri-960h recipes): d=256, 4 heads (head_dim 64), ff 2048, 12 blocks,
     bpe1024 vocabulary.  (a) masked batch at the decoding default C=64 L=R=128 with CTC ids and top-2
-    margins; (b) the padded chunked path (encode()) on the same utterances; (c) a masked batch with
-    C=128 L=R=128 (one of the recipe's dynamic_chunk_sizes, > 64 queries per chunk)."""
+    margins under a peaked head (peaked_ctc_head; reference median top-2 margin >= 0.5); (b) the
+    padded chunked path (encode()) on the same utterances; (c) a masked batch with C=128 L=R=128
+    (one of the recipe's dynamic_chunk_sizes, > 64 queries per chunk)."""
     cfg = SMALL256
     enc, ctc, sd = build_reference(cfg, seed)
     lens = [3000, 1234, 600]
     xs = feats(lens, 8)
     with torch.no_grad():
         r = enc.forward_parallel_chunk(xs, torch.tensor(lens), 64, 128, 128)
+        rows, w_rows, bias = peaked_ctc_head(r[0], sd)
+        w = sd["ctc.ctc_lo.weight"] * PEAK_REST
+        w[torch.from_numpy(rows.astype(np.int64))] = torch.from_numpy(w_rows)
+        ctc.ctc_lo.weight.data.copy_(w)
+        ctc.ctc_lo.bias.data.copy_(torch.from_numpy(bias))
         logp = ctc.log_softmax(r[0])
         xp = torch.zeros(len(lens), max(lens), 80)
         for i, t in enumerate(xs):
@@ -400,7 +435,12 @@ def gen_small256(path, seed=2):
         y, masks = enc.forward_encoder(xp, torch.tensor(lens), 64, 128, 128)
         r2 = enc.forward_parallel_chunk(xs, torch.tensor(lens), 128, 128, 128)
     top2 = torch.topk(logp, 2, dim=-1).values
+    mg = (top2[..., 0] - top2[..., 1]).flatten()
+    ids = logp.argmax(-1).flatten()
+    print(f"small256 peaked head: median top-2 margin {float(mg.median()):.3f}, min {float(mg.min()):.2e}, "
+          f"blank {float((ids == 0).float().mean()):.2f}, ids used {int(ids.unique().numel())}")
     np.savez_compressed(path, sd_digest=sd_digest(sd), seed=np.array(seed), lens=np.array(lens, np.int32),
+                        ctc_rows=rows, ctc_w_rows=w_rows, ctc_bias=bias, ctc_rest_scale=np.array(PEAK_REST),
                         feat_seed=np.array(8), out=r[0].numpy(), outlens=r[1].numpy(),
                         nchunks=np.array(r[2], np.int32), ids=logp.argmax(-1).numpy().astype(np.int32),
                         top2=top2.numpy(), pc_out=y.numpy(), pc_mask=masks.numpy(),
@@ -522,9 +562,109 @@ def gen_rnnt_sparse(path, seed=3, n_steps=64, blank_bias=SPARSE_BLANK_BIAS, enc_
                         margin_endless=np.array(m_e))
 
 
+def gen_autocast(path, seed=0):
+    """The reference decoder's --autocast_dtype fp16 / bf16 (chunkformer_model.py:709-743: the whole
+    decode under torch.autocast): chunkformer-large masked batch at C=64 L=R=128 over four utterances,
+    run in f32 and under CPU autocast float16 and bfloat16, with the CTC ids of each run.  Outputs are
+    stored as float16 (after_norm outputs of magnitude < 64: a relative rounding of 2^-11, below
+    the 1.4e-3 the fp16 run differs from f32 by)."""
+    cfg = LARGE
+    enc, ctc, sd = build_reference(cfg, seed)
+    lens = [3000, 2500, 1234, 600]
+    xs = feats(lens, 6)
+    res = {}
+    with torch.no_grad():
+        r = enc.forward_parallel_chunk(xs, torch.tensor(lens), 64, 128, 128)
+        ref = r[0].float()
+        logp = ctc.log_softmax(ref)
+        res["out_f32"] = ref.numpy().astype(np.float16)
+        res["ids"] = logp.argmax(-1).numpy().astype(np.int32)
+        top2 = torch.topk(logp, 2, dim=-1).values
+        res["margin"] = (top2[..., 0] - top2[..., 1]).numpy()
+        for name, dt in (("f16", torch.float16), ("bf16", torch.bfloat16)):
+            with torch.autocast("cpu", dtype=dt):
+                ra = enc.forward_parallel_chunk(xs, torch.tensor(lens), 64, 128, 128)
+                la = ctc.log_softmax(ra[0])
+            o = ra[0].float()
+            rel = float((o - ref).norm() / ref.norm())
+            ids = la.float().argmax(-1).numpy().astype(np.int32)
+            print(f"autocast {name}: rel-L2 vs f32 {rel:.3e}, CTC ids equal {float((ids == res['ids']).mean()):.4f}")
+            res[f"out_{name}"] = o.numpy().astype(np.float16)
+            res[f"ids_{name}"] = ids
+            res[f"rel_{name}"] = np.array(rel)
+    np.savez_compressed(path, sd_digest=sd_digest(sd), seed=np.array(seed), lens=np.array(lens, np.int32),
+                        feat_seed=np.array(6), nchunks=np.array(r[2], np.int32), outlens=r[1].numpy(), **res)
+
+
+MEMORY_TOKENS, MEMORY_FORGET, MEMORY_SUPPRESS, MEMORY_THRESH = 64, 0.5, 100.0, 1.5
+
+
+def gen_rnnt_memory(path, seed=3, n_steps=64, dir_seed=11):
+    """The regime of a trained transducer: most non-blank frames emit 1-3 tokens and then stop on
+    blank, below the n_steps cap.  Seeded weights reshaped by
+    chunkformer_amd.transducer.with_emission_memory: MEMORY_TOKENS tokens, token k carried by the
+    frames whose standardised projection on a seeded random direction w_k exceeds MEMORY_THRESH,
+    and a decaying per-token memory in the predictor that turns a just-emitted token off.  The
+    directions are standardised on the first ENDLESS_RNNT_FRAMES rows of large_endless.npz.
+    optimized_search (transducer/search/greedy_search.py:6-74) over (a) those rows, B = 1, and (b)
+    large_4h.npz's two utterances as one padded batch (+ batch_greedy_search's hypotheses)."""
+    from chunkformer.transducer.joint import TransducerJoint
+    from chunkformer.transducer.predictor import RNNPredictor
+    from chunkformer.transducer.search.greedy_search import batch_greedy_search, optimized_search
+
+    from chunkformer_amd.transducer import RNNTConfig, synthetic_transducer_state_dict, with_emission_memory
+    c = RNNTConfig()
+    ge = np.load(os.path.join(HERE, "large_endless.npz"))
+    enc_e = torch.from_numpy(ge["out"][:ENDLESS_RNNT_FRAMES]).unsqueeze(0)
+    x = enc_e[0].double()
+    mu = x.mean(0)
+    gen = torch.Generator().manual_seed(dir_seed)
+    w = torch.randn(MEMORY_TOKENS, c.enc_dim, generator=gen, dtype=torch.float64)
+    w /= w.norm(dim=1, keepdim=True)
+    d = w / ((x - mu) @ w.T).std(0)[:, None]
+    frame_dirs = d.float()
+    frame_bias = (-(d @ mu) - MEMORY_THRESH).float()
+    tokens = [1 + k * ((c.vocab - 1) // MEMORY_TOKENS) for k in range(MEMORY_TOKENS)]
+    sd = with_emission_memory(synthetic_transducer_state_dict(c, seed), c, frame_dirs, frame_bias, tokens,
+                              forget=MEMORY_FORGET, suppress=MEMORY_SUPPRESS)
+    pred = RNNPredictor(c.vocab, c.embed_size, c.pred_out, 0.1, c.hidden, c.num_layers, True, "lstm", 0.1).eval()
+    joint = TransducerJoint(c.vocab, c.enc_dim, c.pred_out, c.join_dim, True, False, "add", "tanh").eval()
+    pred.load_state_dict({k[len("predictor."):]: v for k, v in sd.items() if k.startswith("predictor.")}, strict=True)
+    joint.load_state_dict({k[len("joint."):]: v for k, v in sd.items() if k.startswith("joint.")}, strict=True)
+    model = types.SimpleNamespace(predictor=pred, joint=joint, blank=0)
+    g4 = np.load(os.path.join(HERE, "large_4h.npz"))
+    starts = np.cumsum([0] + g4["nchunks"].tolist())
+    utts = [torch.from_numpy(g4["out"][starts[u]: starts[u + 1]].reshape(-1, c.enc_dim)[: int(n)])
+            for u, n in enumerate(g4["outlens"])]
+    lens = torch.tensor([u.shape[0] for u in utts])
+    enc_b = torch.nn.utils.rnn.pad_sequence(utts, batch_first=True)
+    with torch.no_grad():
+        out_e = optimized_search(model, enc_e, torch.tensor([enc_e.shape[1]]), n_steps)
+        out_b = optimized_search(model, enc_b, lens, n_steps)
+        hyps_b = batch_greedy_search(model, enc_b, lens, n_steps)
+    from oracle import rnnt_ref
+    _, m_e = rnnt_ref.optimized_search(sd, c.num_layers, c.hidden, enc_e, [enc_e.shape[1]], n_steps)
+    _, m_b = rnnt_ref.optimized_search(sd, c.num_layers, c.hidden, enc_b, lens, n_steps)
+    for nm, o in (("endless", out_e), ("batch", out_b)):
+        cnt = (o.reshape(-1, n_steps) != 0).sum(-1)
+        nb = cnt[cnt > 0]
+        print(f"rnnt memory {nm}: frames {cnt.numel()}, blank-first {float((cnt == 0).float().mean()):.2f}, "
+              f"non-blank frames {nb.numel()}: 1-3 tokens {float(((nb >= 1) & (nb <= 3)).float().mean()):.2f}, "
+              f"at the cap {float((nb == n_steps).float().mean()):.2f}")
+    print(f"rnnt memory min top-2 margins: endless {m_e:.2e}, batch {m_b:.2e}")
+    flat = [t for h in hyps_b for t in h]
+    np.savez_compressed(path, seed=np.array(seed), n_steps=np.array(n_steps), vocab=np.array(c.vocab),
+                        frame_dirs=frame_dirs.numpy(), frame_bias=frame_bias.numpy(),
+                        tokens=np.array(tokens, np.int32), forget=np.array(MEMORY_FORGET),
+                        suppress=np.array(MEMORY_SUPPRESS), endless_out=out_e.numpy().astype(np.int32),
+                        batch_lens=lens.numpy().astype(np.int32), batch_out=out_b.numpy().astype(np.int32),
+                        batch_hyp_lens=np.array([len(h) for h in hyps_b]), batch_hyps=np.array(flat, np.int32),
+                        margin_endless=np.array(m_e), margin_batch=np.array(m_b))
+
+
 if __name__ == "__main__":
     which = sys.argv[1:] or ["masks", "small", "large", "large_4h", "large_endless", "large_full", "text", "stream",
-                             "endless_tbd", "rnnt", "rows_neq", "small256", "rnnt_sparse"]
+                             "endless_tbd", "rnnt", "rows_neq", "small256", "rnnt_sparse", "rnnt_memory", "autocast"]
     if "masks" in which:
         gen_masks(os.path.join(HERE, "masks.npz"))
     if "small" in which:
@@ -551,4 +691,8 @@ if __name__ == "__main__":
         gen_small256(os.path.join(HERE, "small256.npz"))
     if "rnnt_sparse" in which:
         gen_rnnt_sparse(os.path.join(HERE, "rnnt_sparse.npz"))
+    if "rnnt_memory" in which:
+        gen_rnnt_memory(os.path.join(HERE, "rnnt_memory.npz"))
+    if "autocast" in which:
+        gen_autocast(os.path.join(HERE, "autocast.npz"))
     print("ok", which)

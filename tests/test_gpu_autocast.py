@@ -1,0 +1,84 @@
+"""GPU: the 16-bit compute modes against the reference decoder's own --autocast_dtype runs
+(chunkformer_model.py:709-743; tests/golden/autocast.npz, gen_golden.py gen_autocast: chunkformer-large,
+masked batch C=64 L=R=128 over four utterances, in f32 and under CPU autocast float16 / bfloat16).
+
+Bars (written against the fixture's own numbers):
+  * fp16: the reference's autocast fp16 output differs from its f32 output by rel-L2 1.4e-3 and agrees on
+    99.6% of the CTC ids.  Ours must stay within 2x that distance of the f32 output (3e-3), within 3e-3 of
+    the autocast fp16 output, and agree with the f32 ids on >= 99% of ALL frames.
+  * bf16: the reference's autocast bf16 run is at rel-L2 1.15e-2 from f32 and agrees on 95.8% of the ids
+    (this random-weight V=1024 head is flat).  Ours must be no farther from f32 than that run is, and agree
+    with the f32 ids at least as often as it does.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _rel(a, b):
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    return float(np.linalg.norm(a - b) / np.linalg.norm(b))
+
+
+@pytest.fixture(scope="module")
+def fixture(golden_dir):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from chunkformer_amd.config import LARGE
+    from chunkformer_amd.weights import synthetic_features, synthetic_state_dict
+    g = np.load(os.path.join(golden_dir, "autocast.npz"))
+    sd = synthetic_state_dict(LARGE, int(g["seed"]))
+    np.testing.assert_allclose(np.array([float(v.double().sum()) for v in sd.values()]), g["sd_digest"], rtol=0, atol=0)
+    lens = g["lens"].tolist()
+    return g, sd, synthetic_features(lens, int(g["feat_seed"])), torch.tensor(lens, dtype=torch.int32)
+
+
+def _run(fixture, dtype):
+    from chunkformer_amd.config import LARGE
+    from chunkformer_amd.encoder import ChunkFormerEncoder
+    g, sd, xs, tl = fixture
+    enc = ChunkFormerEncoder(LARGE, sd, dtype=dtype)
+    out, olens, nch, _, _, _ = enc.forward_parallel_chunk(xs, tl, 64, 128, 128)
+    assert nch == g["nchunks"].tolist() and olens.tolist() == g["outlens"].tolist()
+    _, ids = enc.ctc_log_softmax(out, want_logp=False)
+    return out.float().cpu().numpy(), ids.cpu().numpy()
+
+
+def test_fp16_matches_reference_autocast_fp16(fixture):
+    g = fixture[0]
+    out, ids = _run(fixture, "fp16")
+    ref32, ref16 = g["out_f32"].astype(np.float32), g["out_f16"].astype(np.float32)
+    r32, r16 = _rel(out, ref32), _rel(out, ref16)
+    agree = float((ids == g["ids"]).mean())
+    print(f"fp16: rel-L2 vs f32 {r32:.2e} (reference autocast fp16: {float(g['rel_f16']):.2e}), "
+          f"vs autocast fp16 {r16:.2e}; CTC ids equal to f32 {agree:.4f} "
+          f"(reference autocast fp16: {float((g['ids_f16'] == g['ids']).mean()):.4f}), "
+          f"to autocast fp16 {float((ids == g['ids_f16']).mean()):.4f}")
+    assert r32 <= max(3e-3, 2 * float(g["rel_f16"]))
+    assert r16 <= 3e-3
+    assert agree >= 0.99
+
+
+def test_bf16_within_reference_autocast_bf16(fixture):
+    g = fixture[0]
+    out, ids = _run(fixture, "bf16")
+    r32 = _rel(out, g["out_f32"].astype(np.float32))
+    agree = float((ids == g["ids"]).mean())
+    ref_agree = float((g["ids_bf16"] == g["ids"]).mean())
+    print(f"bf16: rel-L2 vs f32 {r32:.2e} (reference autocast bf16: {float(g['rel_bf16']):.2e}); CTC ids equal "
+          f"to f32 {agree:.4f} (reference autocast bf16: {ref_agree:.4f})")
+    assert r32 <= float(g["rel_bf16"])
+    assert agree >= ref_agree
+
+
+def test_fp32_matches_reference_f32(fixture):
+    g = fixture[0]
+    out, ids = _run(fixture, "fp32")
+    # the fixture's f32 output is stored as float16: compare at that rounding (2^-11 relative)
+    assert _rel(out, g["out_f32"].astype(np.float32)) <= 5e-4
+    m = g["margin"] > 1e-3
+    np.testing.assert_array_equal(ids[m], g["ids"][m])

@@ -83,6 +83,33 @@ def test_sparse_emission_matches_reference(golden_dir, key, n_steps, grid):
     np.testing.assert_array_equal(out.cpu().numpy(), g[key])
 
 
+@pytest.mark.parametrize("grid", [64, 16, 0])
+def test_memory_joint_matches_reference(golden_dir, grid):
+    """rnnt_memory.npz: a trained-like joint (with_emission_memory) where 95% of the endless rows'
+    non-blank frames emit 1-3 tokens and then stop on blank below the n_steps 64 cap (the
+    predictor re-evaluated after every emission, the frame loop left on blank); B = 1 on the
+    multi-CU search / one workgroup, and the padded batch of two utterances with its hypotheses."""
+    from chunkformer_amd.transducer import RNNTGreedy
+    from conftest import rnnt_memory_state_dict
+    g = np.load(os.path.join(golden_dir, "rnnt_memory.npz"))
+    c, sd = rnnt_memory_state_dict(g)
+    dec = RNNTGreedy(c, sd, "cuda")
+    n = int(g["n_steps"])
+    dec.set_option("grid_blocks", grid)
+    assert dec.grid_blocks(1) == grid
+    ge = np.load(os.path.join(golden_dir, "large_endless.npz"))
+    T = g["endless_out"].shape[1] // n
+    out = dec.optimized_search(torch.from_numpy(ge["out"][:T]).unsqueeze(0).cuda(), torch.tensor([T]), n)
+    np.testing.assert_array_equal(out.cpu().numpy(), g["endless_out"])
+    utts = _batch_enc(golden_dir, c.enc_dim)
+    lens = torch.tensor([u.shape[0] for u in utts])
+    enc = torch.nn.utils.rnn.pad_sequence(utts, batch_first=True).cuda()
+    np.testing.assert_array_equal(dec.optimized_search(enc, lens, n).cpu().numpy(), g["batch_out"])
+    hyps = dec.batch_greedy_search(enc, lens, n)
+    assert [len(h) for h in hyps] == g["batch_hyp_lens"].tolist()
+    assert [t for h in hyps for t in h] == g["batch_hyps"].tolist()
+
+
 @pytest.mark.parametrize("grid", [64, 0])
 @pytest.mark.parametrize("n_steps", [1, 3])
 def test_small_cap_and_ragged_vs_oracle(rnnt, n_steps, grid):

@@ -437,9 +437,10 @@ def test_small256_recipe_shape(dtype):
     from chunkformer_amd.config import SMALL256
     from chunkformer_amd.encoder import ChunkFormerEncoder
     from chunkformer_amd.weights import synthetic_features, synthetic_state_dict
-    from conftest import GOLDEN
+    from conftest import GOLDEN, with_fixture_ctc_head
     g = np.load(os.path.join(GOLDEN, "small256.npz"))
-    enc = ChunkFormerEncoder(SMALL256, synthetic_state_dict(SMALL256, int(g["seed"])), dtype=dtype)
+    sd = with_fixture_ctc_head(synthetic_state_dict(SMALL256, int(g["seed"])), g)
+    enc = ChunkFormerEncoder(SMALL256, sd, dtype=dtype)
     lens = g["lens"].tolist()
     xs = synthetic_features(lens, int(g["feat_seed"]))
     tl = torch.tensor(lens, dtype=torch.int32)
@@ -456,20 +457,17 @@ def test_small256_recipe_shape(dtype):
     assert nch2 == g["c128_nchunks"].tolist() and olens2.tolist() == g["c128_outlens"].tolist()
     margin = g["top2"][..., 0] - g["top2"][..., 1]
     pairs = ((out, g["out"]), (y, g["pc_out"]), (out2, g["c128_out"]))
-    if dtype == "fp32":
-        for a, b in pairs:
+    for a, b in pairs:
+        if dtype == "fp32":
             np.testing.assert_allclose(a.float().cpu().numpy(), b, atol=1e-4, rtol=0)
-        sure = margin > 1e-3
-        np.testing.assert_array_equal(ids[sure], g["ids"][sure])
-    else:
-        for a, b in pairs:
+        else:
             assert _rel_l2(a.float().cpu().numpy(), b) <= BF16_RELL2
-        # this random-weight V=1024 head is flat: 10% of the frames have a reference top-2 margin
-        # below 1e-2 (chunkformer-large: 3%), the size of bf16's log-prob noise, so the 99% bar is
-        # taken over the frames whose margin exceeds it (overall agreement printed; measured 98.4%)
-        agree = (ids == g["ids"]).mean()
-        clear = margin >= 1e-2
-        print(f"small256 bf16: CTC argmax agreement {agree:.4f} overall, "
-              f"{(ids == g['ids'])[clear].mean():.4f} where the margin >= 1e-2")
-        assert (ids == g["ids"])[clear].mean() >= 0.99
-        np.testing.assert_array_equal(ids[margin > BF16_MARGIN], g["ids"][margin > BF16_MARGIN])
+    # the fixture's CTC head is peaked (reference median top-2 margin 0.70, min 8e-3;
+    # gen_golden.py:peaked_ctc_head): ids are compared over ALL frames, no margin filter
+    agree = float((ids == g["ids"]).mean())
+    print(f"small256 {dtype}: CTC argmax agreement {agree:.4f} over all {ids.size} frames "
+          f"(reference median top-2 margin {float(np.median(margin)):.3f})")
+    if dtype == "fp32":
+        np.testing.assert_array_equal(ids, g["ids"])
+    else:
+        assert agree >= 0.99

@@ -8,6 +8,7 @@ import torch
 from chunkformer_amd.config import LARGE, SMALL
 from chunkformer_amd.weights import synthetic_features, synthetic_state_dict
 from oracle import encoder_ref as ref
+from conftest import with_fixture_ctc_head
 
 torch.set_num_threads(min(8, os.cpu_count() or 1))
 
@@ -101,6 +102,25 @@ def test_large_matches_reference(golden_dir):
     np.testing.assert_array_equal(ids[sure], g["ids"][sure])
 
 
+def test_autocast_fixture_f32_matches_oracle(golden_dir):
+    """autocast.npz (the reference's f32 / autocast fp16 / bf16 runs, gen_golden.py gen_autocast): its f32
+    output (stored as float16) against the oracle, and the autocast runs' recorded distances to it."""
+    g = _load(golden_dir, "autocast.npz")
+    sd = synthetic_state_dict(LARGE, int(g["seed"]))
+    lens = g["lens"].tolist()
+    xs = synthetic_features(lens, int(g["feat_seed"]))
+    out, _, nch, _, _, _ = ref.forward_parallel_chunk(sd, LARGE, xs, lens, 64, 128, 128)
+    assert nch == g["nchunks"].tolist()
+    o, f32 = out.numpy().astype(np.float64), g["out_f32"].astype(np.float64)
+    assert np.linalg.norm(o - f32) / np.linalg.norm(o) < 5e-4
+    ids = ref.ctc_log_softmax(sd, out).argmax(-1).numpy()
+    m = g["margin"] > 1e-4
+    np.testing.assert_array_equal(ids[m], g["ids"][m])
+    for name in ("f16", "bf16"):
+        r = np.linalg.norm(g[f"out_{name}"].astype(np.float64) - o) / np.linalg.norm(o)
+        assert abs(r - float(g[f"rel_{name}"])) < 5e-4, name
+
+
 def test_large_4h_matches_reference(golden_dir):
     """d=512 with 4 heads (head_dim 128): masked batch and the padded chunked path."""
     from chunkformer_amd.config import LARGE_4H
@@ -131,10 +151,9 @@ def test_small256_matches_reference(golden_dir):
     out, olens, nch, _, _, _ = ref.forward_parallel_chunk(sd, SMALL256, xs, lens, 64, 128, 128)
     assert nch == g["nchunks"].tolist() and olens.tolist() == g["outlens"].tolist()
     np.testing.assert_allclose(out.numpy(), g["out"], atol=1e-4, rtol=0)
-    logp = ref.ctc_log_softmax(sd, out).numpy()
-    margin = g["top2"][..., 0] - g["top2"][..., 1]
-    sure = margin > 1e-4
-    np.testing.assert_array_equal(logp.argmax(-1)[sure], g["ids"][sure])
+    # the fixture's peaked CTC head (gen_golden.py:peaked_ctc_head): ids equal on every frame
+    logp = ref.ctc_log_softmax(with_fixture_ctc_head(sd, g), out).numpy()
+    np.testing.assert_array_equal(logp.argmax(-1), g["ids"])
     xp = torch.zeros(len(lens), max(lens), 80)
     for i, t in enumerate(xs):
         xp[i, : t.shape[0]] = t

@@ -66,6 +66,27 @@ def test_oracle_matches_reference_sparse_emission(golden_dir):
         np.testing.assert_array_equal(o.numpy(), g[key].reshape(-1, steps)[:3 * PREFIX], err_msg=key)
 
 
+def test_oracle_matches_reference_memory_joint(golden_dir):
+    """rnnt_memory.npz: a trained-like joint (with_emission_memory) where most non-blank frames emit
+    1-3 tokens and then stop on blank below the cap; the oracle on a prefix of the endless rows and
+    of the batch's first utterance, and the regime itself asserted on the whole fixture."""
+    from conftest import rnnt_memory_state_dict
+    g = np.load(os.path.join(golden_dir, "rnnt_memory.npz"))
+    c, sd = rnnt_memory_state_dict(g)
+    n = int(g["n_steps"])
+    d = g["endless_out"].reshape(-1, n)
+    cnt = (d != 0).sum(1)
+    nb = cnt[cnt > 0]
+    assert 0.2 <= (cnt == 0).mean() <= 0.8 and ((nb >= 1) & (nb <= 3)).mean() >= 0.9 and (nb == n).any()
+    ge = np.load(os.path.join(golden_dir, "large_endless.npz"))
+    o, margin = rnnt_ref.greedy_one(sd, c.num_layers, c.hidden, torch.from_numpy(ge["out"][:4 * PREFIX]), n)
+    np.testing.assert_array_equal(o.numpy(), d[:4 * PREFIX])
+    assert margin > 1e-4
+    utt0 = _batch_enc(golden_dir, c.enc_dim)[0]
+    o, _ = rnnt_ref.greedy_one(sd, c.num_layers, c.hidden, utt0[:2 * PREFIX], n)
+    np.testing.assert_array_equal(o.numpy(), g["batch_out"].reshape(len(g["batch_lens"]), -1, n)[0, :2 * PREFIX])
+
+
 def test_golden_exercises_every_branch(rnnt):
     """The fixture covers blank frames, frames with a few tokens ended by a blank, and frames that
     reach the n_steps cap; the batch hypotheses are the non-blank decisions in order."""
