@@ -245,6 +245,11 @@ CFM_DEV unsigned pack_bf16x2_a(float a, float b) {
   typedef bf16 b2 __attribute__((ext_vector_type(2)));
   return __builtin_bit_cast(unsigned, (b2){(bf16)a, (bf16)b});
 }
+template <typename E>
+CFM_DEV unsigned pack_e2(float a, float b) {
+  typedef E e2 __attribute__((ext_vector_type(2)));
+  return __builtin_bit_cast(unsigned, (e2){(E)a, (E)b});
+}
 CFM_DEV int sw128(int row, int ch) { return row * 128 + ((ch ^ ((row >> 1) & 7)) << 4); }
 #ifndef RING_KPF
 #define RING_KPF 1   // ring kernel, interior chunks: next tile's K fragments read before this tile's skew
@@ -256,11 +261,12 @@ CFM_DEV int sw128(int row, int ch) { return row * 128 + ((ch ^ ((row >> 1) & 7))
 // DG: the timing / A-B hooks of `diag` are compiled in (the production instantiation has none of their
 // uniform branches inside the tile loop, which would cut it into basic blocks the scheduler cannot
 // interleave across); NTI = W / 64 when W is whole 64-key tiles (1..5), else 0
-template <bool DG, int NTI>
+template <bool DG, int NTI, typename E = bf16>
 __global__ __launch_bounds__(512, 1) void chunk_attention_ring_kernel(
-    const bf16* __restrict__ Q, const bf16* __restrict__ KV, int kv_rows, const bf16* __restrict__ P, int p_rows,
+    const E* __restrict__ Q, const E* __restrict__ KV, int kv_rows, const E* __restrict__ P, int p_rows,
     const float* __restrict__ pos_u, const float* __restrict__ pos_v, const int32_t* __restrict__ desc, int n_chunks,
-    int H, int C, int W, bf16* __restrict__ out, int diag_arg, int nch, int p_ld) {
+    int H, int C, int W, E* __restrict__ out, int diag_arg, int nch, int p_ld) {
+  typedef E ex8 __attribute__((ext_vector_type(8)));   // bf16x8 / f16x8 fragments
   const int diag = DG ? diag_arg : 0;
   const bool reuse_band = (diag & 15) != 5;   // diag 5: recompute band subtile 0 of every tile (A/B)
   __shared__ __attribute__((aligned(16))) char smem[RING_LDS];
@@ -271,7 +277,7 @@ __global__ __launch_bounds__(512, 1) void chunk_attention_ring_kernel(
   const int fr = lane & 15, g = lane >> 4;
   // waves 0-3 work on chunk c, waves 4-7 on chunk c+1 (both windows live in the ring: W + C <= RING)
   const int half = __builtin_amdgcn_readfirstlane(w) >> 2, wq = w & 3;
-  bf16* scr = reinterpret_cast<bf16*>(vt + VT_BYTES_ + w * SCR_BYTES);
+  E* scr = reinterpret_cast<E*>(vt + VT_BYTES_ + w * SCR_BYTES);
   const unsigned scr_base = (unsigned)(size_t)(__attribute__((address_space(3))) char*)scr;
   float* uv = reinterpret_cast<float*>(vt + VT_BYTES_ + 8 * SCR_BYTES);   // [2][64]: pos_bias_u / v of head h
   const int h = blockIdx.y;
@@ -294,18 +300,18 @@ __global__ __launch_bounds__(512, 1) void chunk_attention_ring_kernel(
   // staging unit = two consecutive (even-aligned) flat rows x one 16-B chunk of K and V: the K halves
   // go to the swizzled K ring, the V halves are interleaved into 8 bf16x2 words of V^T (conflict-free:
   // the 64 lanes of a wave take 64 consecutive row pairs of one chunk)
-  typedef bf16 bf16x2_ __attribute__((ext_vector_type(2)));
+  typedef E ex2_ __attribute__((ext_vector_type(2)));
   auto stage_pair = [&](int frow, int ch, const u32x4& k0, const u32x4& v0, const u32x4& k1, const u32x4& v1) {
     const int rr = frow % RING;   // even; rr + 1 < RING
     *reinterpret_cast<u32x4*>(kr + sw128(rr, ch)) = k0;
     *reinterpret_cast<u32x4*>(kr + sw128(rr + 1, ch)) = k1;
-    const bf16x8 a = __builtin_bit_cast(bf16x8, v0), b = __builtin_bit_cast(bf16x8, v1);
+    const ex8 a = __builtin_bit_cast(ex8, v0), b = __builtin_bit_cast(ex8, v1);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) *reinterpret_cast<bf16x2_*>(vt + (ch * 8 + e) * VT_PITCH_B + rr * 2) = (bf16x2_){a[e], b[e]};
+    for (int e = 0; e < 8; ++e) *reinterpret_cast<ex2_*>(vt + (ch * 8 + e) * VT_PITCH_B + rr * 2) = (ex2_){a[e], b[e]};
   };
   auto load_pair = [&](int frow, int ch, u32x4& k0, u32x4& v0, u32x4& k1, u32x4& v1) {
-    const bf16* s0 = KV + (size_t)min(frow, kv_rows - 1) * (2 * d) + h * 128 + ch * 8;
-    const bf16* s1 = KV + (size_t)min(frow + 1, kv_rows - 1) * (2 * d) + h * 128 + ch * 8;
+    const E* s0 = KV + (size_t)min(frow, kv_rows - 1) * (2 * d) + h * 128 + ch * 8;
+    const E* s1 = KV + (size_t)min(frow + 1, kv_rows - 1) * (2 * d) + h * 128 + ch * 8;
     k0 = *reinterpret_cast<const u32x4*>(s0);
     v0 = *reinterpret_cast<const u32x4*>(s0 + 64);
     k1 = *reinterpret_cast<const u32x4*>(s1);
@@ -329,12 +335,12 @@ __global__ __launch_bounds__(512, 1) void chunk_attention_ring_kernel(
   // only the key range [lo, hi) varies.  Q fragments and the key range of the wave's NEXT chunk
   // are loaded one pair ahead, so no iteration waits on a dependent global load.
   const int p_base = C - 1, q_valid = C;
-  auto load_q = [&](int c, bf16x8 (&qr)[2]) {
-    const bf16* qp = Q + ((size_t)c * C + i0 + fr) * d + h * 64;
-    qr[0] = *reinterpret_cast<const bf16x8*>(qp + 8 * g);
-    qr[1] = *reinterpret_cast<const bf16x8*>(qp + 32 + 8 * g);
+  auto load_q = [&](int c, ex8 (&qr)[2]) {
+    const E* qp = Q + ((size_t)c * C + i0 + fr) * d + h * 64;
+    qr[0] = *reinterpret_cast<const ex8*>(qp + 8 * g);
+    qr[1] = *reinterpret_cast<const ex8*>(qp + 32 + 8 * g);
   };
-  bf16x8 qraw[2], qnext[2];
+  ex8 qraw[2], qnext[2];
   int klo_n = 0, khi_n = 0;
   {
     const int c = c0 + half;
@@ -385,7 +391,7 @@ __global__ __launch_bounds__(512, 1) void chunk_attention_ring_kernel(
       const int frag_lane[2] = {fr * 128 + ((g ^ key8) << 4), fr * 128 + (((4 + g) ^ key8) << 4)};
       const int vt_lane = fr * VT_PITCH_B + 8 * g;
       // ---- query fragments (B operands): lane (fr, g) = query i0+fr, dims 32s + 8g .. +7
-      bf16x8 qu[2], qv[2];
+      ex8 qu[2], qv[2];
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         const f32x4 u0 = *reinterpret_cast<const f32x4*>(uv + s * 32 + 8 * g);
@@ -394,11 +400,11 @@ __global__ __launch_bounds__(512, 1) void chunk_attention_ring_kernel(
         const f32x4 v1_ = *reinterpret_cast<const f32x4*>(uv + 64 + s * 32 + 8 * g + 4);
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          // the 1/sqrt(dk) = 2^-3 scale is folded into both operands: exact in bf16 and in the f32
+          // the 1/sqrt(dk) = 2^-3 scale is folded into both operands: exact in E and in the f32
           // accumulation, so (qu.k + bd) * 0.125 is reproduced bit for bit
           const float qf = (float)qraw[s][e];
-          qu[s][e] = (bf16)((qf + (e < 4 ? u0[e] : u1[e - 4])) * 0.125f);
-          qv[s][e] = (bf16)((qf + (e < 4 ? v0_[e] : v1_[e - 4])) * 0.125f);
+          qu[s][e] = (E)((qf + (e < 4 ? u0[e] : u1[e - 4])) * 0.125f);
+          qv[s][e] = (E)((qf + (e < 4 ? v0_[e] : v1_[e - 4])) * 0.125f);
         }
       }
       // interior chunks of a window that is whole 64-key tiles (key_lo = 0, key_hi = W = 64 NTI): no
@@ -414,13 +420,13 @@ __global__ __launch_bounds__(512, 1) void chunk_attention_ring_kernel(
         float mx = -INFINITY;
         // RING_KPF (interior chunks): tile t + 1's K fragments are read right after tile t's band
         // MFMAs, so their LDS latency overlaps tile t's skew round trip
-        bf16x8 kf_next[4][2];
-        auto load_kf = [&](int t, bf16x8 (&kf)[4][2]) {
+        ex8 kf_next[4][2];
+        auto load_kf = [&](int t, ex8 (&kf)[4][2]) {
 #pragma unroll
           for (int st = 0; st < 4; ++st) {
             const char* kb_ = kr + ring16(jb + 64 * t + 16 * st) * 128;
 #pragma unroll
-            for (int s = 0; s < 2; ++s) kf[st][s] = *reinterpret_cast<const bf16x8*>(kb_ + frag_lane[s]);
+            for (int s = 0; s < 2; ++s) kf[st][s] = *reinterpret_cast<const ex8*>(kb_ + frag_lane[s]);
           }
         };
         constexpr bool KPF = RING_KPF && !MASK;
@@ -433,9 +439,9 @@ __global__ __launch_bounds__(512, 1) void chunk_attention_ring_kernel(
             for (int st = 0; st < 4; ++st) S[t][st] = (f32x4){-INFINITY, -INFINITY, -INFINITY, -INFINITY};
             continue;
           }
-          // the band first: its skewed values (bf16, through the per-wave scratch) become the C
+          // the band first: its skewed values (E, through the per-wave scratch) become the C
           // operand of the score MFMAs, so S = K.(q+u) + band costs no VALU add
-          bf16x8 kf[4][2], pf[5][2];
+          ex8 kf[4][2], pf[5][2];
           const int kb0 = p_base - i0 - 15 + j0;
           // band subtile 0 of tile t is subtile 4 of tile t - 1 (P rows kb0 .. kb0 + 15, 64 rows on):
           // carried in registers (tiles past key_hi are skipped only at the end, so tile t - 1 ran)
@@ -445,7 +451,7 @@ __global__ __launch_bounds__(512, 1) void chunk_attention_ring_kernel(
             if (pt == 0 && carry) continue;
             const char* pb_ = pl + (kb0 + 16 * pt) * 128;
 #pragma unroll
-            for (int s = 0; s < 2; ++s) pf[pt][s] = *reinterpret_cast<const bf16x8*>(pb_ + frag_lane[s]);
+            for (int s = 0; s < 2; ++s) pf[pt][s] = *reinterpret_cast<const ex8*>(pb_ + frag_lane[s]);
           }
           if constexpr (KPF) {
 #pragma unroll
@@ -454,7 +460,7 @@ __global__ __launch_bounds__(512, 1) void chunk_attention_ring_kernel(
             load_kf(t, kf);
           }
           // band^T[P row kb0 + 16pt + 4g + rr][query fr], pt = 0..4 (80 rows for 64 keys + 15 skew); the
-          // two 32-key halves use subtiles 0-2 and 2-4 -> scratch[query][band pos] (16 x 48 bf16 per wave)
+          // two 32-key halves use subtiles 0-2 and 2-4 -> scratch[query][band pos] (16 x 48 E per wave)
           f32x4 band[5];
 #pragma unroll
           for (int pt = 0; pt < 5; ++pt) {
@@ -464,7 +470,7 @@ __global__ __launch_bounds__(512, 1) void chunk_attention_ring_kernel(
             }
             f32x4 a = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-            for (int s = 0; s < 2; ++s) a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pf[pt][s], qv[s], a, 0, 0, 0);
+            for (int s = 0; s < 2; ++s) a = mma16(pf[pt][s], qv[s], a);
             band[pt] = a;
           }
           band_next = band[4];
@@ -480,15 +486,15 @@ __global__ __launch_bounds__(512, 1) void chunk_attention_ring_kernel(
               // pitch 48, so query fr's band for key jj starts 16 - fr elements later: the reads
               // are aligned 8-B vectors (4 keys), the writes 2-B aligned, as four ds_write_b16
               const unsigned waddr = scr_base + 2u * (unsigned)(fr * SCR_PITCH + 1 + 16 * pt + 4 * g);
-              const unsigned lo = pack_bf16x2_a(a[0], a[1]), hi = pack_bf16x2_a(a[2], a[3]);
+              const unsigned lo = pack_e2<E>(a[0], a[1]), hi = pack_e2<E>(a[2], a[3]);
               if (diag & 16)   // A/B: one unaligned ds_write_b64 (replayed by the LDS)
                 asm volatile("ds_write_b64 %0, %1" ::"v"(waddr), "v"((u32x2_a){lo, hi}) : "memory");
               else
                 lds_store_4bf16_a2(waddr, lo, hi);
             }
             // band of (query fr, key j0+32hh+16st2+4g+rr) = scratch[fr][16st2 + 4g + rr + 15 - fr]
-            typedef bf16 bf16x4 __attribute__((ext_vector_type(4)));
-            bf16x4 bdv4[2];
+            typedef E ex4 __attribute__((ext_vector_type(4)));
+            ex4 bdv4[2];
 #pragma unroll
             for (int st2 = 0; st2 < 2; ++st2)
               asm volatile("ds_read_b64 %0, %1"
@@ -502,7 +508,7 @@ __global__ __launch_bounds__(512, 1) void chunk_attention_ring_kernel(
               const int st = 2 * hh + st2;
               f32x4 a = (f32x4){(float)bdv4[st2][0], (float)bdv4[st2][1], (float)bdv4[st2][2], (float)bdv4[st2][3]};
 #pragma unroll
-              for (int s = 0; s < 2; ++s) a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[st][s], qu[s], a, 0, 0, 0);
+              for (int s = 0; s < 2; ++s) a = mma16(kf[st][s], qu[s], a);
               S[t][st] = a;
             }
           }
@@ -537,11 +543,11 @@ __global__ __launch_bounds__(512, 1) void chunk_attention_ring_kernel(
             for (int rr = 0; rr < 4; ++rr) S[t][st][rr] = __builtin_amdgcn_exp2f(fmaf(S[t][st][rr], 1.4426950408889634f, -mxl));
         // ---- O^T[dim 16nt + 4g + rr][query fr] = sum_keys V^T . P^T (key order permuted, same for both);
         // the softmax denominator as a fifth MFMA against a constant "ones" row (row 0 of an A
-        // fragment held in registers): l = sum over keys of the bf16 p the numerator uses, and no
+        // fragment held in registers): l = sum over keys of the E p the numerator uses, and no
         // VALU add per score
         f32x4 O[4], Ol = (f32x4){0.f, 0.f, 0.f, 0.f};
-        const bf16 one_or_zero = (bf16)(fr == 0 ? 1.f : 0.f);
-        const bf16x8 ones = (bf16x8){one_or_zero, one_or_zero, one_or_zero, one_or_zero,
+        const E one_or_zero = (E)(fr == 0 ? 1.f : 0.f);
+        const ex8 ones = (ex8){one_or_zero, one_or_zero, one_or_zero, one_or_zero,
                                      one_or_zero, one_or_zero, one_or_zero, one_or_zero};
 #pragma unroll
         for (int nt = 0; nt < 4; ++nt) O[nt] = (f32x4){0.f, 0.f, 0.f, 0.f};
@@ -551,23 +557,23 @@ __global__ __launch_bounds__(512, 1) void chunk_attention_ring_kernel(
           if ((MASK && j0 >= key_hi) || (diag & 15) == 3) continue;
 #pragma unroll
           for (int s = 0; s < 2; ++s) {
-            bf16x8 pb;
+            ex8 pb;
 #pragma unroll
             for (int rr = 0; rr < 4; ++rr) {
-              pb[rr] = (bf16)S[t][2 * s][rr];
-              pb[4 + rr] = (bf16)S[t][2 * s + 1][rr];
+              pb[rr] = (E)S[t][2 * s][rr];
+              pb[4 + rr] = (E)S[t][2 * s + 1][rr];
             }
             const char* va_ = vt + vt_lane + ring16(j0 + 32 * s) * 2;
             const char* vb_ = vt + vt_lane + ring16(j0 + 32 * s + 16) * 2;
 #pragma unroll
             for (int nt = 0; nt < 4; ++nt) {
-              typedef bf16 bf16x4 __attribute__((ext_vector_type(4)));
-              const bf16x4 lo = *reinterpret_cast<const bf16x4*>(va_ + 16 * nt * VT_PITCH_B);
-              const bf16x4 hi = *reinterpret_cast<const bf16x4*>(vb_ + 16 * nt * VT_PITCH_B);
-              const bf16x8 va = (bf16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-              O[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va, pb, O[nt], 0, 0, 0);
+              typedef E ex4 __attribute__((ext_vector_type(4)));
+              const ex4 lo = *reinterpret_cast<const ex4*>(va_ + 16 * nt * VT_PITCH_B);
+              const ex4 hi = *reinterpret_cast<const ex4*>(vb_ + 16 * nt * VT_PITCH_B);
+              const ex8 va = (ex8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+              O[nt] = mma16(va, pb, O[nt]);
             }
-            Ol = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pb, Ol, 0, 0, 0);
+            Ol = mma16(ones, pb, Ol);
           }
         }
         // row 0 of Ol^T (query fr) sits in register 0 of lane fr (g = 0)
@@ -575,15 +581,15 @@ __global__ __launch_bounds__(512, 1) void chunk_attention_ring_kernel(
         const int qi = i0 + fr;
         const bool live = qi < q_valid && l > 0.f;
         const float inv = live ? 1.f / l : 0.f;
-        bf16* op = out + (size_t)(q_row0 + qi) * d + h * 64;
+        E* op = out + (size_t)(q_row0 + qi) * d + h * 64;
   #if ATTN_STORE16
         // dim pairs (16 nt .. +15, 16 (nt+1) ..): one permlane16 swap per packed dword leaves lane g with
         // 8 contiguous dims, so each query row leaves as two 64-B pieces (2 x 16-B stores per lane)
 #pragma unroll
         for (int pr = 0; pr < 2; ++pr) {
-          const unsigned x0 = pack_bf16x2_a(O[2 * pr][0] * inv, O[2 * pr][1] * inv), x1 = pack_bf16x2_a(O[2 * pr][2] * inv, O[2 * pr][3] * inv);
-          const unsigned y0 = pack_bf16x2_a(O[2 * pr + 1][0] * inv, O[2 * pr + 1][1] * inv),
-                         y1 = pack_bf16x2_a(O[2 * pr + 1][2] * inv, O[2 * pr + 1][3] * inv);
+          const unsigned x0 = pack_e2<E>(O[2 * pr][0] * inv, O[2 * pr][1] * inv), x1 = pack_e2<E>(O[2 * pr][2] * inv, O[2 * pr][3] * inv);
+          const unsigned y0 = pack_e2<E>(O[2 * pr + 1][0] * inv, O[2 * pr + 1][1] * inv),
+                         y1 = pack_e2<E>(O[2 * pr + 1][2] * inv, O[2 * pr + 1][3] * inv);
           const auto r0 = __builtin_amdgcn_permlane16_swap(x0, y0, false, false);
           const auto r1 = __builtin_amdgcn_permlane16_swap(x1, y1, false, false);
           *reinterpret_cast<u32x4*>(op + 32 * pr + 16 * (g & 1) + 8 * (g >> 1)) = (u32x4){r0[0], r1[0], r0[1], r1[1]};
@@ -591,9 +597,9 @@ __global__ __launch_bounds__(512, 1) void chunk_attention_ring_kernel(
   #else
 #pragma unroll
         for (int nt = 0; nt < 4; ++nt) {
-          typedef bf16 bf16x4 __attribute__((ext_vector_type(4)));
-          *reinterpret_cast<bf16x4*>(op + 16 * nt + 4 * g) =
-              (bf16x4){(bf16)(O[nt][0] * inv), (bf16)(O[nt][1] * inv), (bf16)(O[nt][2] * inv), (bf16)(O[nt][3] * inv)};
+          typedef E ex4 __attribute__((ext_vector_type(4)));
+          *reinterpret_cast<ex4*>(op + 16 * nt + 4 * g) =
+              (ex4){(E)(O[nt][0] * inv), (E)(O[nt][1] * inv), (E)(O[nt][2] * inv), (E)(O[nt][3] * inv)};
         }
   #endif
       };
@@ -610,9 +616,10 @@ __global__ __launch_bounds__(512, 1) void chunk_attention_ring_kernel(
 }
 
 // returns -1 when the shape is not eligible for the ring kernel
-int chunk_attention_masked_bf16(const bf16* q, const bf16* kv, int kv_rows, const bf16* P, int p_rows,
+template <typename E>
+int chunk_attention_masked_ring(const E* q, const E* kv, int kv_rows, const E* P, int p_rows,
                                 const float* pos_u, const float* pos_v, const int32_t* desc, int n_chunks, int H,
-                                int C, int W, bf16* out, hipStream_t st, int diag, int p_ld, int reuse,
+                                int C, int W, E* out, hipStream_t st, int diag, int p_ld, int reuse,
                                 int min_chunks) {
   if (p_ld <= 0) p_ld = H * 64;
   // W <= 320: a query's scores are 5 tiles of 64 keys held in registers (exact softmax)
@@ -628,7 +635,7 @@ int chunk_attention_masked_bf16(const bf16* q, const bf16* kv, int kv_rows, cons
   const int nch = (n_chunks + gx - 1) / gx;
   const dim3 grid(gx, H);
 #define RING_L(DG_, NT_)                                                                                             \
-  hipLaunchKernelGGL((chunk_attention_ring_kernel<DG_, NT_>), grid, dim3(512), 0, st, q, kv, kv_rows, P, p_rows, pos_u, \
+  hipLaunchKernelGGL((chunk_attention_ring_kernel<DG_, NT_, E>), grid, dim3(512), 0, st, q, kv, kv_rows, P, p_rows, pos_u, \
                      pos_v, desc, n_chunks, H, C, W, out, diag, nch, p_ld)
   const int nti = W % 64 == 0 ? W / 64 : 0;
   if (diag) {
@@ -644,6 +651,20 @@ int chunk_attention_masked_bf16(const bf16* q, const bf16* kv, int kv_rows, cons
 #undef RING_L
   CFM_CHECK_LAUNCH();
   return 0;
+}
+int chunk_attention_masked_bf16(const bf16* q, const bf16* kv, int kv_rows, const bf16* P, int p_rows,
+                                const float* pos_u, const float* pos_v, const int32_t* desc, int n_chunks, int H,
+                                int C, int W, bf16* out, hipStream_t st, int diag, int p_ld, int reuse,
+                                int min_chunks) {
+  return chunk_attention_masked_ring<bf16>(q, kv, kv_rows, P, p_rows, pos_u, pos_v, desc, n_chunks, H, C, W, out, st,
+                                           diag, p_ld, reuse, min_chunks);
+}
+int chunk_attention_masked_f16(const f16* q, const f16* kv, int kv_rows, const f16* P, int p_rows,
+                               const float* pos_u, const float* pos_v, const int32_t* desc, int n_chunks, int H,
+                               int C, int W, f16* out, hipStream_t st, int diag, int p_ld, int reuse,
+                               int min_chunks) {
+  return chunk_attention_masked_ring<f16>(q, kv, kv_rows, P, p_rows, pos_u, pos_v, desc, n_chunks, H, C, W, out, st,
+                                          diag, p_ld, reuse, min_chunks);
 }
 
 

@@ -39,6 +39,7 @@ struct EpiArgs {
                                  // (leaves CUs to the other streams of a pipelined caller)
   int wsp_small_rows = 32768;
   int n512 = 0;                  // N = 512, K >= 1024: the full-row 128 x 512 kernel (gemm_rowln.hip, plain form)
+  int f16 = 0;                   // 16-bit operands / outputs are f16 (v_mfma_f32_16x16x32_f16), not bf16
   // DW2 (front-end pw1 + ReLU + dw2, K = N = 512 weight-stationary only): dw2 taps tap-major [9][N]
   // f32, bias [N]; the pw1 rows are (window, t2 < t2n, f2 < 19); out = dw2 rows (window, t3 < t3n, f3 < 9)
   const float* dw_w = nullptr;
@@ -174,6 +175,11 @@ int chunk_attention_masked_bf16(const bf16* q, const bf16* kv, int kv_rows, cons
                                 const float* pos_u, const float* pos_v, const int32_t* desc, int n_chunks, int H,
                                 int C, int W, bf16* out, hipStream_t st, int diag = 0, int p_ld = 0, int reuse = 1,
                                 int min_chunks = 2);
+// the same ring kernel on f16 operands (v_mfma_f32_16x16x32_f16; the fp16 compute mode)
+int chunk_attention_masked_f16(const f16* q, const f16* kv, int kv_rows, const f16* P, int p_rows,
+                               const float* pos_u, const float* pos_v, const int32_t* desc, int n_chunks, int H,
+                               int C, int W, f16* out, hipStream_t st, int diag = 0, int p_ld = 0, int reuse = 1,
+                               int min_chunks = 2);
 
 // masked-batch attention for head_dim 128 (attention128.hip): V^T copy of the KV stream, then the
 // band / score / P.V kernel; -1 when the shape is not eligible (C = 64, W <= 320, W % 64 == 0)

@@ -180,22 +180,30 @@ __global__ __launch_bounds__(512) void conv_dw_ln_silu_lds_kernel(const bf16* __
 // with w[15] = 0 on the window's extra zero row.  LayerNorm statistics by DPP / permlane
 // reductions (no LDS round trips), SiLU as v_exp + v_rcp.
 typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
-CFM_DEV float dot2_bf16(unsigned a, unsigned b, float c) {
-  return __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, a), __builtin_bit_cast(bf16x2_t, b), c, false);
+typedef _Float16 f16x2_t __attribute__((ext_vector_type(2)));
+// E = bf16: v_dot2_f32_bf16; E = f16 (fp16 mode): v_dot2_f32_f16 on f16 taps
+template <typename E>
+CFM_DEV float dot2e(unsigned a, unsigned b, float c) {
+  if constexpr (std::is_same<E, f16>::value)
+    return __builtin_amdgcn_fdot2(__builtin_bit_cast(f16x2_t, a), __builtin_bit_cast(f16x2_t, b), c, false);
+  else
+    return __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, a), __builtin_bit_cast(bf16x2_t, b), c, false);
 }
-CFM_DEV unsigned pk_bf16(float lo, float hi) {
-  return __builtin_bit_cast(unsigned, (bf16x2_t){(__bf16)lo, (__bf16)hi});
+template <typename E>
+CFM_DEV unsigned pke(float lo, float hi) {
+  typedef E e2 __attribute__((ext_vector_type(2)));
+  return __builtin_bit_cast(unsigned, (e2){(E)lo, (E)hi});
 }
 // the compute half of the dot2 kernels: wave w's RW output rows from the staged window `win`
 // (`w` indexes RW-row groups of the chunk; the staged window starts at window row win_row0)
-template <int VPL>
-CFM_DEV void conv_dot2_rows(const bf16* __restrict__ win, int nout, int out_row0, const float* __restrict__ wdw,
+template <int VPL, typename E>
+CFM_DEV void conv_dot2_rows(const E* __restrict__ win, int nout, int out_row0, const float* __restrict__ wdw,
                             const float* __restrict__ bdw, const float* __restrict__ lnw,
-                            const float* __restrict__ lnb, float eps, bf16* __restrict__ out, int w, int lane,
+                            const float* __restrict__ lnb, float eps, E* __restrict__ out, int w, int lane,
                             int win_row0 = 0) {
   constexpr int d = VPL * 64, NW = VPL / 2;
   constexpr int RW = 8;
-  typedef bf16 bvec __attribute__((ext_vector_type(VPL)));
+  typedef E bvec __attribute__((ext_vector_type(VPL)));
   const int i0 = w * RW;
   if (i0 >= nout) return;
   win -= (size_t)win_row0 * d;   // rows below win_row0 are never read
@@ -213,7 +221,7 @@ CFM_DEV void conv_dot2_rows(const bf16* __restrict__ win, int nout, int out_row0
       for (int e = 0; e < VPL; ++e) hi[e] = 0.f;
     }
 #pragma unroll
-    for (int e = 0; e < VPL; ++e) wp[p][e] = pk_bf16(lo[e], hi[e]);
+    for (int e = 0; e < VPL; ++e) wp[p][e] = pke<E>(lo[e], hi[e]);
   }
   float acc[RW][VPL];
 #pragma unroll
@@ -251,7 +259,7 @@ CFM_DEV void conv_dot2_rows(const bf16* __restrict__ win, int nout, int out_row0
       const int t = j - r;
       if (t >= 0 && t <= 14 && (t & 1) == 0) {
 #pragma unroll
-        for (int e = 0; e < VPL; ++e) acc[r][e] = dot2_bf16(pk[e], wp[t >> 1][e], acc[r][e]);
+        for (int e = 0; e < VPL; ++e) acc[r][e] = dot2e<E>(pk[e], wp[t >> 1][e], acc[r][e]);
       }
     }
 #pragma unroll
@@ -278,26 +286,26 @@ CFM_DEV void conv_dot2_rows(const bf16* __restrict__ win, int nout, int out_row0
 #pragma unroll
     for (int e = 0; e < VPL; ++e) {
       const float y = (acc[r][e] - mean) * rstd * lw[e] + lb[e];
-      o[e] = (bf16)(y * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-1.4426950408889634f * y)));
+      o[e] = (E)(y * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-1.4426950408889634f * y)));
     }
     // non-temporal: read once, by pw2 (A/B x3: this kernel 1.72 -> 1.66 ms/step, pw2 1.13 -> 1.09)
     __builtin_nontemporal_store(o, reinterpret_cast<bvec*>(out + (size_t)(out_row0 + i0 + r) * d + c0));
   }
 }
 
-template <int VPL>
-__global__ __launch_bounds__(512) void conv_dw_ln_silu_dot2_kernel(const bf16* __restrict__ glu,
+template <int VPL, typename E>
+__global__ __launch_bounds__(512) void conv_dw_ln_silu_dot2_kernel(const E* __restrict__ glu,
                                                                    const int32_t* __restrict__ desc,
                                                                    const float* __restrict__ wdw,
                                                                    const float* __restrict__ bdw,
                                                                    const float* __restrict__ lnw,
                                                                    const float* __restrict__ lnb, float eps,
-                                                                   bf16* __restrict__ out, int dma) {
+                                                                   E* __restrict__ out, int dma) {
   constexpr int d = VPL * 64, NW = VPL / 2;   // NW dwords (channel pairs) per lane per row
   constexpr int MAXJ = 64 + 15;               // window rows + the zero row of the w[15] = 0 tap
   constexpr int RW = 8;                       // output rows per wave
-  typedef bf16 bvec __attribute__((ext_vector_type(VPL)));
-  __shared__ __attribute__((aligned(16))) bf16 win[MAXJ * d];
+  typedef E bvec __attribute__((ext_vector_type(VPL)));
+  __shared__ __attribute__((aligned(16))) E win[MAXJ * d];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int32_t* D = desc + (size_t)blockIdx.x * CD_INTS;
   const int out_row0 = D[CD_OUT_ROW0], nout = D[CD_NOUT], src0 = D[CD_SRC_ROW0];
@@ -324,7 +332,7 @@ __global__ __launch_bounds__(512) void conv_dw_ln_silu_dot2_kernel(const bf16* _
     }
   }
   __syncthreads();
-  conv_dot2_rows<VPL>(win, nout, out_row0, wdw, bdw, lnw, lnb, eps, out, w, lane);
+  conv_dot2_rows<VPL, E>(win, nout, out_row0, wdw, bdw, lnw, lnb, eps, out, w, lane);
 }
 
 
@@ -332,17 +340,17 @@ __global__ __launch_bounds__(512) void conv_dw_ln_silu_dot2_kernel(const bf16* _
 // a whole CU and every chunk's window DMA waits with no other work on the CU.  Here a 4-wave block
 // takes 32 output rows of a chunk (window rows 32h .. 32h + 46, 47 KiB), two blocks share a CU and
 // one block's window DMA overlaps the other's arithmetic; the 14 overlap rows are read twice.
-template <int VPL, int QR>
-__global__ __launch_bounds__(QR * 8) void conv_dw_ln_silu_dot2h_kernel(const bf16* __restrict__ glu,
+template <int VPL, int QR, typename E>
+__global__ __launch_bounds__(QR * 8) void conv_dw_ln_silu_dot2h_kernel(const E* __restrict__ glu,
                                                                     const int32_t* __restrict__ desc,
                                                                     const float* __restrict__ wdw,
                                                                     const float* __restrict__ bdw,
                                                                     const float* __restrict__ lnw,
                                                                     const float* __restrict__ lnb, float eps,
-                                                                    bf16* __restrict__ out) {
+                                                                    E* __restrict__ out) {
   constexpr int d = VPL * 64, NWV = QR / 8;
   constexpr int HJ = QR + 15;   // window rows of the block (+ the zero row of the w[15] = 0 tap)
-  __shared__ __attribute__((aligned(16))) bf16 win[HJ * d];
+  __shared__ __attribute__((aligned(16))) E win[HJ * d];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int half = blockIdx.y;
   const int32_t* D = desc + (size_t)blockIdx.x * CD_INTS;
@@ -371,7 +379,7 @@ __global__ __launch_bounds__(QR * 8) void conv_dw_ln_silu_dot2h_kernel(const bf1
     }
   }
   __syncthreads();
-  conv_dot2_rows<VPL>(win, nout, out_row0, wdw, bdw, lnw, lnb, eps, out, NWV * half + w, lane, r0);
+  conv_dot2_rows<VPL, E>(win, nout, out_row0, wdw, bdw, lnw, lnb, eps, out, NWV * half + w, lane, r0);
 }
 
 template <typename T>
@@ -379,29 +387,31 @@ int conv_dw_ln_silu(const T* glu, const int32_t* desc, int nblk, int d, const fl
                     const float* lnw, const float* lnb, float eps, T* out, hipStream_t st, int dot2, int dma) {
   if (nblk <= 0) return 0;
   // dot2 = 0: the per-tap f32 kernel; dma = 0: stage the window through registers (A/B, model options)
-  if constexpr (std::is_same<T, bf16>::value) {
+  if constexpr (sizeof(T) == 2) {   // bf16 / f16 (the non-dot2 LDS kernel: bf16 only)
     if (dot2 >= 2 && d == 512) {   // half-chunk blocks (conv_dot2 = 2), quarter-chunk blocks (3)
       if (dot2 == 3)
-        hipLaunchKernelGGL((conv_dw_ln_silu_dot2h_kernel<8, 16>), dim3(nblk, 4), dim3(128), 0, st, glu, desc, wdw_t, bdw, lnw, lnb, eps, out);
+        hipLaunchKernelGGL((conv_dw_ln_silu_dot2h_kernel<8, 16, T>), dim3(nblk, 4), dim3(128), 0, st, glu, desc, wdw_t, bdw, lnw, lnb, eps, out);
       else
-        hipLaunchKernelGGL((conv_dw_ln_silu_dot2h_kernel<8, 32>), dim3(nblk, 2), dim3(256), 0, st, glu, desc, wdw_t, bdw, lnw, lnb, eps, out);
+        hipLaunchKernelGGL((conv_dw_ln_silu_dot2h_kernel<8, 32, T>), dim3(nblk, 2), dim3(256), 0, st, glu, desc, wdw_t, bdw, lnw, lnb, eps, out);
       CFM_CHECK_LAUNCH();
       return 0;
     }
     if (dot2) {
-      if (d == 128) hipLaunchKernelGGL((conv_dw_ln_silu_dot2_kernel<2>), dim3(nblk), dim3(512), 0, st, glu, desc, wdw_t, bdw, lnw, lnb, eps, out, dma);
-      else if (d == 256) hipLaunchKernelGGL((conv_dw_ln_silu_dot2_kernel<4>), dim3(nblk), dim3(512), 0, st, glu, desc, wdw_t, bdw, lnw, lnb, eps, out, dma);
-      else if (d == 512) hipLaunchKernelGGL((conv_dw_ln_silu_dot2_kernel<8>), dim3(nblk), dim3(512), 0, st, glu, desc, wdw_t, bdw, lnw, lnb, eps, out, dma);
+      if (d == 128) hipLaunchKernelGGL((conv_dw_ln_silu_dot2_kernel<2, T>), dim3(nblk), dim3(512), 0, st, glu, desc, wdw_t, bdw, lnw, lnb, eps, out, dma);
+      else if (d == 256) hipLaunchKernelGGL((conv_dw_ln_silu_dot2_kernel<4, T>), dim3(nblk), dim3(512), 0, st, glu, desc, wdw_t, bdw, lnw, lnb, eps, out, dma);
+      else if (d == 512) hipLaunchKernelGGL((conv_dw_ln_silu_dot2_kernel<8, T>), dim3(nblk), dim3(512), 0, st, glu, desc, wdw_t, bdw, lnw, lnb, eps, out, dma);
       else return (int)hipErrorInvalidValue;
       CFM_CHECK_LAUNCH();
       return 0;
     }
-    if (d == 128) hipLaunchKernelGGL((conv_dw_ln_silu_lds_kernel<2>), dim3(nblk), dim3(512), 0, st, glu, desc, wdw_t, bdw, lnw, lnb, eps, out);
-    else if (d == 256) hipLaunchKernelGGL((conv_dw_ln_silu_lds_kernel<4>), dim3(nblk), dim3(512), 0, st, glu, desc, wdw_t, bdw, lnw, lnb, eps, out);
-    else if (d == 512) hipLaunchKernelGGL((conv_dw_ln_silu_lds_kernel<8>), dim3(nblk), dim3(512), 0, st, glu, desc, wdw_t, bdw, lnw, lnb, eps, out);
-    else return (int)hipErrorInvalidValue;
-    CFM_CHECK_LAUNCH();
-    return 0;
+    if constexpr (std::is_same<T, bf16>::value) {
+      if (d == 128) hipLaunchKernelGGL((conv_dw_ln_silu_lds_kernel<2>), dim3(nblk), dim3(512), 0, st, glu, desc, wdw_t, bdw, lnw, lnb, eps, out);
+      else if (d == 256) hipLaunchKernelGGL((conv_dw_ln_silu_lds_kernel<4>), dim3(nblk), dim3(512), 0, st, glu, desc, wdw_t, bdw, lnw, lnb, eps, out);
+      else if (d == 512) hipLaunchKernelGGL((conv_dw_ln_silu_lds_kernel<8>), dim3(nblk), dim3(512), 0, st, glu, desc, wdw_t, bdw, lnw, lnb, eps, out);
+      else return (int)hipErrorInvalidValue;
+      CFM_CHECK_LAUNCH();
+      return 0;
+    }
   }
   const dim3 grid(nblk, 4);   // 4 x 4 waves stride over the (<= 64) rows of a block
   if (d == 128) hipLaunchKernelGGL((conv_dw_ln_silu_kernel<T, 2>), grid, dim3(256), 0, st, glu, desc, wdw_t, bdw, lnw, lnb, eps, out);

@@ -116,15 +116,23 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 constexpr int FE_POS_BLOCK = 128;                     // dw1 positions per block (4 waves x 32)
 constexpr int FE_XROWS = 4 * ((FE_POS_BLOCK - 1) / FE_F2 + 2) + 3;   // staged input rows (>= 4*span + 7)
 
+// v_mfma_f32_32x32x16_{bf16,f16} on 8-element fragments of E
+template <typename E, typename V>
+CFM_DEV f32x16 mfma32x16(const V& a, const V& b, const f32x16& c) {
+  if constexpr (std::is_same<E, f16>::value) return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+  else return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+template <typename E>
 __global__ __launch_bounds__(256, 3) void fe_conv0_dw_mfma_kernel(const float* __restrict__ feats,
                                                                const float* const* __restrict__ tab, int step,
                                                                const int32_t* __restrict__ meta, int meta_stride,
                                                                int W, int T2, const float* __restrict__ cm,
                                                                const float* __restrict__ ci,
                                                                const float* __restrict__ wpack, int d,
-                                                               bf16* __restrict__ out) {
+                                                               E* __restrict__ out) {
+  typedef E ex8 __attribute__((ext_vector_type(8)));   // bf16 / f16 (fp16 mode) operands
   __shared__ float xin[FE_XROWS * FE_F0];
-  // per-wave output staging [32 positions][64 channels] bf16, 144-B rows: the MFMA layout gives
+  // per-wave output staging [32 positions][64 channels] E, 144-B rows: the MFMA layout gives
   // each lane one channel; two channel tiles are gathered here and leave as full 128-B rows
   constexpr int OPITCH = 144;
   __shared__ __attribute__((aligned(16))) char ostage[4][32 * OPITCH];
@@ -146,7 +154,7 @@ __global__ __launch_bounds__(256, 3) void fe_conv0_dw_mfma_kernel(const float* _
   const int pw = p0 + wv * 32;   // this wave's first position
   if (pw >= P) return;
   // A fragments: row m = n -> position pw + n; k = 8*hh + j = conv0 tap e (e < 9)
-  bf16x8 xa[9];
+  ex8 xa[9];
   {
     const int pos = min(pw + n, P - 1);   // rows past P are computed and discarded
     const int t2 = pos / FE_F2, f2 = pos - t2 * FE_F2;
@@ -156,12 +164,12 @@ __global__ __launch_bounds__(256, 3) void fe_conv0_dw_mfma_kernel(const float* _
       const float* xs = xb + 2 * (s / 3) * FE_F0 + 2 * (s % 3);
       if (hh == 0) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) xa[s][j] = (bf16)xs[(j / 3) * FE_F0 + j % 3];
+        for (int j = 0; j < 8; ++j) xa[s][j] = (E)xs[(j / 3) * FE_F0 + j % 3];
       } else {
-        xa[s][0] = (bf16)xs[2 * FE_F0 + 2];
-        xa[s][1] = (bf16)1.f;   // k = 9: the conv0 bias row (B holds b0 there; bf16 as under autocast)
+        xa[s][0] = (E)xs[2 * FE_F0 + 2];
+        xa[s][1] = (E)1.f;   // k = 9: the conv0 bias row (B holds b0 there; E as under autocast)
 #pragma unroll
-        for (int j = 2; j < 8; ++j) xa[s][j] = (bf16)0.f;
+        for (int j = 2; j < 8; ++j) xa[s][j] = (E)0.f;
       }
     }
   }
@@ -195,9 +203,9 @@ __global__ __launch_bounds__(256, 3) void fe_conv0_dw_mfma_kernel(const float* _
       // lanes of the upper half need only conv0 tap 8 (k = 8) and the bias b0 (k = 9); the rest
       // of K is zero, so the conv0 MFMAs start from a zero accumulator
       const float t[9] = {qw[0][0], qw[0][1], qw[0][2], qw[0][3], qw[1][0], qw[1][1], qw[1][2], qw[1][3], qw[2][0]};
-      bf16x8 wcur;
+      ex8 wcur;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) wcur[j] = (bf16)(hh ? (j == 0 ? t[8] : j == 1 ? qw[4][2] : 0.f) : t[j]);
+      for (int j = 0; j < 8; ++j) wcur[j] = (E)(hh ? (j == 0 ? t[8] : j == 1 ? qw[4][2] : 0.f) : t[j]);
       const float wkc[9] = {qw[2][1], qw[2][2], qw[2][3], qw[3][0], qw[3][1], qw[3][2], qw[3][3], qw[4][0], qw[4][1]};
       const f32x16 seed = {};
       f32x16 o;
@@ -207,11 +215,11 @@ __global__ __launch_bounds__(256, 3) void fe_conv0_dw_mfma_kernel(const float* _
       // taps are software-pipelined one deep: MFMA s+1 is issued before tap s's relu/FMA work
       // (scheduling barriers pin the order: without them the compiler sinks MFMA s+1 below tap
       // s's VALU and both accumulator sets share registers, serialising MFMA and VALU per wave)
-      f32x16 acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xa[0], wcur, seed, 0, 0, 0);
+      f32x16 acc = mfma32x16<E>(xa[0], wcur, seed);
 #pragma unroll
       for (int s = 0; s < 9; ++s) {
         f32x16 nxt;
-        if (s + 1 < 9) nxt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xa[s + 1], wcur, seed, 0, 0, 0);
+        if (s + 1 < 9) nxt = mfma32x16<E>(xa[s + 1], wcur, seed);
         __builtin_amdgcn_sched_barrier(0);
         // one v_max_f32 + one v_fma_f32 per value (IEEE mode off in build.py: no canonicalising
         // max in front; no SLP packing: a v_pk_fma_f32 beside MFMAs issues slower than two v_fma_f32)
@@ -224,7 +232,7 @@ __global__ __launch_bounds__(256, 3) void fe_conv0_dw_mfma_kernel(const float* _
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int m = 8 * (r >> 2) + 4 * hh + (r & 3);
-        *reinterpret_cast<bf16*>(os + m * OPITCH + (32 * half + n) * 2) = (bf16)o[r];
+        *reinterpret_cast<E*>(os + m * OPITCH + (32 * half + n) * 2) = (E)o[r];
       }
     }
     // 64 channels staged: lane -> 16-B chunk (lane & 7) of positions (lane >> 3) + 8k, buffer
@@ -577,8 +585,14 @@ int frontend_conv0_dw(const float* feats, const float* const* tab, int step, con
       CFM_CHECK_LAUNCH();
       return 0;
     }
-    hipLaunchKernelGGL(fe_conv0_dw_mfma_kernel, dim3((T2 * FE_F2 + FE_POS_BLOCK - 1) / FE_POS_BLOCK, nwin), dim3(256),
+    hipLaunchKernelGGL(fe_conv0_dw_mfma_kernel<bf16>, dim3((T2 * FE_F2 + FE_POS_BLOCK - 1) / FE_POS_BLOCK, nwin), dim3(256),
                        0, st, feats, tab, step, meta, meta_stride, W, T2, cmvn_mean, cmvn_istd, wpack, d, out);
+  } else if (std::is_same<T, f16>::value && var >= 1 && d % 64 == 0 && (size_t)T2 * FE_F2 * d * 2 < ((size_t)1 << 31)) {
+    // fp16 mode: the position-stationary MFMA kernel on f16 (the channel-stationary one's 2^-24 scaling is
+    // bf16-only: f16 has no exponent range for it)
+    hipLaunchKernelGGL(fe_conv0_dw_mfma_kernel<f16>, dim3((T2 * FE_F2 + FE_POS_BLOCK - 1) / FE_POS_BLOCK, nwin), dim3(256),
+                       0, st, feats, tab, step, meta, meta_stride, W, T2, cmvn_mean, cmvn_istd, wpack, d,
+                       reinterpret_cast<f16*>(out));
   } else {
     hipLaunchKernelGGL((fe_conv0_dw_kernel<T>), grid, dim3(256), 0, st, feats, tab, step, meta, meta_stride, W, T2,
                        cmvn_mean,

@@ -204,9 +204,12 @@ int gemm_bf16_big(int epi, int act, const bf16* A, int lda, const bf16* W, int l
 template <typename T>
 int gemm(int epi, int act, const T* A, int lda, const T* W, int ldw, int M, int N, int K, const EpiArgs& ep,
          hipStream_t st) {
-  if constexpr (std::is_same<T, bf16>::value) {
+  if constexpr (sizeof(T) == 2) {   // bf16 / f16: the 256 x 256 and weight-stationary kernels (EpiArgs::f16)
     if (!ep.small_tiles) {
-      const int r = gemm_bf16_big(epi, act, A, lda, W, ldw, M, N, K, ep, st);
+      EpiArgs e = ep;
+      e.f16 = std::is_same<T, f16>::value;
+      const int r = gemm_bf16_big(epi, act, reinterpret_cast<const bf16*>(A), lda, reinterpret_cast<const bf16*>(W),
+                                  ldw, M, N, K, e, st);
       if (r != -1) return r;
     }
   }

@@ -36,7 +36,7 @@ namespace cfm {
 #endif
 // DIAG: 0 = normal; 1 = skip MFMAs (DMA + epilogue only); 2 = skip DMA inside the loop (MFMA on stale LDS);
 // 3 = skip the epilogue (no bias/activation/stores)
-template <int EPI, int ACT, int DIAG = 0>
+template <int EPI, int ACT, int DIAG = 0, int FMT = 0>
 __global__ __launch_bounds__(512, 1) void gemm_bf16_256_kernel(const bf16* __restrict__ A, int lda,
                                                                const bf16* __restrict__ W, int ldw, int M, int N,
                                                                int K, EpiArgs ep) {
@@ -143,10 +143,10 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_256_kernel(const bf16* __res
                 // staging in A slot (s + 2) % 3: A(s - 1) there was read by both groups' last LOAD
                 // segments, and A(s + 2) is issued only in the ss = 1 LOAD segment, after the barrier
                 // that ends this segment for both groups
-                wave_epilogue_fullrow<ACT>(acc, tile_m(epi_t) * 256 + wm * 128, tile_n(epi_t) * 256 + wn * 64, fr, g,
+                wave_epilogue_fullrow<ACT, FMT>(acc, tile_m(epi_t) * 256 + wm * 128, tile_n(epi_t) * 256 + wn * 64, fr, g,
                                            lane, M, ep, lds_base + (unsigned)(((s + 2) % 3) * 32768 + wid * 2304));
               else
-                tile_epilogue<EPI, ACT>(acc, tile_m(epi_t), tile_n(epi_t), wm, wn, fr, g, M, ep);
+                tile_epilogue<EPI, ACT, false, FMT>(acc, tile_m(epi_t), tile_n(epi_t), wm, wn, fr, g, M, ep);
             }
             epi_t = -1;
           }
@@ -186,7 +186,7 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_256_kernel(const bf16* __res
           for (int i = 0; i < 4; ++i)
 #pragma unroll
             for (int j = 0; j < 8; ++j)
-              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[i], af[j], acc[i][j], 0, 0, 0);
+              acc[i][j] = mfma16x32<FMT>(wf[i], af[j], acc[i][j]);
           if constexpr (DIAG == 5) __builtin_amdgcn_s_setprio(0);
         }
         __builtin_amdgcn_sched_barrier(0);
@@ -203,10 +203,10 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_256_kernel(const bf16* __res
     if constexpr (EPI == EPI_STORE && G256_FULLROW) {
       // every DMA has landed and been read; the other group only runs MFMAs from here on
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      wave_epilogue_fullrow<ACT>(acc, tile_m(epi_t) * 256 + wm * 128, tile_n(epi_t) * 256 + wn * 64, fr, g, lane, M,
+      wave_epilogue_fullrow<ACT, FMT>(acc, tile_m(epi_t) * 256 + wm * 128, tile_n(epi_t) * 256 + wn * 64, fr, g, lane, M,
                                  ep, lds_base + (unsigned)(((s + 2) % 3) * 32768 + wid * 2304));
     } else {
-      tile_epilogue<EPI, ACT>(acc, tile_m(epi_t), tile_n(epi_t), wm, wn, fr, g, M, ep);
+      tile_epilogue<EPI, ACT, false, FMT>(acc, tile_m(epi_t), tile_n(epi_t), wm, wn, fr, g, M, ep);
     }
   }
   if (grp == 0) asm volatile("s_barrier" ::: "memory");
@@ -220,7 +220,13 @@ static int launch256(const bf16* A, int lda, const bf16* W, int ldw, int M, int 
   const int grid = tiles <= n_cu ? tiles : n_cu;   // persistent: one 512-thread block per CU
   // ep.diag (timing diagnostics, model option "gemm_diag"): 1 no MFMA, 2 no DMA in the loop, 3 no
   // epilogue, 5 / 6 wave-group priorities
-#define G256(D) hipLaunchKernelGGL((gemm_bf16_256_kernel<EPI, ACT, D>), dim3(grid), dim3(512), 0, st, A, lda, W, ldw, M, N, K, ep)
+#define G256(D)                                                                                                   \
+  do {                                                                                                            \
+    if (ep.f16)                                                                                                   \
+      hipLaunchKernelGGL((gemm_bf16_256_kernel<EPI, ACT, D, 1>), dim3(grid), dim3(512), 0, st, A, lda, W, ldw, M, N, K, ep); \
+    else                                                                                                          \
+      hipLaunchKernelGGL((gemm_bf16_256_kernel<EPI, ACT, D, 0>), dim3(grid), dim3(512), 0, st, A, lda, W, ldw, M, N, K, ep); \
+  } while (0)
 #ifdef CFM_GEMM_DIAG
   switch (ep.diag) {
     case 1: G256(1); break;
@@ -254,7 +260,7 @@ int gemm_bf16_big(int epi, int act, const bf16* A, int lda, const bf16* W, int l
   // N = 512, K >= 1024 (FFN w2, the front-end output Linear) on full-row 128 x 512 tiles (gemm_rowln.hip): A read
   // once, W from L2.  Option "gemm_n512", off: random operands 394-413 vs 360-435 us, in the 240-min step FFN w2
   // 8.20 -> 9.87 ms/step (its A ring is one K-step deep: the full-row W slot takes 128 of the 160 KiB)
-  if (ep.n512 && N == 512 && K >= 1024 && ep.ldo == 512 && act == ACT_NONE && (epi == EPI_STORE || epi == EPI_STORE_F32)) {
+  if (ep.n512 && !ep.f16 && N == 512 && K >= 1024 && ep.ldo == 512 && act == ACT_NONE && (epi == EPI_STORE || epi == EPI_STORE_F32)) {
     RowLnArgs ra;
     ra.bias = ep.bias;
     ra.alpha = ep.alpha;

@@ -35,6 +35,24 @@ CFM_DEV unsigned pack_bf16x2(float a, float b) {
   typedef bf16 b2 __attribute__((ext_vector_type(2)));
   return __builtin_bit_cast(unsigned, (b2){(bf16)a, (bf16)b});
 }
+// FMT: the 16-bit format of operands and outputs, 0 = bf16, 1 = f16 (the kernels move both as raw
+// 16-bit lanes; only the MFMA and the output conversion differ)
+template <int FMT>
+CFM_DEV unsigned pack_h2(float a, float b) {
+  if constexpr (FMT == 1) {
+    typedef f16 h2 __attribute__((ext_vector_type(2)));
+    return __builtin_bit_cast(unsigned, (h2){(f16)a, (f16)b});
+  } else {
+    return pack_bf16x2(a, b);
+  }
+}
+template <int FMT>
+CFM_DEV f32x4 mfma16x32(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+  if constexpr (FMT == 1)
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
+  else
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
 template <int ACT>
 CFM_DEV f32x4 act4(f32x4 v) {
   if constexpr (ACT == ACT_RELU) {
@@ -69,7 +87,7 @@ CFM_DEV void store_pair16(bf16* base, size_t ld, int row, int g, u32x2_t x, u32x
 
 // One wave's 16*MB x 64 piece of C: m0 = row of m-block 0 for this lane (row base + fr), nw = first
 // column of the wave.
-template <int EPI, int ACT, int MB, bool NOST = false>
+template <int EPI, int ACT, int MB, bool NOST = false, int FMT = 0>
 CFM_DEV void wave_epilogue(f32x4 (&acc)[4][MB], int m0, int nw, int g, int M, const EpiArgs& ep) {
   if constexpr (EPI == EPI_STORE_F32 || EPI == EPI_RESID) {
 #pragma unroll
@@ -99,8 +117,8 @@ CFM_DEV void wave_epilogue(f32x4 (&acc)[4][MB], int m0, int nw, int g, int M, co
 #pragma unroll
       for (int p = 0; p < 2; ++p) {
         const f32x4 a = acc[2 * p][j], gt = acc[2 * p + 1][j];
-        o[p] = (u32x2_t){pack_bf16x2(a[0] * fast_sigmoid(gt[0]), a[1] * fast_sigmoid(gt[1])),
-                         pack_bf16x2(a[2] * fast_sigmoid(gt[2]), a[3] * fast_sigmoid(gt[3]))};
+        o[p] = (u32x2_t){pack_h2<FMT>(a[0] * fast_sigmoid(gt[0]), a[1] * fast_sigmoid(gt[1])),
+                         pack_h2<FMT>(a[2] * fast_sigmoid(gt[2]), a[3] * fast_sigmoid(gt[3]))};
       }
       if (m < M) store_pair16<NOST>(base, ep.ldo, m, g, o[0], o[1], ep.store_mode);
     }
@@ -128,8 +146,8 @@ CFM_DEV void wave_epilogue(f32x4 (&acc)[4][MB], int m0, int nw, int g, int M, co
       for (int j = 0; j < MB; ++j) {
         const int m = m0 + 16 * j;
         const f32x4 v0 = act4<ACT>(acc[2 * p][j]), v1 = act4<ACT>(acc[2 * p + 1][j]);
-        const u32x2_t x = (u32x2_t){pack_bf16x2(v0[0], v0[1]), pack_bf16x2(v0[2], v0[3])};
-        const u32x2_t y = (u32x2_t){pack_bf16x2(v1[0], v1[1]), pack_bf16x2(v1[2], v1[3])};
+        const u32x2_t x = (u32x2_t){pack_h2<FMT>(v0[0], v0[1]), pack_h2<FMT>(v0[2], v0[3])};
+        const u32x2_t y = (u32x2_t){pack_h2<FMT>(v1[0], v1[1]), pack_h2<FMT>(v1[2], v1[3])};
         if (m < M) store_pair16<NOST>(base, ld, m, g, x, y, ep.store_mode);
       }
     }
@@ -139,7 +157,7 @@ CFM_DEV void wave_epilogue(f32x4 (&acc)[4][MB], int m0, int nw, int g, int M, co
 // EPI_STORE through an LDS staging tile (per wave 16 rows x 144 B): each m-block's four 4-column
 // pieces per lane are written with ds_write_b64, read back as full 128-B row pieces (8 rows per
 // read) and stored as whole lines, instead of 16-row x 64-B pieces after permlane swaps.
-template <int ACT>
+template <int ACT, int FMT = 0>
 CFM_DEV void wave_epilogue_fullrow(f32x4 (&acc)[4][8], int row0, int nw, int fr, int g, int lane, int M,
                                    const EpiArgs& ep, unsigned stg) {
   constexpr int PITCH = 144;
@@ -151,7 +169,7 @@ CFM_DEV void wave_epilogue_fullrow(f32x4 (&acc)[4][8], int row0, int nw, int fr,
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const f32x4 v = act4<ACT>(acc[i][j]);
-      asm volatile("ds_write_b64 %0, %1 offset:%2" ::"v"(wr), "v"((u32x2_t){pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3])}),
+      asm volatile("ds_write_b64 %0, %1 offset:%2" ::"v"(wr), "v"((u32x2_t){pack_h2<FMT>(v[0], v[1]), pack_h2<FMT>(v[2], v[3])}),
                    "i"(32 * i) : "memory");
     }
     u32x4 r[2];
@@ -170,10 +188,10 @@ CFM_DEV void wave_epilogue_fullrow(f32x4 (&acc)[4][8], int row0, int nw, int fr,
   }
 }
 
-template <int EPI, int ACT, bool NOST = false>
+template <int EPI, int ACT, bool NOST = false, int FMT = 0>
 CFM_DEV void tile_epilogue(f32x4 (&acc)[4][8], int tm, int tn, int wm, int wn, int fr, int g, int M,
                            const EpiArgs& ep) {
-  wave_epilogue<EPI, ACT, 8, NOST>(acc, tm * 256 + wm * 128 + fr, tn * 256 + wn * 64, g, M, ep);
+  wave_epilogue<EPI, ACT, 8, NOST, FMT>(acc, tm * 256 + wm * 128 + fr, tn * 256 + wn * 64, g, M, ep);
 }
 
 // seed the accumulators of tile (tm, tn) with the bias (every m-block of an n-block gets the same 4 values)

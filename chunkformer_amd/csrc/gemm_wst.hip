@@ -93,8 +93,12 @@ template <int N> CFM_DEV void wst_vmcnt() { asm volatile("s_waitcnt vmcnt(%0)" :
 // AGPRs but copies each one to VGPRs before use).  asm volatile keeps program order with the
 // explicit LDS waits; the VALU <-> MFMA hazards around it are padded by hand (s_nop) where the
 // accumulators are seeded (VALU write -> MFMA srcC) and read back (MFMA write -> VALU read).
+template <int FMT>
 CFM_DEV void mfma_wa(f32x4& acc, const bf16x8& w, const bf16x8& a) {
-  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(acc) : "a"(w), "v"(a));
+  if constexpr (FMT == 1)
+    asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, %0" : "+v"(acc) : "a"(w), "v"(a));
+  else
+    asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(acc) : "a"(w), "v"(a));
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -168,7 +172,7 @@ constexpr int wsp_late_seeds(int s) {
 }
 }  // namespace
 
-template <int EPI, int ACT, int DIAG = 0>
+template <int EPI, int ACT, int DIAG = 0, int FMT = 0>
 __global__ __launch_bounds__(256, 1) void gemm_wsp_kernel(const bf16* __restrict__ A, int lda,
                                                           const bf16* __restrict__ W, int ldw, int M, int N,
                                                           EpiArgs ep) {
@@ -398,7 +402,7 @@ __global__ __launch_bounds__(256, 1) void gemm_wsp_kernel(const bf16* __restrict
         pin(et[o]);
       } else if constexpr (o < H - 2) {
         constexpr int k = o - (H - 4);
-        epk[2 * q + k] = pack_bf16x2(et[2 * k], et[2 * k + 1]);
+        epk[2 * q + k] = pack_h2<FMT>(et[2 * k], et[2 * k + 1]);
         pin(epk[2 * q + k]);
       } else {
         typedef unsigned u32x2_w __attribute__((ext_vector_type(2)));
@@ -417,7 +421,7 @@ __global__ __launch_bounds__(256, 1) void gemm_wsp_kernel(const bf16* __restrict
       } else if constexpr (O < 20) {
         chain(O, gate, lin);
       } else if constexpr (O < 22) {
-        epk[2 * h + O - 20] = pack_bf16x2(et[2 * (O - 20)], et[2 * (O - 20) + 1]);
+        epk[2 * h + O - 20] = pack_h2<FMT>(et[2 * (O - 20)], et[2 * (O - 20) + 1]);
         pin(epk[2 * h + O - 20]);
       } else if constexpr (O < 26) {
         swap(O - 24);
@@ -444,8 +448,8 @@ __global__ __launch_bounds__(256, 1) void gemm_wsp_kernel(const bf16* __restrict
           }
         } else {
           constexpr int k = o - (H - 3);   // pack k of this half: values 2k, 2k+1
-          if constexpr (ACT == ACT_NONE) epk[2 * q + k] = pack_bf16x2(val(2 * k), val(2 * k + 1));
-          else epk[2 * q + k] = pack_bf16x2(et[2 * k], et[2 * k + 1]);
+          if constexpr (ACT == ACT_NONE) epk[2 * q + k] = pack_h2<FMT>(val(2 * k), val(2 * k + 1));
+          else epk[2 * q + k] = pack_h2<FMT>(et[2 * k], et[2 * k + 1]);
           pin(epk[2 * q + k]);
         }
       } else if constexpr (O < 2 * H + 2) {
@@ -484,8 +488,8 @@ __global__ __launch_bounds__(256, 1) void gemm_wsp_kernel(const bf16* __restrict
           }
         } else if constexpr (o < H - 1) {
           constexpr int k = o - (H - 3);   // pack k of this half: values 2k, 2k+1
-          if constexpr (ACT == ACT_NONE) epk[2 * q + k] = pack_bf16x2(val(2 * k), val(2 * k + 1));
-          else epk[2 * q + k] = pack_bf16x2(et[2 * k], et[2 * k + 1]);
+          if constexpr (ACT == ACT_NONE) epk[2 * q + k] = pack_h2<FMT>(val(2 * k), val(2 * k + 1));
+          else epk[2 * q + k] = pack_h2<FMT>(et[2 * k], et[2 * k + 1]);
           pin(epk[2 * q + k]);
         } else {   // o == H - 1: 4 packed columns -> staging tile
           typedef unsigned u32x2_w __attribute__((ext_vector_type(2)));
@@ -527,7 +531,7 @@ __global__ __launch_bounds__(256, 1) void gemm_wsp_kernel(const bf16* __restrict
       sfor<0, 32>([&](auto Ic) {
         constexpr int i = decltype(Ic)::value;
         constexpr int kh = i >> 4, nb = (i >> 2) & 3, mb = i & 3;
-        if constexpr (DIAG != 1) mfma_wa(acc[BUF][nb][mb], wf[nb][2 * KS + kh], cur[mb][kh]);
+        if constexpr (DIAG != 1) mfma_wa<FMT>(acc[BUF][nb][mb], wf[nb][2 * KS + kh], cur[mb][kh]);
         if constexpr (i < 16 && (i & 1) == 0) {
           constexpr int rmb = (i >> 1) & 3, rkh = i >> 3;
           lds_read_into<(slot_n & 7) * WST_SLOT + rmb * 2048>(nxt[rmb][rkh], rdb[slot_n >> 3][rkh]);
@@ -804,7 +808,16 @@ static int launch_wst(const bf16* A, int lda, const bf16* W, int ldw, int M, int
   if (ep.wsp_small_div > 1 && M < ep.wsp_small_rows) n_cu = max(8 * (N >> 8), n_cu / ep.wsp_small_div / 8 * 8);
   // buffer descriptors are built per 64-row tile on 64-bit bases (offsets inside one tile stay
   // below 64 rows x ld), so outputs past 2 GiB (a 980-minute batch's FFN hidden: 3 GB) stay here
-#define WSP_LAUNCH(D) hipLaunchKernelGGL((gemm_wsp_kernel<EPI, ACT, D>), dim3(n_cu), dim3(256), 0, st, A, lda, W, ldw, M, N, ep)
+#define WSP_LAUNCH(D)                                                                                         \
+  do {                                                                                                        \
+    if constexpr (EPI != EPI_DW2) {                                                                           \
+      if (ep.f16) {                                                                                           \
+        hipLaunchKernelGGL((gemm_wsp_kernel<EPI, ACT, D, 1>), dim3(n_cu), dim3(256), 0, st, A, lda, W, ldw, M, N, ep); \
+        break;                                                                                                \
+      }                                                                                                       \
+    }                                                                                                         \
+    hipLaunchKernelGGL((gemm_wsp_kernel<EPI, ACT, D, 0>), dim3(n_cu), dim3(256), 0, st, A, lda, W, ldw, M, N, ep); \
+  } while (0)
 #ifdef CFM_GEMM_DIAG
   // DIAG (timing experiments only, diagnostic builds, model option "gemm_diag"): 1 = no MFMAs,
   // 2 = no DMA wait (stale LDS), 3 = no epilogue (re-seeds only), 4 = no DMA in the loop (stale LDS),
@@ -852,8 +865,8 @@ int gemm_bf16_wst(int epi, int act, const bf16* A, int lda, const bf16* W, int l
     case EPI_GLU:
       if (ep.bias == nullptr) return -1;
       return launch_wst<EPI_GLU, ACT_NONE>(A, lda, W, ldw, M, N, ep, st);
-    case EPI_DW2:   // front-end pw1 + ReLU + dw2 (N = 512, dw2 taps / bias / geometry in ep)
-      if (act != ACT_RELU || N != 512 || !ep.dw_w || !ep.dw_b || ep.t2n < 3 || ep.ldo % 8) return -1;
+    case EPI_DW2:   // front-end pw1 + ReLU + dw2 (N = 512, dw2 taps / bias / geometry in ep; bf16 only)
+      if (ep.f16 || act != ACT_RELU || N != 512 || !ep.dw_w || !ep.dw_b || ep.t2n < 3 || ep.ldo % 8) return -1;
       return launch_wst<EPI_DW2, ACT_RELU>(A, lda, W, ldw, M, N, ep, st);
   }
   return -1;

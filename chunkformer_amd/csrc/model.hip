@@ -416,6 +416,12 @@ struct ModelT : public cfm_model {
             r = full_attention_bf16(w.q, w.kv, kv_rows, w.P + (size_t)l * d, p_rows, Lw.pu, Lw.pv, attd, hh[PH_NWIN],
                                     (hh[PH_TOUT] + 63) / 64, H, dk, hh[PH_TOUT], w.ao, st, p_ld);
         }
+        if constexpr (std::is_same<T, f16>::value) {
+          if (masked && use_ring_attention && dk == 64)
+            r = chunk_attention_masked_f16(w.q, w.kv, kv_rows, w.P + (size_t)l * d, p_rows, Lw.pu, Lw.pv, attd, natt, H, C,
+                                           hh[PH_L] + C + hh[PH_R], w.ao, st, attn_diag, p_ld, tune.attn_reuse,
+                                           tune.attn_min_chunks);
+        }
         if (r == -1)
           r = chunk_attention<T>(w.q, w.kv, kv_rows, w.P + (size_t)l * d, p_rows, Lw.pu, Lw.pv, attd, natt,
                                  H, dk, w.ao, st, p_ld);

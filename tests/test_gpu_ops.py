@@ -1,4 +1,4 @@
-"""Kernel-level GPU parity: the projection GEMM (every epilogue, both tile paths, bf16
+"""Kernel-level GPU parity: the projection GEMM (every epilogue, every tile path, bf16, fp16
 and exact-f32) against a torch fp32 reference of the same op (cfm_op_gemm, include/cfm_ops.h)."""
 import pytest
 import torch
@@ -44,7 +44,14 @@ SHAPES = [(1000, 512, 512), (700, 2048, 512), (513, 512, 2048), (256, 256, 4608)
 # variant bits (include/cfm_ops.h): 1 = 128x128 tiles; 7 << 18 = K = 512 weight-stationary kernel off
 # (the 256 x 256 kernel takes its shapes); 2 << 16 = nt stores; 1 << 21 = the N = 512, K >= 1024 shapes on the
 # full-row 128 x 512 kernel (gemm_rowln.hip) instead of 256 x 256 tiles
-MODES = [("bf16", 0), ("bf16", 1), ("fp32", 0), ("bf16", 7 << 18), ("bf16", 2 << 16), ("bf16", 1 << 21)]
+MODES = [("bf16", 0), ("bf16", 1), ("fp32", 0), ("bf16", 7 << 18), ("bf16", 2 << 16), ("bf16", 1 << 21),
+         ("fp16", 0), ("fp16", 1), ("fp16", 7 << 18)]   # fp16: the same kernels on f16 MFMA (EpiArgs::f16)
+
+
+def _dt(L, dt):
+    """(torch dtype, cfm_dtype code, max-error tolerance relative to the output scale)"""
+    return {"bf16": (torch.bfloat16, L.DTYPE_BF16, 1e-2), "fp16": (torch.float16, L.DTYPE_F16, 2e-3),
+            "fp32": (torch.float32, L.DTYPE_F32, 1e-5)}[dt]
 
 
 @pytest.mark.parametrize("M,N,K", SHAPES)
@@ -52,16 +59,16 @@ MODES = [("bf16", 0), ("bf16", 1), ("fp32", 0), ("bf16", 7 << 18), ("bf16", 2 <<
 @pytest.mark.parametrize("act", [0, 1, 2])
 def test_gemm_store(L, M, N, K, mode, act):
     dt, small = mode
-    tdt = torch.bfloat16 if dt == "bf16" else torch.float32
+    tdt, code, tol = _dt(L, dt)
     g = torch.Generator(device="cuda").manual_seed(M + N + K)
     A = (torch.randn(M, K, device="cuda", generator=g) * 0.5).to(tdt)
     W = (torch.randn(N, K, device="cuda", generator=g) / K ** 0.5).to(tdt)
     bias = torch.randn(N, device="cuda", generator=g)
     out = torch.full((M + 3, N), float("nan"), device="cuda", dtype=tdt)
-    _run(L, L.DTYPE_BF16 if dt == "bf16" else L.DTYPE_F32, 0, act, A, W, bias, out=out, ldo=N, row_off=3, small=small)
+    _run(L, code, 0, act, A, W, bias, out=out, ldo=N, row_off=3, small=small)
     r = _ref(A, W, bias)
     r = torch.relu(r) if act == 1 else (torch.nn.functional.silu(r) if act == 2 else r)
-    _close(out[3:], r, 1e-2 if dt == "bf16" else 1e-5)
+    _close(out[3:], r, tol)
     assert torch.isnan(out[:3].float()).all()
 
 
@@ -78,8 +85,7 @@ def test_gemm_no_bias(L, M, N, K):
 @pytest.mark.parametrize("mode", MODES)
 def test_gemm_store_f32_and_resid(L, mode):
     dt, small = mode
-    tdt = torch.bfloat16 if dt == "bf16" else torch.float32
-    code = L.DTYPE_BF16 if dt == "bf16" else L.DTYPE_F32
+    tdt, code, _ = _dt(L, dt)
     M, N, K = 777, 512, 4608
     g = torch.Generator(device="cuda").manual_seed(5)
     A = (torch.randn(M, K, device="cuda", generator=g) * 0.5).to(tdt)
@@ -87,20 +93,19 @@ def test_gemm_store_f32_and_resid(L, mode):
     bias = torch.randn(N, device="cuda", generator=g)
     out = torch.empty(M, N, device="cuda")
     _run(L, code, 1, 0, A, W, bias, alpha=22.627, out=out, ldo=N, small=small)
-    _close(out, 22.627 * _ref(A, W, bias), 1e-3 if dt == "bf16" else 1e-5)
+    _close(out, 22.627 * _ref(A, W, bias), 1e-5 if dt == "fp32" else 1e-3)
     x0 = torch.randn(M, N, device="cuda", generator=g)
     x = x0.clone()
     rm = (torch.rand(M, device="cuda", generator=g) > 0.3).to(torch.uint8)
     _run(L, code, 2, 0, A, W, bias, alpha=0.5, x=x, rowmask=rm, small=small)
-    _close(x, x0 + 0.5 * _ref(A, W, bias) * rm.float()[:, None], 1e-3 if dt == "bf16" else 1e-5)
+    _close(x, x0 + 0.5 * _ref(A, W, bias) * rm.float()[:, None], 1e-5 if dt == "fp32" else 1e-3)
 
 
 @pytest.mark.parametrize("mode", MODES)
 @pytest.mark.parametrize("M", [900, 40000])   # 40000 rows: the K = 512 weight-in-registers kernel
 def test_gemm_qkv_and_glu(L, mode, M):
     dt, small = mode
-    tdt = torch.bfloat16 if dt == "bf16" else torch.float32
-    code = L.DTYPE_BF16 if dt == "bf16" else L.DTYPE_F32
+    tdt, code, tol = _dt(L, dt)
     d, Lc = 512, 5
     g = torch.Generator(device="cuda").manual_seed(9)
     A = (torch.randn(M, d, device="cuda", generator=g) * 0.5).to(tdt)
@@ -110,7 +115,6 @@ def test_gemm_qkv_and_glu(L, mode, M):
     kv = torch.zeros(M + Lc + 2, 2 * d, device="cuda", dtype=tdt)
     _run(L, code, 3, 0, A, W, bias, out=q, out2=kv, row_off=Lc, d=d, small=small)
     r = _ref(A, W, bias)
-    tol = 1e-2 if dt == "bf16" else 1e-5
     _close(q, r[:, :d], tol)
     kvr = kv[Lc: Lc + M].view(M, d // 64, 2, 64)
     _close(kvr[:, :, 0].reshape(M, d), r[:, d: 2 * d], tol)
