@@ -14,7 +14,10 @@ namespace cfm {
 int cu_count();
 
 enum { EPI_STORE = 0, EPI_STORE_F32 = 1, EPI_RESID = 2, EPI_QKV = 3, EPI_GLU = 4, EPI_DW2 = 5 };
-enum { ACT_NONE = 0, ACT_RELU = 1, ACT_SILU = 2 };
+// ACT_SILU_L2E: the accumulator holds a = -log2(e) z (weights and bias pre-scaled at model build), and the
+// output is a / (1 + 2^a) = -log2(e) silu(z) (the next GEMM's weights carry the -1 / log2(e)): one multiply per
+// value less in the epilogue.  With EPI_GLU it marks the gate half as pre-scaled: out = lin / (1 + 2^gate)
+enum { ACT_NONE = 0, ACT_RELU = 1, ACT_SILU = 2, ACT_SILU_L2E = 3 };
 
 struct EpiArgs {
   const float* bias = nullptr;   // [N] f32 or null

@@ -145,7 +145,8 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const T* __restrict__ A, i
           const int row = rbase + i * 16 + r;
           if (row < M) {
             const float a = acc[i][j][r] + ba, gt = acc[i][j + 1][r] + bg;
-            out[(size_t)(row + ep.row_off) * ep.ldo + ch] = from_f32<T>(a * sigmoid_f(gt));
+            const float sg = ACT == ACT_SILU_L2E ? 1.f / (1.f + exp2f(gt)) : sigmoid_f(gt);
+            out[(size_t)(row + ep.row_off) * ep.ldo + ch] = from_f32<T>(a * sg);
           }
         }
     }
@@ -165,6 +166,7 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const T* __restrict__ A, i
           if constexpr (EPI == EPI_STORE) {
             if constexpr (ACT == ACT_RELU) v = fmaxf(v, 0.f);
             if constexpr (ACT == ACT_SILU) v = silu_f(v);
+            if constexpr (ACT == ACT_SILU_L2E) v = v / (1.f + exp2f(v));
             reinterpret_cast<T*>(ep.out)[(size_t)(row + ep.row_off) * ep.ldo + col] = from_f32<T>(v);
           } else if constexpr (EPI == EPI_STORE_F32) {
             reinterpret_cast<float*>(ep.out)[(size_t)(row + ep.row_off) * ep.ldo + col] = ep.alpha * v;
@@ -217,11 +219,14 @@ int gemm(int epi, int act, const T* A, int lda, const T* W, int ldw, int M, int 
     case EPI_STORE:
       if (act == ACT_RELU) return launch<T, EPI_STORE, ACT_RELU>(A, lda, W, ldw, M, N, K, ep, st);
       if (act == ACT_SILU) return launch<T, EPI_STORE, ACT_SILU>(A, lda, W, ldw, M, N, K, ep, st);
+      if (act == ACT_SILU_L2E) return launch<T, EPI_STORE, ACT_SILU_L2E>(A, lda, W, ldw, M, N, K, ep, st);
       return launch<T, EPI_STORE, ACT_NONE>(A, lda, W, ldw, M, N, K, ep, st);
     case EPI_STORE_F32: return launch<T, EPI_STORE_F32, ACT_NONE>(A, lda, W, ldw, M, N, K, ep, st);
     case EPI_RESID: return launch<T, EPI_RESID, ACT_NONE>(A, lda, W, ldw, M, N, K, ep, st);
     case EPI_QKV: return launch<T, EPI_QKV, ACT_NONE>(A, lda, W, ldw, M, N, K, ep, st);
-    case EPI_GLU: return launch<T, EPI_GLU, ACT_NONE>(A, lda, W, ldw, M, N, K, ep, st);
+    case EPI_GLU:
+      if (act == ACT_SILU_L2E) return launch<T, EPI_GLU, ACT_SILU_L2E>(A, lda, W, ldw, M, N, K, ep, st);
+      return launch<T, EPI_GLU, ACT_NONE>(A, lda, W, ldw, M, N, K, ep, st);
   }
   return (int)hipErrorInvalidValue;
 }

@@ -276,11 +276,14 @@ int gemm_bf16_big(int epi, int act, const bf16* A, int lda, const bf16* W, int l
     case EPI_STORE:
       if (act == ACT_RELU) return launch256<EPI_STORE, ACT_RELU>(A, lda, W, ldw, M, N, K, ep, st);
       if (act == ACT_SILU) return launch256<EPI_STORE, ACT_SILU>(A, lda, W, ldw, M, N, K, ep, st);
+      if (act == ACT_SILU_L2E) return launch256<EPI_STORE, ACT_SILU_L2E>(A, lda, W, ldw, M, N, K, ep, st);
       return launch256<EPI_STORE, ACT_NONE>(A, lda, W, ldw, M, N, K, ep, st);
     case EPI_STORE_F32: return launch256<EPI_STORE_F32, ACT_NONE>(A, lda, W, ldw, M, N, K, ep, st);
     case EPI_RESID: return launch256<EPI_RESID, ACT_NONE>(A, lda, W, ldw, M, N, K, ep, st);
     case EPI_QKV: return launch256<EPI_QKV, ACT_NONE>(A, lda, W, ldw, M, N, K, ep, st);
-    case EPI_GLU: return launch256<EPI_GLU, ACT_NONE>(A, lda, W, ldw, M, N, K, ep, st);
+    case EPI_GLU:
+      if (act == ACT_SILU_L2E) return launch256<EPI_GLU, ACT_SILU_L2E>(A, lda, W, ldw, M, N, K, ep, st);
+      return launch256<EPI_GLU, ACT_NONE>(A, lda, W, ldw, M, N, K, ep, st);
   }
   return -1;
 }

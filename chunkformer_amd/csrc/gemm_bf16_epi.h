@@ -63,6 +63,10 @@ CFM_DEV f32x4 act4(f32x4 v) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) v[r] = fast_silu(v[r]);
   }
+  if constexpr (ACT == ACT_SILU_L2E) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = v[r] * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(v[r]));
+  }
   return v;
 }
 // store two packed 16-column blocks (x = block 0, y = block 1) of row `row` after the swap
@@ -117,8 +121,12 @@ CFM_DEV void wave_epilogue(f32x4 (&acc)[4][MB], int m0, int nw, int g, int M, co
 #pragma unroll
       for (int p = 0; p < 2; ++p) {
         const f32x4 a = acc[2 * p][j], gt = acc[2 * p + 1][j];
-        o[p] = (u32x2_t){pack_h2<FMT>(a[0] * fast_sigmoid(gt[0]), a[1] * fast_sigmoid(gt[1])),
-                         pack_h2<FMT>(a[2] * fast_sigmoid(gt[2]), a[3] * fast_sigmoid(gt[3]))};
+        auto sg = [](float x) {   // sigmoid of the gate (pre-scaled by -log2(e) with ACT_SILU_L2E)
+          if constexpr (ACT == ACT_SILU_L2E) return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(x));
+          else return fast_sigmoid(x);
+        };
+        o[p] = (u32x2_t){pack_h2<FMT>(a[0] * sg(gt[0]), a[1] * sg(gt[1])),
+                         pack_h2<FMT>(a[2] * sg(gt[2]), a[3] * sg(gt[3]))};
       }
       if (m < M) store_pair16<NOST>(base, ep.ldo, m, g, o[0], o[1], ep.store_mode);
     }

@@ -132,7 +132,11 @@ namespace {
 // GLU: group s = (m-block s/2, channel half s%1): 20 sigmoid-gate ops + 2 packs (+ swaps and the
 // store on odd s), 2 re-seeds.
 template <int ACT>
-constexpr int wsp_half() { return (ACT == ACT_SILU ? 20 : ACT == ACT_RELU ? 4 : 0) + 2; }
+constexpr int wsp_half() { return (ACT == ACT_SILU ? 20 : ACT == ACT_SILU_L2E ? 16 : ACT == ACT_RELU ? 4 : 0) + 2; }
+// GLU: gate-chain ops per group (4 values x 5 steps, or x 4 with the gate pre-scaled by -log2(e)); then
+// 2 packs, 2 re-seeds, 2 swaps and (odd groups) the store
+template <int ACT>
+constexpr int glu_chain() { return ACT == ACT_SILU_L2E ? 16 : 20; }
 // Full-row stores (non-GLU, WSP_FULLROW): per half q the activation ops, 2 packs, one ds_write_b64
 // of the 4 packed columns into the wave's 16 x 64 staging tile, the re-seed; an odd group then
 // reads the tile back as full 128-B rows (2 x ds_read_b128: rows 0-7, 8-15) and the next (even)
@@ -149,7 +153,8 @@ constexpr bool wsp_fullrow() {
 template <int EPI, int ACT>
 constexpr int wsp_nops(int s) {
   return EPI == EPI_DW2 ? 2 * (wsp_half<ACT>() + 2)
-         : EPI == EPI_GLU ? ((s & 1) ? 27 : 24) : wsp_fullrow<EPI, ACT>() ? 2 * wsp_half<ACT>() + 6 : 2 * wsp_half<ACT>() + 5;
+         : EPI == EPI_GLU ? glu_chain<ACT>() + ((s & 1) ? 7 : 4)
+         : wsp_fullrow<EPI, ACT>() ? 2 * wsp_half<ACT>() + 6 : 2 * wsp_half<ACT>() + 5;
 }
 constexpr int wsp_lo(int i, int n) { return (i * n + 31) / 32; }   // first op of gap i
 constexpr int wsp_gap(int o, int n) {                                  // gap that carries op o
@@ -166,8 +171,9 @@ constexpr int wsp_late_seeds(int s) {
   // full-row: even groups open with the 2 deferred stores (seeds at 2 + H, 2H + 3); odd groups
   // end with the 2 row reads and then both seeds (2H + 2, 2H + 3)
   const bool fr = wsp_fullrow<EPI, ACT>();
-  const int o0 = EPI == EPI_DW2 ? H : EPI == EPI_GLU ? 22 : fr ? ((s & 1) ? 2 * H + 2 : H + 2) : H - 1;
-  const int o1 = EPI == EPI_DW2 ? 2 * H + 1 : EPI == EPI_GLU ? 23 : fr ? 2 * H + 3 : 2 * H - 1;
+  const int G = glu_chain<ACT>();
+  const int o0 = EPI == EPI_DW2 ? H : EPI == EPI_GLU ? G + 2 : fr ? ((s & 1) ? 2 * H + 2 : H + 2) : H - 1;
+  const int o1 = EPI == EPI_DW2 ? 2 * H + 1 : EPI == EPI_GLU ? G + 3 : fr ? 2 * H + 3 : 2 * H - 1;
   return (wsp_gap(o0, n) >= 14) + (wsp_gap(o1, n) >= 14);
 }
 }  // namespace
@@ -379,13 +385,21 @@ __global__ __launch_bounds__(256, 1) void gemm_wsp_kernel(const bf16* __restrict
       if constexpr (RESEED) lds_read_into<nb * 64>(a[nb][jj], bias_lds);
     };
     // sigmoid-style chain on 4 values: t = x * -log2e; t = 2^t; t += 1; t = 1 / t; t = y * t
+    // (ACT_SILU_L2E: x arrives pre-scaled by -log2e, the first step is t = 2^x)
     auto chain = [&](int o, auto xf, auto yf) {
       const int i = o & 3;
-      if (o < 4) et[i] = xf(i) * NL2E;
-      else if (o < 8) et[i] = __builtin_amdgcn_exp2f(et[i]);
-      else if (o < 12) et[i] = et[i] + 1.f;
-      else if (o < 16) et[i] = __builtin_amdgcn_rcpf(et[i]);
-      else et[i] = yf(i) * et[i];
+      if constexpr (ACT == ACT_SILU_L2E) {
+        if (o < 4) et[i] = __builtin_amdgcn_exp2f(xf(i));
+        else if (o < 8) et[i] = et[i] + 1.f;
+        else if (o < 12) et[i] = __builtin_amdgcn_rcpf(et[i]);
+        else et[i] = yf(i) * et[i];
+      } else {
+        if (o < 4) et[i] = xf(i) * NL2E;
+        else if (o < 8) et[i] = __builtin_amdgcn_exp2f(et[i]);
+        else if (o < 12) et[i] = et[i] + 1.f;
+        else if (o < 16) et[i] = __builtin_amdgcn_rcpf(et[i]);
+        else et[i] = yf(i) * et[i];
+      }
       pin(et[i]);
     };
     if constexpr (EPI == EPI_DW2) {
@@ -410,22 +424,22 @@ __global__ __launch_bounds__(256, 1) void gemm_wsp_kernel(const bf16* __restrict
                      "i"(SL * 64 * DW2_RP + jj * 16 * DW2_RP + 64 * p + 32 * q) : "memory");
       }
     } else if constexpr (EPI == EPI_GLU) {
-      // ops 0-19 gate chain, 20-21 packs, 22-23 re-seeds (both accumulators are dead after op 19),
-      // then on odd S the 2 swaps and the store
-      constexpr int jj = S >> 1, h = S & 1;
+      // ops 0 .. G-1 gate chain, G, G+1 packs, G+2, G+3 re-seeds (both accumulators are dead after
+      // op G-1), then on odd S the 2 swaps and the store
+      constexpr int jj = S >> 1, h = S & 1, G = glu_chain<ACT>();
       auto gate = [&](int i) -> float { return a[2 * h + 1][jj][i]; };
       auto lin = [&](int i) -> float { return a[2 * h][jj][i]; };
-      if constexpr (O == 22 || O == 23) {
-        seed(std::integral_constant<int, 2 * h + (O - 22)>{}, jj);
+      if constexpr (O == G + 2 || O == G + 3) {
+        seed(std::integral_constant<int, 2 * h + (O - G - 2)>{}, jj);
       } else if constexpr (DIAG == 3) {
-      } else if constexpr (O < 20) {
+      } else if constexpr (O < G) {
         chain(O, gate, lin);
-      } else if constexpr (O < 22) {
-        epk[2 * h + O - 20] = pack_h2<FMT>(et[2 * (O - 20)], et[2 * (O - 20) + 1]);
-        pin(epk[2 * h + O - 20]);
-      } else if constexpr (O < 26) {
-        swap(O - 24);
-      } else {   // O == 26
+      } else if constexpr (O < G + 2) {
+        epk[2 * h + O - G] = pack_h2<FMT>(et[2 * (O - G)], et[2 * (O - G) + 1]);
+        pin(epk[2 * h + O - G]);
+      } else if constexpr (O < G + 6) {
+        swap(O - G - 4);
+      } else {   // O == G + 6
         store(0, jj);
       }
     } else if constexpr (!wsp_fullrow<EPI, ACT>()) {
@@ -440,7 +454,7 @@ __global__ __launch_bounds__(256, 1) void gemm_wsp_kernel(const bf16* __restrict
         constexpr int q = O / H, o = O % H;
         auto val = [&](int i) -> float { return a[2 * p + q][jj][i]; };
         if constexpr (o < H - 3) {
-          if constexpr (ACT == ACT_SILU) {
+          if constexpr (ACT == ACT_SILU || ACT == ACT_SILU_L2E) {
             chain(o, val, val);
           } else {
             et[o] = fmaxf(val(o), 0.f);
@@ -480,7 +494,7 @@ __global__ __launch_bounds__(256, 1) void gemm_wsp_kernel(const bf16* __restrict
           seed(std::integral_constant<int, 2 * p + q>{}, jj);
         } else if constexpr (DIAG == 3) {
         } else if constexpr (o < H - 3) {
-          if constexpr (ACT == ACT_SILU) {
+          if constexpr (ACT == ACT_SILU || ACT == ACT_SILU_L2E) {
             chain(o, val, val);
           } else {
             et[o] = fmaxf(val(o), 0.f);
@@ -860,10 +874,12 @@ int gemm_bf16_wst(int epi, int act, const bf16* A, int lda, const bf16* W, int l
     case EPI_STORE:
       if (act == ACT_RELU) return launch_wst<EPI_STORE, ACT_RELU>(A, lda, W, ldw, M, N, ep, st);
       if (act == ACT_SILU) return launch_wst<EPI_STORE, ACT_SILU>(A, lda, W, ldw, M, N, ep, st);
+      if (act == ACT_SILU_L2E) return launch_wst<EPI_STORE, ACT_SILU_L2E>(A, lda, W, ldw, M, N, ep, st);
       return launch_wst<EPI_STORE, ACT_NONE>(A, lda, W, ldw, M, N, ep, st);
     case EPI_QKV: return launch_wst<EPI_QKV, ACT_NONE>(A, lda, W, ldw, M, N, ep, st);
     case EPI_GLU:
       if (ep.bias == nullptr) return -1;
+      if (act == ACT_SILU_L2E) return launch_wst<EPI_GLU, ACT_SILU_L2E>(A, lda, W, ldw, M, N, ep, st);
       return launch_wst<EPI_GLU, ACT_NONE>(A, lda, W, ldw, M, N, ep, st);
     case EPI_DW2:   // front-end pw1 + ReLU + dw2 (N = 512, dw2 taps / bias / geometry in ep; bf16 only)
       if (ep.f16 || act != ACT_RELU || N != 512 || !ep.dw_w || !ep.dw_b || ep.t2n < 3 || ep.ldo % 8) return -1;

@@ -171,6 +171,15 @@ struct cfm_model {
 
 namespace cfm {
 
+// 16-bit modes run the FFN SiLU and the conv module's GLU on -log2(e)-prescaled accumulators (ACT_SILU_L2E,
+// cfm_kernels.h): the weights are scaled once in build_model
+#ifndef CFM_SILU_PRE
+#define CFM_SILU_PRE 1   // 0: the plain SiLU / GLU epilogues in the 16-bit modes too (A/B builds)
+#endif
+template <typename T> constexpr bool kSiluPre = CFM_SILU_PRE && sizeof(T) == 2;
+template <typename T> constexpr int kActSilu = kSiluPre<T> ? ACT_SILU_L2E : ACT_SILU;
+constexpr float kLog2e = 1.4426950408889634f;
+
 template <typename T>
 struct ModelT : public cfm_model {
   // front-end window group size: bounds the [G, T2, 19, d] intermediates to 768 MiB each (measured:
@@ -343,7 +352,7 @@ struct ModelT : public cfm_model {
     // y = w2 . SiLU(w1 . h + b1) + b2: two GEMMs through w.hid
     auto ffn = [&](const void* w1, const float* b1, const void* w2, const float* b2, T* yout) -> cfm_status {
       { EpiArgs e = E(SITE_FFN1); e.bias = b1; e.out = w.hid; e.ldo = ff;
-        PROF(PC_FFN1, gemm<T>(EPI_STORE, ACT_SILU, w.h, d, (const T*)w1, d, rows, ff, d, e, st)); }
+        PROF(PC_FFN1, gemm<T>(EPI_STORE, kActSilu<T>, w.h, d, (const T*)w1, d, rows, ff, d, e, st)); }
       { EpiArgs e = E(SITE_FFN2); e.bias = b2; e.out = yout; e.ldo = d;
         PROF(PC_FFN2, gemm<T>(EPI_STORE, ACT_NONE, w.hid, ff, (const T*)w2, ff, rows, d, ff, e, st)); }
       return CFM_OK;
@@ -370,7 +379,7 @@ struct ModelT : public cfm_model {
       const LayerW& Lw = layers[l];
       if (fused) {   // macaron FFN: w1 + SiLU, then w2 -> y_mac, h = LN_mha(x + 0.5 y_mac)
         { EpiArgs e = E(SITE_FFN1); e.bias = Lw.b_ff1m; e.out = w.hid; e.ldo = ff;
-          PROF(PC_FFN1, gemm<T>(EPI_STORE, ACT_SILU, w.h, d, (const T*)Lw.ff1m, d, rows, ff, d, e, st)); }
+          PROF(PC_FFN1, gemm<T>(EPI_STORE, kActSilu<T>, w.h, d, (const T*)Lw.ff1m, d, rows, ff, d, e, st)); }
         RowLnArgs a = ln_args(Lw.b_ff2m, 0.5f, Lw.ln_mha_w, Lw.ln_mha_b);
         if constexpr (std::is_same<T, bf16>::value) a.y_out = w.y;
         if (rowln(PC_FFN2, w.hid, ff, Lw.ff2m, a) < 0) return set_error(CFM_ERR_RUNTIME, "fused FFN w2 not eligible");
@@ -443,7 +452,7 @@ struct ModelT : public cfm_model {
       }
       if (cci) PROF(PC_CACHE, cnn_cache_in<T>(cci + l * cnn_ls, d, 7, w.glu, st));
       { EpiArgs e = E(SITE_PW1); e.bias = Lw.b_pw1; e.out = w.glu; e.ldo = d; e.row_off = gluoff;
-        PROF(PC_PW1, gemm<T>(EPI_GLU, ACT_NONE, w.h, d, (const T*)Lw.pw1, d, rows, 2 * d, d, e, st)); }
+        PROF(PC_PW1, gemm<T>(EPI_GLU, kSiluPre<T> ? ACT_SILU_L2E : ACT_NONE, w.h, d, (const T*)Lw.pw1, d, rows, 2 * d, d, e, st)); }
       if (cci && cco) PROF(PC_CACHE, cnn_cache_out<T>(w.glu, cache_start, d, 7, cco + l * cnn_ls, st));
       PROF(PC_CONV, conv_dw_ln_silu<T>(w.glu, convd, nconv, d, Lw.dw_t, Lw.b_dw, Lw.cn_w, Lw.cn_b, eps, w.cv, st,
                                         tune.conv_dot2, tune.conv_dma));
@@ -454,7 +463,7 @@ struct ModelT : public cfm_model {
         if (rowln(PC_PW2, w.cv, d, Lw.pw2, a) < 0) return set_error(CFM_ERR_RUNTIME, "fused pointwise_conv2 not eligible");
         // FFN: w1 + SiLU, then w2: x = LN_fin(x + y_conv + 0.5 y_ffn), h = next LN_ffm (or after_norm -> out)
         { EpiArgs e = E(SITE_FFN1); e.bias = Lw.b_ff1; e.out = w.hid; e.ldo = ff;
-          PROF(PC_FFN1, gemm<T>(EPI_STORE, ACT_SILU, w.h, d, (const T*)Lw.ff1, d, rows, ff, d, e, st)); }
+          PROF(PC_FFN1, gemm<T>(EPI_STORE, kActSilu<T>, w.h, d, (const T*)Lw.ff1, d, rows, ff, d, e, st)); }
         RowLnArgs f = ln_args(Lw.b_ff2, 0.5f, Lw.ln_fin_w, Lw.ln_fin_b);
         f.y1 = reinterpret_cast<const bf16*>(w.y); f.a1 = 1.f; f.y1mask = rmask;
         f.ybuf = reinterpret_cast<bf16*>(w.y2);
@@ -673,13 +682,17 @@ static cfm_status build_model(const cfm_config& cfg, const HostW& hw, int device
     for (int l = 0; l < nb; ++l) {
       LayerW& Lw = M->layers[l];
       const std::string p = E + "encoders." + std::to_string(l) + ".";
-      put_T(vec(p + "feed_forward_macaron.w_1.weight", (int64_t)ff * d), &Lw.ff1m);
-      put_f32(hw.get(p + "feed_forward_macaron.w_1.bias", ff), ff, &Lw.b_ff1m);
-      put_T(vec(p + "feed_forward_macaron.w_2.weight", (int64_t)d * ff), &Lw.ff2m);
+      // 16-bit modes (ACT_SILU_L2E): w_1 and its bias x -log2(e), w_2 x -1/log2(e), so the SiLU epilogue
+      // skips its input multiply; the product w_2 . silu(w_1 h + b_1) is unchanged
+      auto scaled = [](std::vector<float> v, float f) { for (float& x : v) x *= f; return v; };
+      const float s1 = kSiluPre<T> ? -kLog2e : 1.f, s2 = kSiluPre<T> ? -1.f / kLog2e : 1.f;
+      put_T(scaled(vec(p + "feed_forward_macaron.w_1.weight", (int64_t)ff * d), s1), &Lw.ff1m);
+      { const auto b = scaled(vec(p + "feed_forward_macaron.w_1.bias", ff), s1); put_f32(b.data(), b.size(), &Lw.b_ff1m); }
+      put_T(scaled(vec(p + "feed_forward_macaron.w_2.weight", (int64_t)d * ff), s2), &Lw.ff2m);
       put_f32(hw.get(p + "feed_forward_macaron.w_2.bias", d), d, &Lw.b_ff2m);
-      put_T(vec(p + "feed_forward.w_1.weight", (int64_t)ff * d), &Lw.ff1);
-      put_f32(hw.get(p + "feed_forward.w_1.bias", ff), ff, &Lw.b_ff1);
-      put_T(vec(p + "feed_forward.w_2.weight", (int64_t)d * ff), &Lw.ff2);
+      put_T(scaled(vec(p + "feed_forward.w_1.weight", (int64_t)ff * d), s1), &Lw.ff1);
+      { const auto b = scaled(vec(p + "feed_forward.w_1.bias", ff), s1); put_f32(b.data(), b.size(), &Lw.b_ff1); }
+      put_T(scaled(vec(p + "feed_forward.w_2.weight", (int64_t)d * ff), s2), &Lw.ff2);
       put_f32(hw.get(p + "feed_forward.w_2.bias", d), d, &Lw.b_ff2);
       {
         std::vector<float> w, b;
@@ -701,13 +714,15 @@ static cfm_status build_model(const cfm_config& cfg, const HostW& hw, int device
         const float* s = hw.get(p + "conv_module.pointwise_conv1.weight", (int64_t)2 * d * d);
         const float* sb = hw.get(p + "conv_module.pointwise_conv1.bias", 2 * d);
         std::vector<float> w((size_t)2 * d * d), b(2 * d);
+        // 16-bit modes: the gate rows and bias x -log2(e) (EPI_GLU with ACT_SILU_L2E)
+        const float sg = kSiluPre<T> ? -kLog2e : 1.f;
         for (int t = 0; t < d / 16; ++t)
           for (int r = 0; r < 16; ++r) {
             const int ra = 16 * t + r, rg = d + 16 * t + r;
             std::memcpy(&w[(size_t)(32 * t + r) * d], s + (size_t)ra * d, 4 * d);
-            std::memcpy(&w[(size_t)(32 * t + 16 + r) * d], s + (size_t)rg * d, 4 * d);
+            for (int k = 0; k < d; ++k) w[(size_t)(32 * t + 16 + r) * d + k] = sg * s[(size_t)rg * d + k];
             b[32 * t + r] = sb[ra];
-            b[32 * t + 16 + r] = sb[rg];
+            b[32 * t + 16 + r] = sg * sb[rg];
           }
         put_T(w, &Lw.pw1);
         put_f32(b.data(), b.size(), &Lw.b_pw1);

@@ -56,7 +56,7 @@ def _dt(L, dt):
 
 @pytest.mark.parametrize("M,N,K", SHAPES)
 @pytest.mark.parametrize("mode", MODES)
-@pytest.mark.parametrize("act", [0, 1, 2])
+@pytest.mark.parametrize("act", [0, 1, 2, 3])   # 3: SiLU on a -log2(e)-prescaled input (a / (1 + 2^a))
 def test_gemm_store(L, M, N, K, mode, act):
     dt, small = mode
     tdt, code, tol = _dt(L, dt)
@@ -68,6 +68,8 @@ def test_gemm_store(L, M, N, K, mode, act):
     _run(L, code, 0, act, A, W, bias, out=out, ldo=N, row_off=3, small=small)
     r = _ref(A, W, bias)
     r = torch.relu(r) if act == 1 else (torch.nn.functional.silu(r) if act == 2 else r)
+    if act == 3:
+        r = r / (1 + torch.exp2(r))
     _close(out[3:], r, tol)
     assert torch.isnan(out[:3].float()).all()
 
@@ -132,6 +134,9 @@ def test_gemm_qkv_and_glu(L, mode, M):
     _run(L, code, 4, 0, A, W1[perm].contiguous(), b1[perm].contiguous(), out=out, ldo=d, row_off=7, small=small)
     r = _ref(A, W1, b1)
     _close(out[7:], r[:, :d] * torch.sigmoid(r[:, d:]), tol)
+    # act 3: the gate half arrives pre-scaled by -log2(e) (the model's 16-bit weights): lin / (1 + 2^gate)
+    _run(L, code, 4, 3, A, W1[perm].contiguous(), b1[perm].contiguous(), out=out, ldo=d, row_off=7, small=small)
+    _close(out[7:], r[:, :d] / (1 + torch.exp2(r[:, d:])), tol)
 
 
 
