@@ -19,6 +19,10 @@ CLASSES = [
     ("gemm_bf16_256_kernel<0, 1,", "frontend_pw_gemm"),
     ("gemm_bf16_256_kernel<0, 0,", "plain_gemm_k2048+ (ffn_w2 / frontend out)"),
     ("gemm_wsp_kernel<0, 2,", "ffn_w1_gemm"), ("gemm_wsp_kernelILi0ELi2E", "ffn_w1_gemm"),
+    # ACT_SILU_L2E (3): the 16-bit modes' FFN w1 and (with EPI_GLU = 4) the conv module's pw1
+    ("gemm_wsp_kernel<0, 3,", "ffn_w1_gemm"), ("gemm_wsp_kernelILi0ELi3E", "ffn_w1_gemm"),
+    ("gemm_bf16_256_kernel<0, 3,", "ffn_w1_gemm"), ("gemm_bf16_256_kernelILi0ELi3E", "ffn_w1_gemm"),
+    ("gemm_wsp_kernel<4, 3,", "pw1_glu_gemm"), ("gemm_bf16_256_kernel<4, 3,", "pw1_glu_gemm"),
     ("gemm_wsp_kernel<5, 1,", "frontend_pw1_dw2 (fused)"), ("gemm_wsp_kernelILi5ELi1E", "frontend_pw1_dw2 (fused)"),
     ("gemm_wsp_kernel<0, 1,", "frontend_pw_gemm"), ("gemm_wsp_kernel<3, 0,", "qkv_gemm"),
     ("gemm_wsp_kernel<4, 0,", "pw1_glu_gemm"), ("gemm_wsp_kernel<0, 0,", "plain_gemm_k512 (out_proj / pw2)"),
