@@ -235,6 +235,10 @@ template <typename T>
 int cnn_cache_in(const float* cache /*[d][7]*/, int d, int lorder, T* glu, hipStream_t st);
 template <typename T>
 int cnn_cache_out(const T* glu, int start_row, int d, int lorder, float* cache, hipStream_t st);
+// both caches of a layer in one launch (attention: flat rows, or head-major when hl; conv: optional)
+template <typename T>
+int cache_io(bool in, bool hl, float* acache, int H, int L, int dk, T* kv, float* ccache, int d, int lorder, T* glu,
+             hipStream_t st);
 int masks_from_plan(const int32_t* meta, int n, int C, int L, int R, uint8_t* att, uint8_t* pad, hipStream_t st);
 // CTC head (ctc.hip): ids-only argmax of enc . W^T + b without a logit tensor (bf16 W with rows padded
 // to a multiple of 64, d = 512; -1 = not eligible), and the collapse / silence segmentation of ids

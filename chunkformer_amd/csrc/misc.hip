@@ -122,6 +122,48 @@ int cnn_cache_out(const T* glu, int start_row, int d, int lorder, float* cache, 
   return 0;
 }
 
+// Both caches of one layer in ONE launch (endless_decode's / forward_chunk's per-layer cache traffic: four
+// 5-us launches per layer on the segment pipeline's critical path otherwise).  Blocks [0, na) copy the
+// attention cache (flat [L][2d] rows, or head-major [H][L][2dk] when HL), the rest the conv cache
+// ([d][lorder] channel-major <-> GLU rows [t][d]); IN: f32 caches -> T stream rows, else the reverse.
+template <typename T, bool IN, bool HL>
+__global__ void cache_io_kernel(float* acache, int H, int L, int dk2, T* kv, float* ccache, int d, int lorder, T* glu,
+                                int na) {
+  if ((int)blockIdx.x < na) {
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    const size_t n = (size_t)H * L * dk2;
+    if (i >= n) return;
+    T* r = kv + i;   // flat: cache row t = stream row t, same [H][2dk] order
+    if constexpr (HL) {
+      const int e = (int)(i % dk2), t = (int)((i / dk2) % L), h = (int)(i / ((size_t)dk2 * L));
+      r = kv + ((size_t)t * H + h) * dk2 + e;
+    }
+    if (IN) *r = from_f32<T>(acache[i]);
+    else acache[i] = to_f32(*r);
+    return;
+  }
+  const int i = ((int)blockIdx.x - na) * 256 + threadIdx.x;
+  if (i >= d * lorder) return;
+  const int t = i / d, c = i - t * d;
+  if (IN) glu[(size_t)t * d + c] = from_f32<T>(ccache[c * lorder + t]);
+  else ccache[c * lorder + t] = to_f32(glu[(size_t)t * d + c]);
+}
+// kv / glu point at the first stream row of the copied range (start row already applied)
+template <typename T>
+int cache_io(bool in, bool hl, float* acache, int H, int L, int dk, T* kv, float* ccache, int d, int lorder, T* glu,
+             hipStream_t st) {
+  const int na = (int)(((size_t)H * L * 2 * dk + 255) / 256), nc = ccache ? (d * lorder + 255) / 256 : 0;
+  if (!acache) return (int)hipErrorInvalidValue;
+  if (na + nc == 0) return 0;
+#define CIO(I_, H_) hipLaunchKernelGGL((cache_io_kernel<T, I_, H_>), dim3(na + nc), dim3(256), 0, st, acache, H, L, 2 * dk, \
+                                       kv, ccache, d, lorder, glu, na)
+  if (in) { if (hl) CIO(true, true); else CIO(true, false); }
+  else { if (hl) CIO(false, true); else CIO(false, false); }
+#undef CIO
+  CFM_CHECK_LAUNCH();
+  return 0;
+}
+
 // att_mask [n][L+C+R] / mask_pad [n][C+14] from the plan (encoder.py:625-645 closed form)
 __global__ void masks_kernel(const int32_t* meta, int n, int wa, int wp, uint8_t* att, uint8_t* pad) {
   const int i = blockIdx.x * 256 + threadIdx.x;
@@ -194,5 +236,9 @@ template int cnn_cache_in<f16>(const float*, int, int, f16*, hipStream_t);
 template int cnn_cache_out<float>(const float*, int, int, int, float*, hipStream_t);
 template int cnn_cache_out<bf16>(const bf16*, int, int, int, float*, hipStream_t);
 template int cnn_cache_out<f16>(const f16*, int, int, int, float*, hipStream_t);
+
+template int cache_io<float>(bool, bool, float*, int, int, int, float*, float*, int, int, float*, hipStream_t);
+template int cache_io<bf16>(bool, bool, float*, int, int, int, bf16*, float*, int, int, bf16*, hipStream_t);
+template int cache_io<f16>(bool, bool, float*, int, int, int, f16*, float*, int, int, f16*, hipStream_t);
 
 }  // namespace cfm

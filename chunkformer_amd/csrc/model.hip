@@ -102,6 +102,7 @@ struct cfm_model {
   int fe_group_windows = 0;         // "fe_group_windows": cap on front-end windows per group (0 = by memory)
   bool use_ring_attention = true;
   bool use_fused_ctc = true;        // "ctc_fused": bf16 ids-only CTC head as one argmax kernel (ctc.hip), no [rows, V] logits
+  int cache_fuse = 1;               // "cache_fuse": both caches of a layer in one launch at its start / end
   int attn_diag = 0;                // "attn_diag": 1 = ring kernel without compute (staging only)
   cfm::Tuning tune;                 // per-model kernel selection / diagnostics (cfm_model_set_option)
   // profiler: bitmask of PC_* classes to bracket with events on the launch stream
@@ -375,8 +376,20 @@ struct ModelT : public cfm_model {
       if constexpr (std::is_same<T, bf16>::value) a.h_out = w.h;
       return a;
     };
+    // "cache_fuse": the layer's two cache copies in one launch at the layer start (into the KV / GLU stream rows
+    // that QKV / pw1 leave alone) and one at the layer end (the KV / GLU rows stay intact after attention / the
+    // conv module); 0 = four separate launches next to QKV and pw1
+    auto caches_out = [&](int l) -> cfm_status {
+      if (cache_fuse && aci && aco)
+        PROF(PC_CACHE, cache_io<T>(false, stream, aco + l * att_ls, H, L, dk, w.kv + (size_t)cache_start * 2 * d,
+                                   cci && cco ? cco + l * cnn_ls : nullptr, d, 7, w.glu + (size_t)cache_start * d, st));
+      return CFM_OK;
+    };
     for (int l = std::max(0, stage_lo); l < nl && l <= stage_hi; ++l) {
       const LayerW& Lw = layers[l];
+      if (cache_fuse && aci)
+        PROF(PC_CACHE, cache_io<T>(true, stream, const_cast<float*>(aci + l * att_ls), H, L, dk, w.kv,
+                                   cci ? const_cast<float*>(cci + l * cnn_ls) : nullptr, d, 7, w.glu, st));
       if (fused) {   // macaron FFN: w1 + SiLU, then w2 -> y_mac, h = LN_mha(x + 0.5 y_mac)
         { EpiArgs e = E(SITE_FFN1); e.bias = Lw.b_ff1m; e.out = w.hid; e.ldo = ff;
           PROF(PC_FFN1, gemm<T>(EPI_STORE, kActSilu<T>, w.h, d, (const T*)Lw.ff1m, d, rows, ff, d, e, st)); }
@@ -390,13 +403,13 @@ struct ModelT : public cfm_model {
       { ResidAdd<T> r = resid(w.y, 0.5f, nullptr); r.defer = true;
         PROF(PC_LN, layernorm<T>(w.x, r, rows, d, Lw.ln_mha_w, Lw.ln_mha_b, eps, w.h, nullptr, st)); }
       }
-      if (aci) {
+      if (aci && !cache_fuse) {
         if (stream) PROF(PC_CACHE, att_cache_in_hl<T>(aci + l * att_ls, H, L, dk, w.kv, st));
         else PROF(PC_CACHE, att_cache_in<T>(aci + l * att_ls, L, 2 * d, w.kv, st));
       }
       { EpiArgs e = E(SITE_QKV); e.bias = Lw.b_qkv; e.out = w.q; e.out2 = w.kv; e.row_off = kvoff; e.d = d; e.dk = dk;
         PROF(PC_QKV, gemm<T>(EPI_QKV, ACT_NONE, w.h, d, (const T*)Lw.qkv, d, rows, 3 * d, d, e, st)); }
-      if (aci && aco) {
+      if (aci && aco && !cache_fuse) {
         if (stream) PROF(PC_CACHE, att_cache_out_hl<T>(w.kv, cache_start, H, L, dk, aco + l * att_ls, st));
         else PROF(PC_CACHE, att_cache_out<T>(w.kv, cache_start, L, 2 * d, aco + l * att_ls, st));
       }
@@ -450,10 +463,10 @@ struct ModelT : public cfm_model {
       PROF(PC_LN, layernorm<T>(w.x, resid2(w.y, 0.5f, nullptr, w.y2, 1.f, nullptr), rows, d, Lw.ln_conv_w, Lw.ln_conv_b,
                                eps, w.h, (masked || stream) ? nullptr : rmask, st));
       }
-      if (cci) PROF(PC_CACHE, cnn_cache_in<T>(cci + l * cnn_ls, d, 7, w.glu, st));
+      if (cci && !cache_fuse) PROF(PC_CACHE, cnn_cache_in<T>(cci + l * cnn_ls, d, 7, w.glu, st));
       { EpiArgs e = E(SITE_PW1); e.bias = Lw.b_pw1; e.out = w.glu; e.ldo = d; e.row_off = gluoff;
         PROF(PC_PW1, gemm<T>(EPI_GLU, kSiluPre<T> ? ACT_SILU_L2E : ACT_NONE, w.h, d, (const T*)Lw.pw1, d, rows, 2 * d, d, e, st)); }
-      if (cci && cco) PROF(PC_CACHE, cnn_cache_out<T>(w.glu, cache_start, d, 7, cco + l * cnn_ls, st));
+      if (cci && cco && !cache_fuse) PROF(PC_CACHE, cnn_cache_out<T>(w.glu, cache_start, d, 7, cco + l * cnn_ls, st));
       PROF(PC_CONV, conv_dw_ln_silu<T>(w.glu, convd, nconv, d, Lw.dw_t, Lw.b_dw, Lw.cn_w, Lw.cn_b, eps, w.cv, st,
                                         tune.conv_dot2, tune.conv_dma));
       if (fused) {   // pointwise_conv2 -> y_conv, h = LN_ff(x + y_conv) (x not stored)
@@ -473,6 +486,7 @@ struct ModelT : public cfm_model {
           f.g2 = fe.an_w; f.b2 = fe.an_b; f.h_out = nullptr; f.f_out = out;
         }
         if (rowln(PC_FFN2, w.hid, ff, Lw.ff2, f) < 0) return set_error(CFM_ERR_RUNTIME, "fused FFN w2 not eligible");
+        { const cfm_status cs = caches_out(l); if (cs != CFM_OK) return cs; }
         continue;
       }
       { EpiArgs e = E(SITE_PW2); e.bias = Lw.b_pw2; e.out = w.y; e.ldo = d;
@@ -488,6 +502,7 @@ struct ModelT : public cfm_model {
                                   layers[l + 1].ln_ffm_b, eps, w.h, st));
       else
         PROF(PC_LN, layernorm2_f32<T>(w.x, rf, rows, d, Lw.ln_fin_w, Lw.ln_fin_b, fe.an_w, fe.an_b, eps, out, st));
+      { const cfm_status cs = caches_out(l); if (cs != CFM_OK) return cs; }
     }
     return CFM_OK;
   }
@@ -825,6 +840,7 @@ cfm_status cfm_model_set_option(cfm_model* m, const char* key, int64_t value) {
       if (!std::strcmp(key, k.first)) { *k.second = (int)value; return CFM_OK; }
   }
   if (!std::strcmp(key, "attn_diag")) { m->attn_diag = (int)value; return CFM_OK; }
+  if (!std::strcmp(key, "cache_fuse")) { m->cache_fuse = (int)(value != 0); return CFM_OK; }
   if (!std::strcmp(key, "profile_reset")) {
     m->prof_collect();
     for (int i = 0; i < PC_N; ++i) { m->prof_ms[i] = 0; m->prof_n[i] = 0; }
