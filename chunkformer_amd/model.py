@@ -35,7 +35,7 @@ import torch
 
 from .config import EncoderConfig
 from .encoder import ChunkFormerEncoder
-from .streaming import EndlessGraphPipeline, EndlessGraphRunner, EndlessPipeline
+from .streaming import EndlessGraphPipeline, EndlessGraphRunner, EndlessPipeline, retire_graphs
 from .transducer import RNNTConfig, RNNTGreedy
 
 Features = Union[torch.Tensor, np.ndarray, str]
@@ -337,6 +337,9 @@ class ChunkFormerModel:
                           else EndlessPipeline(enc, C, L, R, trunc, want_eo, pipeline_depth))
             else:
                 runner = EndlessGraphRunner(enc, C, L, R, trunc, seg_len, want_eo, use_graph=cuda_graph)
+            for old in self._endless_runners.values():   # their captured graphs outlive them (streaming.py)
+                g = getattr(old, "graphs", None) or []
+                retire_graphs(g.values() if isinstance(g, dict) else g)
             self._endless_runners = {key: runner}
         if pipeline:
             tids, teos, cur = runner.run(xs_dev, segs)

@@ -26,6 +26,18 @@ import torch
 
 from . import _lib
 
+# Captured graphs are never destroyed while the process runs: on ROCm 7.2 a HIP graph of this multi-stream
+# pipeline destroyed (its runner replaced by another segment geometry or pipeline mode) was followed by a host
+# segfault inside a LATER graph launch (the test sequence of three models' endless_decode modes in one process,
+# any dtypes; keeping the runners alive or parking their graphs here removes it).  A retired graph keeps only
+# its node parameters and its (empty) capture pool; the runner's buffers are freed, and it is never replayed.
+_RETIRED_GRAPHS: list = []
+
+
+def retire_graphs(graphs) -> None:
+    """Park `graphs` (CUDAGraph objects, or tuples holding them) so that they are never destroyed."""
+    _RETIRED_GRAPHS.extend(g for g in graphs if g is not None)
+
 
 class EndlessGraphRunner:
     """Runs the segment schedule of one endless_decode call; middle segments by graph replay."""
@@ -101,6 +113,7 @@ class EndlessGraphRunner:
         # on scratch caches so the carried state is untouched
         saved = [(a.clone(), c.clone()) for a, c in zip(self.att, self.cnn)]
         side = torch.cuda.Stream(self.dev)
+        self._capture_stream = side   # kept alive with the graphs captured on it
         side.wait_stream(torch.cuda.current_stream(self.dev))
         with torch.cuda.stream(side):
             body(0)
@@ -331,7 +344,8 @@ class EndlessGraphPipeline:
         t = lst[i]
         if t is None or t.numel() < n:
             lst[i] = torch.empty(n, dtype=dtype, device=self.dev)
-            self.graphs.clear()   # captured graphs hold the old buffer's address
+            retire_graphs(self.graphs.values())   # captured graphs hold the old buffer's address
+            self.graphs.clear()
         return lst[i]
 
     def _segment(self, seg: dict, prev, ids_dst, eo_dst):
@@ -450,14 +464,25 @@ class EndlessGraphPipeline:
                 s = info[k0 + i]
                 self.g_feats[i][: s["len"] * enc.cfg.input_dim].view(s["len"], -1).copy_(s["x"])
             key = (k0 % self.period, cnt)
-            g = self.graphs.get(key)
-            if g is None:
+            entry = self.graphs.get(key)
+            if entry is None:
                 g = torch.cuda.CUDAGraph()
                 cap = self.streams[0]
                 cap.wait_stream(caller)
+                # every event recorded inside the capture (the per-layer edges between the streams and the
+                # fork / join) is kept alive with the graph: the captured graph can refer to them, and a
+                # destroyed one was a host crash at a later replay (three models' pipelines in one process)
+                keep: List[torch.cuda.Event] = []
+
+                def edge(dst, src):
+                    e = torch.cuda.Event()
+                    e.record(src)
+                    dst.wait_event(e)
+                    keep.append(e)
+
                 with torch.cuda.graph(g, stream=cap):
                     for st in self.streams[1:]:
-                        st.wait_stream(cap)
+                        edge(st, cap)
                     gp = None
                     for i in range(cnt):
                         s = dict(info[k0 + i])
@@ -465,10 +490,13 @@ class EndlessGraphPipeline:
                         gp = self._segment(s, gp,
                                            self.g_ids[i][: s["rows"]] if self.vocab > 0 else None,
                                            self.g_eo[i][: s["rows"] * d].view(s["rows"], d) if self.want_out else None)
+                        keep.extend(gp)
                     for st in self.streams[1:]:
-                        cap.wait_stream(st)
-                self.graphs[key] = g
+                        edge(cap, st)
+                entry = (g, keep)
+                self.graphs[key] = entry
                 caller.wait_stream(cap)
+            g = entry[0]
             g.replay()
             self.replayed += cnt
             for i in range(cnt):

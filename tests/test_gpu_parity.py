@@ -5,6 +5,8 @@ Tolerances:
   masks / n_chunks / lens : bit-exact
   fp32 mode               : max-abs <= FP32_ATOL on encoder output and CTC log-probs
   bf16 mode               : rel-L2 <= 2e-2 and CTC argmax agreement >= 99%
+  fp16 mode               : rel-L2 <= 5e-3 (the reference's own autocast fp16 run is at 1.4e-3 of its f32
+                            run on the 12-layer model, tests/test_gpu_autocast.py) and agreement >= 99%
 """
 import os
 
@@ -16,6 +18,7 @@ pytestmark = pytest.mark.gpu
 
 FP32_ATOL = 1e-4
 BF16_RELL2 = 2e-2
+RELL2 = {"bf16": BF16_RELL2, "fp16": 5e-3}
 
 
 def _rel_l2(a, b):
@@ -42,7 +45,7 @@ def small_models(cfm, small_g):
     from chunkformer_amd.config import SMALL
     from chunkformer_amd.weights import synthetic_state_dict
     sd = synthetic_state_dict(SMALL, int(small_g["seed"]))
-    return {dt: cfm.ChunkFormerEncoder(SMALL, sd, dtype=dt) for dt in ("fp32", "bf16")}
+    return {dt: cfm.ChunkFormerEncoder(SMALL, sd, dtype=dt) for dt in ("fp32", "bf16", "fp16")}
 
 
 def test_masks_bit_exact(cfm, small_models, golden_dir):
@@ -61,7 +64,7 @@ def test_masks_bit_exact(cfm, small_models, golden_dir):
 
 
 @pytest.mark.parametrize("case", ["a", "b", "c", "d"])
-@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+@pytest.mark.parametrize("dtype", ["fp32", "bf16", "fp16"])
 def test_masked_batch(cfm, small_models, small_g, case, dtype):
     from chunkformer_amd.weights import synthetic_features
     g = small_g
@@ -80,7 +83,7 @@ def test_masked_batch(cfm, small_models, small_g, case, dtype):
     if dtype == "fp32":
         np.testing.assert_allclose(o, exp, atol=FP32_ATOL, rtol=0)
     else:
-        assert _rel_l2(o, exp) <= BF16_RELL2
+        assert _rel_l2(o, exp) <= RELL2[dtype]
     if case == "a":
         logp, ids = enc.ctc_log_softmax(out)
         lp = logp.cpu().numpy()
@@ -90,7 +93,7 @@ def test_masked_batch(cfm, small_models, small_g, case, dtype):
         assert agree >= (0.999 if dtype == "fp32" else 0.99)
 
 
-@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+@pytest.mark.parametrize("dtype", ["fp32", "bf16", "fp16"])
 def test_cache_path(cfm, small_models, small_g, dtype):
     from chunkformer_amd.weights import synthetic_features
     g = small_g
@@ -106,11 +109,11 @@ def test_cache_path(cfm, small_models, small_g, dtype):
         if dtype == "fp32":
             np.testing.assert_allclose(got, exp, atol=FP32_ATOL, rtol=0)
         else:
-            assert _rel_l2(got, exp) <= BF16_RELL2
+            assert _rel_l2(got, exp) <= RELL2[dtype]
 
 
 @pytest.mark.parametrize("case", ["pc", "pf"])
-@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+@pytest.mark.parametrize("dtype", ["fp32", "bf16", "fp16"])
 def test_padded_path(cfm, small_models, small_g, case, dtype):
     from chunkformer_amd.weights import synthetic_features
     g = small_g
@@ -127,7 +130,7 @@ def test_padded_path(cfm, small_models, small_g, case, dtype):
     if dtype == "fp32":
         np.testing.assert_allclose(o, g[f"{case}_out"], atol=FP32_ATOL, rtol=0)
     else:
-        assert _rel_l2(o, g[f"{case}_out"]) <= BF16_RELL2
+        assert _rel_l2(o, g[f"{case}_out"]) <= RELL2[dtype]
 
 
 @pytest.fixture(scope="module")
@@ -136,10 +139,10 @@ def large(cfm, golden_dir):
     from chunkformer_amd.weights import synthetic_state_dict
     g = np.load(os.path.join(golden_dir, "large.npz"))
     sd = synthetic_state_dict(LARGE, int(g["seed"]))
-    return g, {dt: cfm.ChunkFormerEncoder(LARGE, sd, dtype=dt) for dt in ("fp32", "bf16")}
+    return g, {dt: cfm.ChunkFormerEncoder(LARGE, sd, dtype=dt) for dt in ("fp32", "bf16", "fp16")}
 
 
-@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+@pytest.mark.parametrize("dtype", ["fp32", "bf16", "fp16"])
 def test_large_12L(cfm, large, dtype):
     from chunkformer_amd.weights import synthetic_features
     g, models = large
@@ -159,7 +162,7 @@ def test_large_12L(cfm, large, dtype):
         sure = margin > 1e-4
         np.testing.assert_array_equal(ids[sure], g["ids"][sure])
     else:
-        assert _rel_l2(o, g["out"]) <= BF16_RELL2
+        assert _rel_l2(o, g["out"]) <= RELL2[dtype]
         assert (ids == g["ids"]).mean() >= 0.99
 
 

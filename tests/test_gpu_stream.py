@@ -4,7 +4,7 @@
 reference's own run of the same steps (tests/golden/stream.npz, gen_golden.py:gen_stream).
 
 Tolerances (SURVEY §8c): fp32 max-abs 1e-4 on every step's output and on the carried caches;
-bf16 rel-L2 <= 2e-2."""
+bf16 rel-L2 <= 2e-2; fp16 rel-L2 <= 5e-3."""
 import os
 
 import numpy as np
@@ -13,6 +13,7 @@ import torch
 
 pytestmark = pytest.mark.gpu
 BF16_RELL2 = 2e-2
+RELL2 = {"bf16": BF16_RELL2, "fp16": 5e-3}
 
 
 def _rel(a, b):
@@ -44,11 +45,11 @@ def _run(tag, cfg, seed, dtype):
         if dtype == "fp32":
             np.testing.assert_allclose(y.cpu().numpy(), exp, atol=1e-4, rtol=0, err_msg=f"step {i}")
         else:
-            assert _rel(y.cpu().numpy(), exp) <= BF16_RELL2, (i, _rel(y.cpu().numpy(), exp))
+            assert _rel(y.cpu().numpy(), exp) <= RELL2[dtype], (i, _rel(y.cpu().numpy(), exp))
     return g, att.cpu().numpy(), cnn.cpu().numpy()
 
 
-@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+@pytest.mark.parametrize("dtype", ["fp32", "bf16", "fp16"])
 def test_forward_chunk_small_batch2(dtype):
     """d=128 2-layer model, batch 2, C=16 L=32 R=16: four full steps and a short last step."""
     from chunkformer_amd.config import SMALL
@@ -57,10 +58,10 @@ def test_forward_chunk_small_batch2(dtype):
         np.testing.assert_allclose(att, g["a_att"], atol=1e-4, rtol=0)
         np.testing.assert_allclose(cnn, g["a_cnn"], atol=1e-4, rtol=0)
     else:
-        assert _rel(att, g["a_att"]) <= BF16_RELL2 and _rel(cnn, g["a_cnn"]) <= BF16_RELL2
+        assert _rel(att, g["a_att"]) <= RELL2[dtype] and _rel(cnn, g["a_cnn"]) <= RELL2[dtype]
 
 
-@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+@pytest.mark.parametrize("dtype", ["fp32", "bf16", "fp16"])
 def test_forward_chunk_large_4h(dtype):
     """d=512, 4 heads (head_dim 128), 12 layers, C=64 L=R=128: three steps, carried caches."""
     from chunkformer_amd.config import LARGE_4H
@@ -70,7 +71,7 @@ def test_forward_chunk_large_4h(dtype):
         np.testing.assert_allclose(att, g["b_att"], atol=1e-4, rtol=0)
         np.testing.assert_allclose(cnn, g["b_cnn"], atol=1e-4, rtol=0)
     else:
-        assert _rel(att, g["b_att"]) <= BF16_RELL2 and _rel(cnn, g["b_cnn"]) <= BF16_RELL2
+        assert _rel(att, g["b_att"]) <= RELL2[dtype] and _rel(cnn, g["b_cnn"]) <= RELL2[dtype]
 
 
 def test_forward_chunk_matches_oracle_offsets():
