@@ -103,6 +103,7 @@ struct cfm_model {
   bool use_ring_attention = true;
   bool use_fused_ctc = true;        // "ctc_fused": bf16 ids-only CTC head as one argmax kernel (ctc.hip), no [rows, V] logits
   int cache_fuse = 1;               // "cache_fuse": both caches of a layer in one launch at its start / end
+  int trim_right = 0;               // "trim_right": this call's rows past `trunc` are dropped by the caller (encode)
   int attn_diag = 0;                // "attn_diag": 1 = ring kernel without compute (staging only)
   cfm::Tuning tune;                 // per-model kernel selection / diagnostics (cfm_model_set_option)
   // profiler: bitmask of PC_* classes to bracket with events on the launch stream
@@ -351,11 +352,11 @@ struct ModelT : public cfm_model {
       ResidAdd<T> r = resid(y, alpha, ym); r.y2 = y2; r.alpha2 = alpha2; r.ymask2 = ym2; return r;
     };
     // y = w2 . SiLU(w1 . h + b1) + b2: two GEMMs through w.hid
-    auto ffn = [&](const void* w1, const float* b1, const void* w2, const float* b2, T* yout) -> cfm_status {
+    auto ffn = [&](const void* w1, const float* b1, const void* w2, const float* b2, T* yout, int M) -> cfm_status {
       { EpiArgs e = E(SITE_FFN1); e.bias = b1; e.out = w.hid; e.ldo = ff;
-        PROF(PC_FFN1, gemm<T>(EPI_STORE, kActSilu<T>, w.h, d, (const T*)w1, d, rows, ff, d, e, st)); }
+        PROF(PC_FFN1, gemm<T>(EPI_STORE, kActSilu<T>, w.h, d, (const T*)w1, d, M, ff, d, e, st)); }
       { EpiArgs e = E(SITE_FFN2); e.bias = b2; e.out = yout; e.ldo = d;
-        PROF(PC_FFN2, gemm<T>(EPI_STORE, ACT_NONE, w.hid, ff, (const T*)w2, ff, rows, d, ff, e, st)); }
+        PROF(PC_FFN2, gemm<T>(EPI_STORE, ACT_NONE, w.hid, ff, (const T*)w2, ff, M, d, ff, e, st)); }
       return CFM_OK;
     };
     // Fused form (bf16, d = 512, "ln_fuse"): each N = 512 GEMM of the layer owns whole rows
@@ -385,8 +386,25 @@ struct ModelT : public cfm_model {
                                    cci && cco ? cco + l * cnn_ls : nullptr, d, 7, w.glu + (size_t)cache_start * d, st));
       return CFM_OK;
     };
+    // "trim_right" (endless_decode's segments, whose rows past `trunc` are dropped): layer l computes only the
+    // chunks the kept ones depend on.  Kept chunks K = trunc / C; the conv module of a chunk reads 7 rows of
+    // the next one (ceil(7 / C) chunks) and attention R keys past a chunk (ceil(R / C)), so layer l's output
+    // is needed for n_l = K + (nl - 1 - l)(ceil(7 / C) + ceil(R / C)) chunks: its conv module / pw2 / FFN /
+    // norm_final run over n_l, attention / out-proj / pw1 over n_l + ceil(7 / C) and the macaron FFN / LN /
+    // QKV over that + ceil(R / C) (= the previous layer's n).  Every row's arithmetic is
+    // unchanged (row-wise kernels, per-chunk attention / conv blocks), so the kept rows and the caches are
+    // as without it; the rows past them are left unwritten.
+    const int n_ch = rows / C, keep_ch = C > 0 ? trunc / C : 0;
+    const bool trim = trim_right && masked && !fused && aco && trunc > 0 && trunc % C == 0 && trunc < rows &&
+                      rows % C == 0 && natt == n_ch && nconv == n_ch && hh[PH_NWIN] == n_ch;
+    // chunks of right reach per layer: the conv module's 7 rows, then attention's R keys past those
+    const int reach_conv = (7 + C - 1) / C, reach_att = (hh[PH_R] + C - 1) / C;
     for (int l = std::max(0, stage_lo); l < nl && l <= stage_hi; ++l) {
       const LayerW& Lw = layers[l];
+      const int n_l = trim ? std::min(n_ch, keep_ch + (reach_conv + reach_att) * (nl - 1 - l)) : n_ch;
+      const int cB = trim ? std::min(n_ch, n_l + reach_conv) : n_ch, cA = trim ? std::min(n_ch, cB + reach_att) : n_ch;
+      const int rA = trim ? cA * C : rows, rB = trim ? cB * C : rows, rN = trim ? n_l * C : rows;
+      const int aB = trim ? cB : natt, vN = trim ? n_l : nconv;   // attention / conv descriptor counts
       if (cache_fuse && aci)
         PROF(PC_CACHE, cache_io<T>(true, stream, const_cast<float*>(aci + l * att_ls), H, L, dk, w.kv,
                                    cci ? const_cast<float*>(cci + l * cnn_ls) : nullptr, d, 7, w.glu, st));
@@ -398,17 +416,17 @@ struct ModelT : public cfm_model {
         if (rowln(PC_FFN2, w.hid, ff, Lw.ff2m, a) < 0) return set_error(CFM_ERR_RUNTIME, "fused FFN w2 not eligible");
       } else {
       // macaron FFN (x 0.5)
-      { const cfm_status fs = ffn(Lw.ff1m, Lw.b_ff1m, Lw.ff2m, Lw.b_ff2m, w.y); if (fs != CFM_OK) return fs; }
+      { const cfm_status fs = ffn(Lw.ff1m, Lw.b_ff1m, Lw.ff2m, Lw.b_ff2m, w.y, rA); if (fs != CFM_OK) return fs; }
       // MHSA (x + 0.5 y_ffm is not stored: the conv LayerNorm re-applies it)
       { ResidAdd<T> r = resid(w.y, 0.5f, nullptr); r.defer = true;
-        PROF(PC_LN, layernorm<T>(w.x, r, rows, d, Lw.ln_mha_w, Lw.ln_mha_b, eps, w.h, nullptr, st)); }
+        PROF(PC_LN, layernorm<T>(w.x, r, rA, d, Lw.ln_mha_w, Lw.ln_mha_b, eps, w.h, nullptr, st)); }
       }
       if (aci && !cache_fuse) {
         if (stream) PROF(PC_CACHE, att_cache_in_hl<T>(aci + l * att_ls, H, L, dk, w.kv, st));
         else PROF(PC_CACHE, att_cache_in<T>(aci + l * att_ls, L, 2 * d, w.kv, st));
       }
       { EpiArgs e = E(SITE_QKV); e.bias = Lw.b_qkv; e.out = w.q; e.out2 = w.kv; e.row_off = kvoff; e.d = d; e.dk = dk;
-        PROF(PC_QKV, gemm<T>(EPI_QKV, ACT_NONE, w.h, d, (const T*)Lw.qkv, d, rows, 3 * d, d, e, st)); }
+        PROF(PC_QKV, gemm<T>(EPI_QKV, ACT_NONE, w.h, d, (const T*)Lw.qkv, d, rA, 3 * d, d, e, st)); }
       if (aci && aco && !cache_fuse) {
         if (stream) PROF(PC_CACHE, att_cache_out_hl<T>(w.kv, cache_start, H, L, dk, aco + l * att_ls, st));
         else PROF(PC_CACHE, att_cache_out<T>(w.kv, cache_start, L, 2 * d, aco + l * att_ls, st));
@@ -420,16 +438,16 @@ struct ModelT : public cfm_model {
         if constexpr (std::is_same<T, bf16>::value) {
           if (masked && use_ring_attention && dk == 64 && tune.attn_q32)
             r = chunk_attention_masked_q32(w.q, w.kv, kv_rows, w.P + (size_t)l * d, p_rows, p_ld, Lw.pu, Lw.pv, attd,
-                                           natt, H, C, hh[PH_L] + C + hh[PH_R], w.ao, st,
+                                           aB, H, C, hh[PH_L] + C + hh[PH_R], w.ao, st,
                                            attn_diag >= 64 ? attn_diag - 64 : 0, tune.attn_q32);
           if (r == -1 && masked && use_ring_attention && dk == 64)
             r = chunk_attention_masked_bf16(w.q, w.kv, kv_rows, w.P + (size_t)l * d, p_rows, Lw.pu, Lw.pv,
-                                            attd, natt, H, C, hh[PH_L] + C + hh[PH_R], w.ao, st, attn_diag, p_ld,
+                                            attd, aB, H, C, hh[PH_L] + C + hh[PH_R], w.ao, st, attn_diag, p_ld,
                                             tune.attn_reuse, tune.attn_min_chunks);
           else if (w.vt) {   // head_dim 128 (4-head d=512): V^T copy, then the band / score / P.V kernel
             KCHK(vt_transpose_bf16(w.kv, kv_rows, H, w.vt, w.vt_ld, st));
             r = chunk_attention_masked_a128(w.q, w.kv, kv_rows, w.vt, w.vt_ld, w.P + (size_t)l * d, p_rows, p_ld,
-                                            Lw.pu, Lw.pv, attd, natt, H, C, hh[PH_L] + C + hh[PH_R], w.ao, st,
+                                            Lw.pu, Lw.pv, attd, aB, H, C, hh[PH_L] + C + hh[PH_R], w.ao, st,
                                             tune.attn128_var);
           }
           // full attention (padded plan, one chunk of T' per utterance: key window [0, T')) -> dense kernel
@@ -440,12 +458,12 @@ struct ModelT : public cfm_model {
         }
         if constexpr (std::is_same<T, f16>::value) {
           if (masked && use_ring_attention && dk == 64)
-            r = chunk_attention_masked_f16(w.q, w.kv, kv_rows, w.P + (size_t)l * d, p_rows, Lw.pu, Lw.pv, attd, natt, H, C,
+            r = chunk_attention_masked_f16(w.q, w.kv, kv_rows, w.P + (size_t)l * d, p_rows, Lw.pu, Lw.pv, attd, aB, H, C,
                                            hh[PH_L] + C + hh[PH_R], w.ao, st, attn_diag, p_ld, tune.attn_reuse,
                                            tune.attn_min_chunks);
         }
         if (r == -1)
-          r = chunk_attention<T>(w.q, w.kv, kv_rows, w.P + (size_t)l * d, p_rows, Lw.pu, Lw.pv, attd, natt,
+          r = chunk_attention<T>(w.q, w.kv, kv_rows, w.P + (size_t)l * d, p_rows, Lw.pu, Lw.pv, attd, aB,
                                  H, dk, w.ao, st, p_ld);
         KCHK(r);
         prof_end(PC_ATTN, st, pb_);
@@ -458,16 +476,16 @@ struct ModelT : public cfm_model {
         if (rowln(PC_OPROJ, w.ao, d, Lw.wo, a) < 0) return set_error(CFM_ERR_RUNTIME, "fused linear_out not eligible");
       } else {
       { EpiArgs e = E(SITE_OPROJ); e.bias = Lw.b_o; e.out = w.y2; e.ldo = d;
-        PROF(PC_OPROJ, gemm<T>(EPI_STORE, ACT_NONE, w.ao, d, (const T*)Lw.wo, d, rows, d, d, e, st)); }
+        PROF(PC_OPROJ, gemm<T>(EPI_STORE, ACT_NONE, w.ao, d, (const T*)Lw.wo, d, rB, d, d, e, st)); }
       // convolution module: x += 0.5 y_ffm + y_attn, stored
-      PROF(PC_LN, layernorm<T>(w.x, resid2(w.y, 0.5f, nullptr, w.y2, 1.f, nullptr), rows, d, Lw.ln_conv_w, Lw.ln_conv_b,
+      PROF(PC_LN, layernorm<T>(w.x, resid2(w.y, 0.5f, nullptr, w.y2, 1.f, nullptr), rB, d, Lw.ln_conv_w, Lw.ln_conv_b,
                                eps, w.h, (masked || stream) ? nullptr : rmask, st));
       }
       if (cci && !cache_fuse) PROF(PC_CACHE, cnn_cache_in<T>(cci + l * cnn_ls, d, 7, w.glu, st));
       { EpiArgs e = E(SITE_PW1); e.bias = Lw.b_pw1; e.out = w.glu; e.ldo = d; e.row_off = gluoff;
-        PROF(PC_PW1, gemm<T>(EPI_GLU, kSiluPre<T> ? ACT_SILU_L2E : ACT_NONE, w.h, d, (const T*)Lw.pw1, d, rows, 2 * d, d, e, st)); }
+        PROF(PC_PW1, gemm<T>(EPI_GLU, kSiluPre<T> ? ACT_SILU_L2E : ACT_NONE, w.h, d, (const T*)Lw.pw1, d, rB, 2 * d, d, e, st)); }
       if (cci && cco && !cache_fuse) PROF(PC_CACHE, cnn_cache_out<T>(w.glu, cache_start, d, 7, cco + l * cnn_ls, st));
-      PROF(PC_CONV, conv_dw_ln_silu<T>(w.glu, convd, nconv, d, Lw.dw_t, Lw.b_dw, Lw.cn_w, Lw.cn_b, eps, w.cv, st,
+      PROF(PC_CONV, conv_dw_ln_silu<T>(w.glu, convd, vN, d, Lw.dw_t, Lw.b_dw, Lw.cn_w, Lw.cn_b, eps, w.cv, st,
                                         tune.conv_dot2, tune.conv_dma));
       if (fused) {   // pointwise_conv2 -> y_conv, h = LN_ff(x + y_conv) (x not stored)
         RowLnArgs a = ln_args(Lw.b_pw2, 1.f, Lw.ln_ff_w, Lw.ln_ff_b);
@@ -490,18 +508,18 @@ struct ModelT : public cfm_model {
         continue;
       }
       { EpiArgs e = E(SITE_PW2); e.bias = Lw.b_pw2; e.out = w.y; e.ldo = d;
-        PROF(PC_PW2, gemm<T>(EPI_STORE, ACT_NONE, w.cv, d, (const T*)Lw.pw2, d, rows, d, d, e, st)); }
+        PROF(PC_PW2, gemm<T>(EPI_STORE, ACT_NONE, w.cv, d, (const T*)Lw.pw2, d, rN, d, d, e, st)); }
       // FFN (x 0.5); x + y_conv is not stored: norm_final re-applies it
       { ResidAdd<T> r = resid(w.y, 1.f, rmask); r.defer = true;
-        PROF(PC_LN, layernorm<T>(w.x, r, rows, d, Lw.ln_ff_w, Lw.ln_ff_b, eps, w.h, nullptr, st)); }
-      { const cfm_status fs = ffn(Lw.ff1, Lw.b_ff1, Lw.ff2, Lw.b_ff2, w.y2); if (fs != CFM_OK) return fs; }
+        PROF(PC_LN, layernorm<T>(w.x, r, rN, d, Lw.ln_ff_w, Lw.ln_ff_b, eps, w.h, nullptr, st)); }
+      { const cfm_status fs = ffn(Lw.ff1, Lw.b_ff1, Lw.ff2, Lw.b_ff2, w.y2, rN); if (fs != CFM_OK) return fs; }
       // norm_final over x + y_conv + 0.5 y_ffn (+ next layer's macaron LN, or after_norm)
       const ResidAdd<T> rf = resid2(w.y, 1.f, rmask, w.y2, 0.5f, nullptr);
       if (l + 1 < nl)
-        PROF(PC_LN, layernorm2<T>(w.x, rf, rows, d, Lw.ln_fin_w, Lw.ln_fin_b, layers[l + 1].ln_ffm_w,
+        PROF(PC_LN, layernorm2<T>(w.x, rf, rN, d, Lw.ln_fin_w, Lw.ln_fin_b, layers[l + 1].ln_ffm_w,
                                   layers[l + 1].ln_ffm_b, eps, w.h, st));
       else
-        PROF(PC_LN, layernorm2_f32<T>(w.x, rf, rows, d, Lw.ln_fin_w, Lw.ln_fin_b, fe.an_w, fe.an_b, eps, out, st));
+        PROF(PC_LN, layernorm2_f32<T>(w.x, rf, rN, d, Lw.ln_fin_w, Lw.ln_fin_b, fe.an_w, fe.an_b, eps, out, st));
       { const cfm_status cs = caches_out(l); if (cs != CFM_OK) return cs; }
     }
     return CFM_OK;
@@ -841,6 +859,7 @@ cfm_status cfm_model_set_option(cfm_model* m, const char* key, int64_t value) {
   }
   if (!std::strcmp(key, "attn_diag")) { m->attn_diag = (int)value; return CFM_OK; }
   if (!std::strcmp(key, "cache_fuse")) { m->cache_fuse = (int)(value != 0); return CFM_OK; }
+  if (!std::strcmp(key, "trim_right")) { m->trim_right = (int)(value != 0); return CFM_OK; }
   if (!std::strcmp(key, "profile_reset")) {
     m->prof_collect();
     for (int i = 0; i < PC_N; ++i) { m->prof_ms[i] = 0; m->prof_n[i] = 0; }

@@ -113,6 +113,11 @@ class ChunkFormerEncoder:
                 if k not in explicit:
                     _lib.check(_lib.cfm_model_set_option(self._h, k.encode(), int(keep[k])))
 
+    def _set_trim(self, on: bool) -> None:
+        """Native "trim_right" for the next encode calls (endless_decode's truncated segments only: their
+        rows past truncated_context_size are not computed -- the caller drops them)."""
+        _lib.check(_lib.cfm_model_set_option(self._h, b"trim_right", int(bool(on))))
+
     # ------------------------------------------------------------------ helpers
     def _workspace(self, nbytes: int) -> torch.Tensor:
         if self._ws is None or self._ws.numel() < nbytes:

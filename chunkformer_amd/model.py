@@ -203,6 +203,9 @@ class ChunkFormerModel:
         self.resample_conf = dict(resample_conf or {})
         self._fbank = None
         self._endless_runners: Dict[tuple, EndlessGraphRunner] = {}
+        # endless_decode: truncated segments compute only the rows their kept rows depend on (native
+        # "trim_right"; the kept rows, ids and caches are unchanged -- test_endless_trim_equals_full)
+        self.endless_trim = True
 
     def extract_features(self, samples, sample_rate: Optional[int] = None) -> torch.Tensor:
         """_load_audio_and_extract_features (chunkformer_model.py:276-318) after decoding:
@@ -329,14 +332,15 @@ class ChunkFormerModel:
             pipeline = len(segs) >= 3
         if pipeline_depth is None:
             pipeline_depth = 4 if cuda_graph else 3
-        key = (C, L, R, trunc, seg_len, want_eo, bool(cuda_graph), bool(pipeline), int(pipeline_depth))
+        trim = bool(self.endless_trim)
+        key = (C, L, R, trunc, seg_len, want_eo, bool(cuda_graph), bool(pipeline), int(pipeline_depth), trim)
         runner = self._endless_runners.get(key)
         if runner is None:   # graphs are captured once per segment geometry and reused across calls
             if pipeline:
-                runner = (EndlessGraphPipeline(enc, C, L, R, trunc, seg_len, want_eo, pipeline_depth) if cuda_graph
-                          else EndlessPipeline(enc, C, L, R, trunc, want_eo, pipeline_depth))
+                runner = (EndlessGraphPipeline(enc, C, L, R, trunc, seg_len, want_eo, pipeline_depth, trim=trim)
+                          if cuda_graph else EndlessPipeline(enc, C, L, R, trunc, want_eo, pipeline_depth, trim=trim))
             else:
-                runner = EndlessGraphRunner(enc, C, L, R, trunc, seg_len, want_eo, use_graph=cuda_graph)
+                runner = EndlessGraphRunner(enc, C, L, R, trunc, seg_len, want_eo, use_graph=cuda_graph, trim=trim)
             for old in self._endless_runners.values():   # their captured graphs outlive them (streaming.py)
                 g = getattr(old, "graphs", None) or []
                 retire_graphs(g.values() if isinstance(g, dict) else g)
@@ -349,14 +353,17 @@ class ChunkFormerModel:
         else:
             runner.reset()
             offset = 0
-            for start, stop, keep_trunc, _ in segs:
-                # forward_parallel_chunk with att/cnn caches carried; offset += len, then -= dropped rows
-                tok, eo, kept = runner.step(xs_dev[start:stop], offset, keep_trunc)
-                offset += kept
-                if tok is not None:
-                    ids.append(tok)
-                if eo is not None:
-                    outs.append(eo)
+            try:
+                for start, stop, keep_trunc, _ in segs:
+                    # forward_parallel_chunk with att/cnn caches carried; offset += len, then -= dropped rows
+                    tok, eo, kept = runner.step(xs_dev[start:stop], offset, keep_trunc)
+                    offset += kept
+                    if tok is not None:
+                        ids.append(tok)
+                    if eo is not None:
+                        outs.append(eo)
+            finally:
+                enc._set_trim(False)
             # the caches carried out of the last segment (r_att_cache / r_cnn_cache of its
             # forward_parallel_chunk call, chunkformer_model.py:407-417)
             self.last_endless_caches = (runner.att[runner.cur], runner.cnn[runner.cur])

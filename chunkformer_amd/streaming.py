@@ -43,8 +43,9 @@ class EndlessGraphRunner:
     """Runs the segment schedule of one endless_decode call; middle segments by graph replay."""
 
     def __init__(self, encoder, C: int, L: int, R: int, trunc: int, seg_len: int, want_out: bool,
-                 use_graph: bool = True):
+                 use_graph: bool = True, trim: bool = False):
         self.enc = encoder
+        self.trim = trim   # truncated segments skip the rows past trunc (model option "trim_right")
         cfg = encoder.cfg
         self.C, self.L, self.R, self.trunc = C, L, R, trunc
         self.seg_len = seg_len
@@ -68,8 +69,9 @@ class EndlessGraphRunner:
         self.cnn[0].zero_()
 
     # ------------------------------------------------------------------ eager step
-    def _eager(self, x: torch.Tensor, offset: int):
+    def _eager(self, x: torch.Tensor, offset: int, keep_trunc: bool):
         enc = self.enc
+        enc._set_trim(self.trim and keep_trunc)
         n_frames = x.shape[0]
         plan, n_chunks, out_lens = _lib.plan_masked([n_frames], [offset], self.C, self.L, self.R)
         N = n_chunks[0]
@@ -101,6 +103,7 @@ class EndlessGraphRunner:
             nb = enc.ctc_ws_bytes(self.g_rows, False)   # 0 on the fused argmax head
             self.g_ctc_ws = torch.empty(nb, dtype=torch.uint8, device=self.dev) if nb > 0 else None
         torch.cuda.current_stream(self.dev).synchronize()
+        self.enc._set_trim(self.trim)   # only truncated middle segments replay (_replayable)
 
         def body(src: int):
             dst = 1 - src
@@ -127,8 +130,8 @@ class EndlessGraphRunner:
             a.copy_(sa)
             c.copy_(sc)
 
-    def _replayable(self, n_frames: int, offset: int) -> bool:
-        if not self.use_graph or n_frames != self.seg_len:
+    def _replayable(self, n_frames: int, offset: int, keep_trunc: bool) -> bool:
+        if not self.use_graph or n_frames != self.seg_len or not keep_trunc:
             return False
         if self.g_plan is None:   # capture only where the plan no longer depends on offset
             return offset >= max(self.L, 7)
@@ -138,7 +141,7 @@ class EndlessGraphRunner:
     def step(self, x: torch.Tensor, offset: int, keep_trunc: bool):
         """One segment: returns (CTC ids of the kept rows or None, kept encoder rows or None, kept row
         count).  Rows are kept as chunkformer_model.py:419-431 keeps them: eo[:n], then [:trunc]."""
-        if self._replayable(x.shape[0], offset):
+        if self._replayable(x.shape[0], offset, keep_trunc):
             if self.graphs[0] is None:
                 self._capture(offset)
             self.g_feats.copy_(x)
@@ -152,7 +155,7 @@ class EndlessGraphRunner:
             else:
                 ids = self.enc.ctc_log_softmax(eo, want_logp=False)[1] if self.vocab > 0 else None
             return ids, (eo.clone() if self.want_out else None), eo.shape[0]
-        out, n = self._eager(x, offset)
+        out, n = self._eager(x, offset, keep_trunc)
         eo = out[:n]
         if keep_trunc:
             eo = eo[: self.trunc]
@@ -181,10 +184,12 @@ class EndlessPipeline:
     call (stage -1: front-end + relative positions; stage l: layer l), so the result is bit-identical
     to the one-call-per-segment loop (same kernels, same inputs, same order per segment)."""
 
-    def __init__(self, encoder, C: int, L: int, R: int, trunc: int, want_out: bool, depth: int = 3):
+    def __init__(self, encoder, C: int, L: int, R: int, trunc: int, want_out: bool, depth: int = 3,
+                 trim: bool = False):
         if depth < 1:
             raise ValueError(f"pipeline depth {depth} < 1")
         self.enc = encoder
+        self.trim = trim
         self.depth = depth
         cfg = encoder.cfg
         self.C, self.L, self.R, self.trunc = C, L, R, trunc
@@ -212,7 +217,10 @@ class EndlessPipeline:
         index of the cache pair holding the caches after the last segment); the tensors are ready on
         the caller's current stream.  Launch parameters for segments in flight: PIPELINE_OPTS."""
         with self.enc.scoped_options(**PIPELINE_OPTS):
-            return self._run(xs_dev, segs)
+            try:
+                return self._run(xs_dev, segs)
+            finally:
+                self.enc._set_trim(False)
 
     def _run(self, xs_dev: torch.Tensor, segs):
         enc, C, L, R = self.enc, self.C, self.L, self.R
@@ -235,6 +243,7 @@ class EndlessPipeline:
             N = n_chunks[0]
             wsb = int(_lib.cfm_workspace_bytes_masked(enc._h, N, C, L, R))
             cur = []
+            enc._set_trim(self.trim and keep_trunc)
             with torch.cuda.stream(st):
                 plan_dev = plan.pin_memory().to(self.dev, non_blocking=True)
                 ws = self._buf(self.ws, p, wsb, torch.uint8)
@@ -312,10 +321,11 @@ class EndlessGraphPipeline:
     bit-identical to the one-call-per-segment loop."""
 
     def __init__(self, encoder, C: int, L: int, R: int, trunc: int, seg_len: int, want_out: bool, depth: int = 3,
-                 block: int = 64):
+                 block: int = 64, trim: bool = False):
         if depth < 1:
             raise ValueError(f"pipeline depth {depth} < 1")
         self.enc = encoder
+        self.trim = trim
         cfg = encoder.cfg
         self.C, self.L, self.R, self.trunc, self.seg_len = C, L, R, trunc, seg_len
         self.want_out = want_out
@@ -358,6 +368,7 @@ class EndlessGraphPipeline:
         p, c = k % self.depth, k % 2
         st = self.streams[p]
         cur = []
+        enc._set_trim(self.trim and seg["keep"])
         for stage in range(-1, enc.cfg.num_blocks):
             if stage >= 0 and prev is not None:
                 st.wait_event(prev[stage])
@@ -385,7 +396,10 @@ class EndlessGraphPipeline:
         the cache pair holding the caches after the last segment), ready on the caller's stream.
         Launch parameters for segments in flight: PIPELINE_OPTS (baked into the captured graphs)."""
         with self.enc.scoped_options(**PIPELINE_OPTS):
-            return self._run(xs_dev, segs)
+            try:
+                return self._run(xs_dev, segs)
+            finally:
+                self.enc._set_trim(False)
 
     def _run(self, xs_dev: torch.Tensor, segs):
         enc, C, L, R, D = self.enc, self.C, self.L, self.R, self.depth
@@ -403,7 +417,7 @@ class EndlessGraphPipeline:
             plan, n_chunks, out_lens = _lib.plan_masked([n_frames], [offset], C, L, R)
             N = n_chunks[0]
             kept = min(out_lens[0], self.trunc) if keep_trunc else out_lens[0]
-            info.append({"k": k, "x": xs_dev[start:stop], "plan": plan, "N": N, "rows": kept,
+            info.append({"k": k, "x": xs_dev[start:stop], "plan": plan, "N": N, "rows": kept, "keep": keep_trunc,
                          "wsb": int(_lib.cfm_workspace_bytes_masked(enc._h, N, C, L, R)), "len": n_frames})
             offset += kept
         # the graph plan: the first middle segment whose plan no longer depends on the offset

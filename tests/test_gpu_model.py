@@ -137,3 +137,30 @@ def test_endless_decode_larger_segments_match_reference(small, golden_dir, dtype
     else:
         assert np.linalg.norm(eo - exp) / np.linalg.norm(exp) <= RELL2[dtype]
         assert (ids == g["ids"]).mean() >= 0.99
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16", "fp16"])
+def test_endless_trim_equals_full(small, dtype):
+    """endless_decode's truncated segments computing only the rows their kept rows depend on (native
+    "trim_right", model.endless_trim) give exactly the rows, ids and final caches of the full
+    computation, in the one-segment-at-a-time loop and in the graph-replayed pipeline."""
+    from chunkformer_amd.weights import synthetic_features
+    g, models = small
+    C, L, R, tbd = (int(v) for v in g["endless_clrt"])
+    x = synthetic_features([6000], int(g["endless_seed"]))[0]
+    m = models[dtype]
+    try:
+        for graph, pipe in ((False, False), (True, False), (True, True)):
+            res = {}
+            for trim in (False, True):
+                m.endless_trim = trim
+                ids, eo = m.endless_decode(x, C, L, R, total_batch_duration=tbd, return_encoder_out=True,
+                                           cuda_graph=graph, pipeline=pipe)
+                res[trim] = (ids, eo, [c.clone() for c in m.last_endless_caches])
+            (i0, e0, c0), (i1, e1, c1) = res[False], res[True]
+            assert torch.equal(e0, e1), (graph, pipe)
+            assert torch.equal(i0, i1), (graph, pipe)
+            for a, b in zip(c0, c1):
+                assert torch.equal(a, b), (graph, pipe)
+    finally:
+        m.endless_trim = True
