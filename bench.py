@@ -280,7 +280,7 @@ def main():
                          "attention, B=256)")
     ap.add_argument("--hours", type=float, default=16.0, help="endless: audio hours")
     ap.add_argument("--endless-mode", default="graphpipe", choices=["graphpipe", "pipeline", "graph"],
-                    help="endless: --pipeline-depth segments in flight, runs of up to 64 middle segments replaying "
+                    help="endless: --pipeline-depth segments in flight, every segment (up to 128 per graph) replaying "
                          "one captured HIP graph of that multi-stream pipeline (graphpipe), the same pipeline "
                          "launched eagerly (pipeline), or one segment "
                          "at a time replaying one captured graph per middle segment (graph); all bit-identical "
@@ -586,7 +586,7 @@ def bench_single(args):
                     f"R=128, total_batch_duration={args.tbd}: {len(segs)} segments of <= {seg_len} frames "
                     f"(trunc {trunc} rows kept each), att/cnn caches carried, " +
                     {"graphpipe": f"{depth} segments in flight on as many HIP streams (segment k+1 "
-                                  "layer l after segment k layer l), each run of up to 64 middle segments one "
+                                  "layer l after segment k layer l), all segments (up to 128 per graph) one "
                                   "replay of a captured HIP graph of that whole multi-stream pipeline",
                      "pipeline": f"{depth} segments in flight on {depth} HIP streams "
                                  "(segment k+1 layer l waits for segment k layer l), launched eagerly",

@@ -312,8 +312,8 @@ class ChunkFormerModel:
         `return_encoder_out` also the concatenated encoder output [1, T', d] (fp32).
         `pipeline` (default: on from 3 segments up): `pipeline_depth` (default 4 with graphs, 3 eager:
         the measured best of each at tbd 1800) segments in flight on as many
-        streams, segment k + 1's layer l waiting only for segment k's layer l; with `cuda_graph` runs of
-        up to 64 middle segments replay one captured HIP graph of that whole multi-stream pipeline
+        streams, segment k + 1's layer l waiting only for segment k's layer l; with `cuda_graph` all
+        segments (up to 128 per graph) replay one captured HIP graph of that whole multi-stream pipeline
         (EndlessGraphPipeline), without it every call is launched eagerly (EndlessPipeline).  pipeline=False: one segment at a time, the full-size
         middle segments replaying one captured graph (EndlessGraphRunner) when `cuda_graph`.  Every
         mode gives the same result as the eager loop (same kernels, same plans); see streaming.py."""

@@ -281,47 +281,36 @@ class EndlessPipeline:
         return ids_out, eo_out, len(segs) % 2
 
 
-def graph_blocks(graph_ok: List[bool], kmax: int):
-    """EndlessGraphPipeline's schedule (host logic): the segments as [(start, count, replay), ...] in
-    order -- maximal runs of graph-eligible segments cut into blocks of at most `kmax` (replayed from
-    one captured graph each), every other segment a block of 1 run eagerly."""
-    out, k, n = [], 0, len(graph_ok)
-    while k < n:
-        if not graph_ok[k]:
-            out.append((k, 1, False))
-            k += 1
-            continue
-        m = k
-        while m < n and graph_ok[m]:
-            m += 1
-        while k < m:
-            cnt = min(kmax, m - k)
-            out.append((k, cnt, True))
-            k += cnt
-    return out
+def graph_blocks(n: int, block: int, period: int):
+    """EndlessGraphPipeline's schedule (host logic): the n segments as [(start, count, phase), ...] in
+    order -- consecutive blocks of at most `block` segments, each replayed from one captured graph; a
+    block's graph depends on its first segment's phase start % period (stream, workspace and cache
+    slots cycle with that period) and on its segments' plans."""
+    return [(k0, min(block, n - k0), k0 % period) for k0 in range(0, n, max(1, block))]
 
 
 class EndlessGraphPipeline:
     """endless_decode's segments with `depth` in flight (as EndlessPipeline: segment k on stream
-    k % depth, its layer l waiting only for segment k - 1's layer l) where runs of middle segments are
-    replayed from HIP graphs (BASELINE configs[3]: context caches carried across graph-captured steps,
+    k % depth, its layer l waiting only for segment k - 1's layer l), all of them replayed from HIP
+    graphs (BASELINE configs[3]: context caches carried across graph-captured steps,
     several segments in flight).
 
-    A block of up to `block` (64: a 16 h input at tbd 1800 is one block) consecutive middle segments (the same length and, once offset >= max(L, 7),
-    the same plan: streaming.py's module note) is captured once as ONE graph holding the whole
+    Every segment runs from HIP graphs: a block of up to `block` (128: a 16 h input at tbd 1800, 65
+    segments, is one block) consecutive segments is captured once as ONE graph holding the whole
     multi-stream pipeline of those segments -- every stage call, the per-layer cross-stream event
     edges, the CTC head and the copies of each segment's kept rows / ids into the block's output
-    slots -- and replayed for every later block at the same phase (segment k uses stream, workspace and
-    output slot k % depth and cache pair k % 2, so a block's graph depends on its first segment's
-    phase k mod lcm(depth, 2) and its length).  Inside a replay the segments overlap exactly as in the
-    eager pipeline; a block's first segment starts after the previous block, so the pipeline drains
-    once per block (blocks of 12 at tbd 1800: 21.5 M frames/s against 22.1 M eager -- five drains; a
-    join after every tick of 3 segments: 18.0 M).  The first segments (offset 0), the ragged
-    last one and short runs are launched eagerly through the same calls, so the result is
-    bit-identical to the one-call-per-segment loop."""
+    slots.  Segment k uses stream, workspace and output slot k % depth and cache pair k % 2, so a
+    block's graph is keyed by its first segment's phase k mod lcm(depth, 2) and by its segments'
+    plans (the offset-0 first segment and the ragged last one have their own; the middle ones, once
+    offset >= max(L, 7), share one: streaming.py's module note), lengths and kept rows; the device
+    plans are kept per distinct plan, so a repeated input (or the middle blocks of any input) replays
+    without re-capture.  Inside a replay the segments overlap exactly as in the eager pipeline, with
+    no drain between the first, middle and last segments; a block's first segment starts after the
+    previous block (one drain per block).  The calls are the ones the eager pipeline makes, so the
+    result is bit-identical to the one-call-per-segment loop."""
 
     def __init__(self, encoder, C: int, L: int, R: int, trunc: int, seg_len: int, want_out: bool, depth: int = 3,
-                 block: int = 64, trim: bool = False):
+                 block: int = 128, trim: bool = False):
         if depth < 1:
             raise ValueError(f"pipeline depth {depth} < 1")
         self.enc = encoder
@@ -346,7 +335,7 @@ class EndlessGraphPipeline:
         self.g_ids: List[Optional[torch.Tensor]] = [None] * self.block
         self.g_eo: List[Optional[torch.Tensor]] = [None] * self.block
         self.graphs: dict = {}
-        self.g_plan = None
+        self.plans: dict = {}   # plan bytes -> (host plan, device plan, id): the graphs' plan inputs
         self.vocab = cfg.vocab
         self.replayed = 0   # segments replayed from graphs in the last run (tests / bench)
 
@@ -420,22 +409,17 @@ class EndlessGraphPipeline:
             info.append({"k": k, "x": xs_dev[start:stop], "plan": plan, "N": N, "rows": kept, "keep": keep_trunc,
                          "wsb": int(_lib.cfm_workspace_bytes_masked(enc._h, N, C, L, R)), "len": n_frames})
             offset += kept
-        # the graph plan: the first middle segment whose plan no longer depends on the offset
-        if self.g_plan is None:
-            for s in info:
-                if s["len"] == self.seg_len and sum(s2["rows"] for s2 in info[: s["k"]]) >= max(L, 7):
-                    self.g_plan = s["plan"]
-                    self.g_plan_dev = enc._upload(s["plan"])
-                    self.g_rows = s["rows"]
-                    break
+        # every segment runs from a captured graph: device plans are kept per distinct plan (the middle
+        # segments share one; the first, offset-0 segment and the ragged last one have their own), and a
+        # block's graph is keyed by its phase and its segments' plans / lengths / kept rows, so the middle
+        # blocks of any input and the whole of a same-length input replay without re-capture
         for s in info:
-            s["graph"] = (self.g_plan is not None and s["len"] == self.seg_len and s["rows"] == self.g_rows
-                          and torch.equal(s["plan"], self.g_plan))
-            if s["graph"]:
-                s["plan"], s["plan_dev"] = self.g_plan, self.g_plan_dev
-            else:
-                s["plan_dev"] = enc._upload(s["plan"])
-                s["feats"] = s["x"].contiguous()
+            pk = s["plan"].numpy().tobytes()
+            ent = self.plans.get(pk)
+            if ent is None:
+                ent = (s["plan"], enc._upload(s["plan"]), len(self.plans))
+                self.plans[pk] = ent
+            s["plan"], s["plan_dev"], s["pid"] = ent
         max_rows = max([s["rows"] for s in info] + [1])
         ctc_b = enc.ctc_ws_bytes(max_rows, False) if self.vocab > 0 else 0   # 0 on the fused argmax head
         for p in range(D):   # slot buffers sized for the largest segment
@@ -443,49 +427,30 @@ class EndlessGraphPipeline:
             self._buf(self.out, p, max(s["N"] for s in info) * C * d, torch.float32)
             if ctc_b > 0:
                 self._buf(self.ctc_ws, p, ctc_b, torch.uint8)
-        if self.g_plan is not None:
-            for i in range(self.block):
-                self._buf(self.g_feats, i, self.seg_len * enc.cfg.input_dim, torch.float32)
-                if self.vocab > 0:
-                    self._buf(self.g_ids, i, max(self.g_rows, 1), torch.int32)
-                if self.want_out:
-                    self._buf(self.g_eo, i, max(self.g_rows, 1) * d, torch.float32)
-        for st in self.streams:
-            st.wait_stream(caller)   # inputs, zeroed caches, buffers
+        nblk = min(self.block, n)
+        for i in range(nblk):
+            self._buf(self.g_feats, i, self.seg_len * enc.cfg.input_dim, torch.float32)
+            if self.vocab > 0:
+                self._buf(self.g_ids, i, max_rows, torch.int32)
+            if self.want_out:
+                self._buf(self.g_eo, i, max_rows * d, torch.float32)
         ids_out: List[Optional[torch.Tensor]] = [None] * n
         eo_out: List[Optional[torch.Tensor]] = [None] * n
-        prev = None
-        for k0, cnt, replay in graph_blocks([s["graph"] for s in info], self.block):
-            if not replay:
-                s = info[k0]
-                st = self.streams[k0 % D]
-                ids = eo = None
-                with torch.cuda.stream(st):
-                    if self.vocab > 0 and s["rows"] > 0:
-                        ids = torch.empty(s["rows"], dtype=torch.int32, device=self.dev)
-                    if self.want_out:
-                        eo = torch.empty(s["rows"], d, dtype=torch.float32, device=self.dev)
-                prev = self._segment(s, prev, ids, eo)
-                for t in (ids, eo):
-                    if t is not None:
-                        t.record_stream(caller)
-                ids_out[k0], eo_out[k0] = ids, eo
-                continue
-            # a block: everything before it has finished when the replay starts (one drain)
+        for k0, cnt, phase in graph_blocks(n, self.block, self.period):
+            # a block starts after everything before it (inputs, zeroed caches, the previous block)
             for st in self.streams:
                 caller.wait_stream(st)
             for i in range(cnt):
                 s = info[k0 + i]
                 self.g_feats[i][: s["len"] * enc.cfg.input_dim].view(s["len"], -1).copy_(s["x"])
-            key = (k0 % self.period, cnt)
+            key = (phase, tuple((s["pid"], s["len"], s["rows"], s["keep"]) for s in info[k0: k0 + cnt]))
             entry = self.graphs.get(key)
             if entry is None:
                 g = torch.cuda.CUDAGraph()
                 cap = self.streams[0]
                 cap.wait_stream(caller)
                 # every event recorded inside the capture (the per-layer edges between the streams and the
-                # fork / join) is kept alive with the graph: the captured graph can refer to them, and a
-                # destroyed one was a host crash at a later replay (three models' pipelines in one process)
+                # fork / join) is kept with the graph, which can refer to them
                 keep: List[torch.cuda.Event] = []
 
                 def edge(dst, src):
@@ -510,8 +475,7 @@ class EndlessGraphPipeline:
                 entry = (g, keep)
                 self.graphs[key] = entry
                 caller.wait_stream(cap)
-            g = entry[0]
-            g.replay()
+            entry[0].replay()
             self.replayed += cnt
             for i in range(cnt):
                 rows = info[k0 + i]["rows"]
@@ -521,7 +485,6 @@ class EndlessGraphPipeline:
                     eo_out[k0 + i] = self.g_eo[i][: rows * d].view(rows, d).clone()
             for st in self.streams:
                 st.wait_stream(caller)
-            prev = None   # the next segment's layer waits are covered by the stream order
         for st in self.streams:
             caller.wait_stream(st)
         self._keep = info

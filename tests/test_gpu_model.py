@@ -98,8 +98,8 @@ def test_endless_graph_replay_equals_eager(small, dtype):
     assert eo_g.shape == eo_e.shape
     assert torch.equal(eo_g, eo_e)
     assert torch.equal(ids_g, ids_e)
-    # segments in flight on several streams, eagerly (EndlessPipeline) and with runs of middle segments
-    # replayed as one HIP graph (EndlessGraphPipeline, twice: captured, then reused), at depths
+    # segments in flight on several streams, eagerly (EndlessPipeline) and with every segment
+    # replayed from one HIP graph (EndlessGraphPipeline, twice: captured, then reused), at depths
     # 2, 3 (default) and 4: same rows, ids and caches
     for graph, depth in ((False, 3), (True, 3), (True, 3), (True, 2), (True, 4)):
         ids_p, eo_p = m.endless_decode(x, C, L, R, total_batch_duration=tbd, return_encoder_out=True, pipeline=True,
@@ -110,7 +110,7 @@ def test_endless_graph_replay_equals_eager(small, dtype):
             assert torch.equal(a, b), (graph, depth)
         if graph:
             runner = next(iter(m._endless_runners.values()))
-            assert runner.replayed > 0, depth   # some segments did replay from a graph
+            assert runner.replayed == len(runner._keep) > 0, depth   # every segment replayed from a graph
 
 
 @pytest.mark.parametrize("dtype", ["fp32", "bf16", "fp16"])

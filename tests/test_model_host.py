@@ -127,20 +127,14 @@ def test_cmvn_loaders_agree(tmp_path):
 
 
 def test_endless_graph_blocks_schedule():
-    """EndlessGraphPipeline's schedule (host logic): every segment exactly once, in order; runs of
-    graph-eligible segments cut into replayed blocks of at most kmax, every other segment eager."""
-    import itertools
+    """EndlessGraphPipeline's schedule (host logic): every segment exactly once, in order, in blocks
+    of at most `block`, all full but the last; a block's phase is its first segment's slot phase."""
     from chunkformer_amd.streaming import graph_blocks
-    for n in range(0, 9):
-        for flags in itertools.product([False, True], repeat=n):
-            for kmax in (1, 2, 3, 12):
-                blocks = graph_blocks(list(flags), kmax)
-                covered = [k for k0, cnt, _ in blocks for k in range(k0, k0 + cnt)]
-                assert covered == list(range(n))
-                for k0, cnt, replay in blocks:
-                    assert 1 <= cnt <= (kmax if replay else 1)
-                    assert all(flags[k] == replay for k in range(k0, k0 + cnt))
-                # maximal packing: two adjacent replayed blocks only where the first one is full
-                for (a0, ac, ar), (b0, bc, br) in zip(blocks, blocks[1:]):
-                    if ar and br:
-                        assert ac == kmax
+    for n in range(0, 40):
+        for block in (1, 2, 3, 12, 128):
+            for period in (2, 4, 6):
+                blocks = graph_blocks(n, block, period)
+                assert [k for k0, cnt, _ in blocks for k in range(k0, k0 + cnt)] == list(range(n))
+                assert all(1 <= cnt <= block for _, cnt, _ in blocks)
+                assert all(cnt == block for _, cnt, _ in blocks[:-1])
+                assert all(ph == k0 % period for k0, _, ph in blocks)
