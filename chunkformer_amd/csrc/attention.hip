@@ -254,6 +254,20 @@ CFM_DEV int sw128(int row, int ch) { return row * 128 + ((ch ^ ((row >> 1) & 7))
 #ifndef RING_KPF
 #define RING_KPF 1   // ring kernel, interior chunks: next tile's K fragments read before this tile's skew
 #endif
+#ifndef ATTN_PRIO
+#define ATTN_PRIO 1   // static wave priority: 1 = the second-dispatched half (waves 4-7) at s_setprio 1 (ring attention
+                      // 4.82 -> 4.74 ms/step, tools/ab_prio.sh); 2 = waves 0-3 instead (4.77); 0 = none
+#endif
+// the two halves of an 8-wave block are SIMD partners running the same program (MI355X_MICROARCH.md,
+// "Two waves per SIMD" item 4: a static priority for the arbitration loser)
+CFM_DEV void attn_static_prio(int half) {
+  if constexpr (ATTN_PRIO == 1) { if (half) __builtin_amdgcn_s_setprio(1); }
+  if constexpr (ATTN_PRIO == 2) { if (!half) __builtin_amdgcn_s_setprio(1); }
+  (void)half;
+}
+#ifndef ATTN_STAGGER
+#define ATTN_STAGGER 0   // A/B: waves 4-7 store their output rows one pair late (see the ring kernel)
+#endif
 #ifndef ATTN_STORE16
 #define ATTN_STORE16 1   // ring kernel output as 16-B stores after permlane swaps (A/B: 0 = 8-B stores)
 #endif
@@ -330,6 +344,7 @@ __global__ __launch_bounds__(512, 1) void chunk_attention_ring_kernel(
   __syncthreads();
 
   const int i0 = wq * 16;
+  attn_static_prio(half);
   // masked-batch descriptors (planner.cpp, C <= 64: one query block per chunk): chunk c's queries
   // are rows c*C.., its window starts at flat KV row c*C, P_BASE = C-1, every query row valid;
   // only the key range [lo, hi) varies.  Q fragments and the key range of the wave's NEXT chunk
@@ -349,7 +364,39 @@ __global__ __launch_bounds__(512, 1) void chunk_attention_ring_kernel(
     klo_n = desc[(size_t)cc * AD_INTS + AD_KEY_LO];
     khi_n = desc[(size_t)cc * AD_INTS + AD_KEY_HI];
   }
+  // the output rows of a query group: O^T / l as E, dims 16nt + 4g .. of query row op
+  auto store_out = [&](const f32x4 (&O)[4], float inv, E* op) {
+  #if ATTN_STORE16
+    // dim pairs (16 nt .. +15, 16 (nt+1) ..): one permlane16 swap per packed dword leaves lane g with
+    // 8 contiguous dims, so each query row leaves as two 64-B pieces (2 x 16-B stores per lane)
+#pragma unroll
+    for (int pr = 0; pr < 2; ++pr) {
+      const unsigned x0 = pack_e2<E>(O[2 * pr][0] * inv, O[2 * pr][1] * inv), x1 = pack_e2<E>(O[2 * pr][2] * inv, O[2 * pr][3] * inv);
+      const unsigned y0 = pack_e2<E>(O[2 * pr + 1][0] * inv, O[2 * pr + 1][1] * inv),
+                     y1 = pack_e2<E>(O[2 * pr + 1][2] * inv, O[2 * pr + 1][3] * inv);
+      const auto r0 = __builtin_amdgcn_permlane16_swap(x0, y0, false, false);
+      const auto r1 = __builtin_amdgcn_permlane16_swap(x1, y1, false, false);
+      *reinterpret_cast<u32x4*>(op + 32 * pr + 16 * (g & 1) + 8 * (g >> 1)) = (u32x4){r0[0], r1[0], r0[1], r1[1]};
+    }
+  #else
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      typedef E ex4 __attribute__((ext_vector_type(4)));
+      *reinterpret_cast<ex4*>(op + 16 * nt + 4 * g) =
+          (ex4){(E)(O[nt][0] * inv), (E)(O[nt][1] * inv), (E)(O[nt][2] * inv), (E)(O[nt][3] * inv)};
+    }
+  #endif
+  };
+  // ATTN_STAGGER: waves 4-7 keep their finished O across the staging barriers and store it at the start of
+  // the next pair (offsets the SIMD partners' phases by the epilogue; MI355X_MICROARCH.md item 9)
+  f32x4 Od[4];
+  float invd = 0.f;
+  E* opd = nullptr;
   for (int cp = c0; cp < c1; cp += 2) {
+    if (ATTN_STAGGER && opd) {
+      store_out(Od, invd, opd);
+      opd = nullptr;
+    }
     const int kvp = kvb + (cp - c0) * C;
     const int c = cp + half;
     const bool active = c < c1 && i0 < C && (diag & 15) != 1;
@@ -582,26 +629,14 @@ __global__ __launch_bounds__(512, 1) void chunk_attention_ring_kernel(
         const bool live = qi < q_valid && l > 0.f;
         const float inv = live ? 1.f / l : 0.f;
         E* op = out + (size_t)(q_row0 + qi) * d + h * 64;
-  #if ATTN_STORE16
-        // dim pairs (16 nt .. +15, 16 (nt+1) ..): one permlane16 swap per packed dword leaves lane g with
-        // 8 contiguous dims, so each query row leaves as two 64-B pieces (2 x 16-B stores per lane)
+        if (ATTN_STAGGER && half) {   // waves 4-7: the store leaves after the staging barriers
 #pragma unroll
-        for (int pr = 0; pr < 2; ++pr) {
-          const unsigned x0 = pack_e2<E>(O[2 * pr][0] * inv, O[2 * pr][1] * inv), x1 = pack_e2<E>(O[2 * pr][2] * inv, O[2 * pr][3] * inv);
-          const unsigned y0 = pack_e2<E>(O[2 * pr + 1][0] * inv, O[2 * pr + 1][1] * inv),
-                         y1 = pack_e2<E>(O[2 * pr + 1][2] * inv, O[2 * pr + 1][3] * inv);
-          const auto r0 = __builtin_amdgcn_permlane16_swap(x0, y0, false, false);
-          const auto r1 = __builtin_amdgcn_permlane16_swap(x1, y1, false, false);
-          *reinterpret_cast<u32x4*>(op + 32 * pr + 16 * (g & 1) + 8 * (g >> 1)) = (u32x4){r0[0], r1[0], r0[1], r1[1]};
+          for (int nt = 0; nt < 4; ++nt) Od[nt] = O[nt];
+          invd = inv;
+          opd = op;
+        } else {
+          store_out(O, inv, op);
         }
-  #else
-#pragma unroll
-        for (int nt = 0; nt < 4; ++nt) {
-          typedef E ex4 __attribute__((ext_vector_type(4)));
-          *reinterpret_cast<ex4*>(op + 16 * nt + 4 * g) =
-              (ex4){(E)(O[nt][0] * inv), (E)(O[nt][1] * inv), (E)(O[nt][2] * inv), (E)(O[nt][3] * inv)};
-        }
-  #endif
       };
       if (whole) body(std::false_type{});
       else body(std::true_type{});
@@ -613,6 +648,7 @@ __global__ __launch_bounds__(512, 1) void chunk_attention_ring_kernel(
       if (pf_row[q] >= 0) stage_pair(pf_row[q], pf_ch[q], pk0[q], pv0[q], pk1[q], pv1[q]);
     __syncthreads();
   }
+  if (ATTN_STAGGER && opd) store_out(Od, invd, opd);
 }
 
 // returns -1 when the shape is not eligible for the ring kernel
@@ -769,6 +805,7 @@ __global__ __launch_bounds__(512, 1) void full_attention_bf16_kernel(
   __syncthreads();
 
   const int i0 = wq * 16;
+  attn_static_prio(half);
   const bool active = has && i0 < nq;
   // the block's key tiles (one utterance: uniform), as a compile-time count: the tile loops are
   // straight-line code without per-tile skip branches; only the last tile can need the key mask
