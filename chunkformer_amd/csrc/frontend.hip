@@ -273,6 +273,9 @@ __global__ __launch_bounds__(256, 3) void fe_conv0_dw_mfma_kernel(const float* _
 #ifndef FE2_WAVES
 #define FE2_WAVES 4   // waves (32-channel tiles) per workgroup sharing one im2col build: 4 (2 workgroups per CU) or 8
 #endif
+#ifndef FE2_PRIO
+#define FE2_PRIO 0
+#endif
 #ifndef FE2_STG
 #define FE2_STG 1   // output staging buffers per wave (2: a tile's outputs leave during the next tile; 2.709 vs 2.688 ms)
 #endif
@@ -332,6 +335,11 @@ __global__ __launch_bounds__(FE2_NT, 8 / FE2_WAVES) void fe_conv0_dw_mfma2_kerne
   const int win = blockIdx.z;
   const int P = T2 * FE_F2;
   const int ct = blockIdx.y * FE2_WAVES + wv;   // this wave's 32-channel tile (waves past d only help build)
+  // FE2_PRIO (A/B): static priority for one of a SIMD's two partner waves (MI355X_MICROARCH.md, two waves per
+  // SIMD, item 4): waves 4-7 of an 8-wave workgroup, or the odd channel groups' workgroups
+  if constexpr (FE2_PRIO) {
+    if (FE2_WAVES == 8 ? wv >= 4 : (blockIdx.y & 1) != 0) __builtin_amdgcn_s_setprio(1);
+  }
   const bool active = ct * 32 < d;
   // loop-invariant operands (host-built per-lane fragments, model.hip), loaded first so their latency
   // overlaps the first chunk's input loads: W0 rows (+ b0 at k = 9), the diagonal dw1 fragments, the
