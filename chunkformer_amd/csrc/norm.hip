@@ -11,6 +11,10 @@
 #include "cfm_common.h"
 #include "cfm_kernels.h"
 
+#ifndef LN_Y16
+#define LN_Y16 0   // A/B: 16-bit rows (d = 512) as one 16-B load / store per lane instead of two 8-B ones
+#endif
+
 namespace cfm {
 
 template <int VPL>
@@ -65,6 +69,10 @@ CFM_DEV void store_row(H* p, const float (&v)[VPL]) {   // bf16 / f16 rows
   typedef H h4 __attribute__((ext_vector_type(4)));
   if constexpr (VPL == 2) {
     *reinterpret_cast<h2*>(p) = (h2){(H)v[0], (H)v[1]};
+  } else if constexpr (VPL == 8 && LN_Y16) {   // one 16-B store per lane
+    typedef H h8 __attribute__((ext_vector_type(8)));
+    __builtin_nontemporal_store((h8){(H)v[0], (H)v[1], (H)v[2], (H)v[3], (H)v[4], (H)v[5], (H)v[6], (H)v[7]},
+                                reinterpret_cast<h8*>(p));
   } else {
 #pragma unroll
     for (int e = 0; e < VPL; e += 4) {
@@ -80,6 +88,11 @@ CFM_DEV void load_row(const H* p, float (&v)[VPL]) {
   if constexpr (VPL == 2) {
     const h2 t = *reinterpret_cast<const h2*>(p);
     v[0] = (float)t[0]; v[1] = (float)t[1];
+  } else if constexpr (VPL == 8 && LN_Y16) {   // one 16-B load per lane
+    typedef H h8 __attribute__((ext_vector_type(8)));
+    const h8 t = __builtin_nontemporal_load(reinterpret_cast<const h8*>(p));
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = (float)t[e];
   } else {
 #pragma unroll
     for (int e = 0; e < VPL; e += 4) {
