@@ -405,7 +405,11 @@ class EndlessGraphPipeline:
             n_frames = stop - start
             plan, n_chunks, out_lens = _lib.plan_masked([n_frames], [offset], C, L, R)
             N = n_chunks[0]
-            kept = min(out_lens[0], self.trunc) if keep_trunc else out_lens[0]
+            # rows of out[:n] with Python slice semantics, as the reference's encoder_out[:, :encoder_len]
+            # (chunkformer_model.py:419): a segment of < 15 frames has calc_length -1, which drops the
+            # last row of its one padded chunk instead of returning none (EndlessPipeline: eo[:n])
+            n_rows = len(range(N * C)[: out_lens[0]])
+            kept = min(n_rows, self.trunc) if keep_trunc else n_rows
             info.append({"k": k, "x": xs_dev[start:stop], "plan": plan, "N": N, "rows": kept, "keep": keep_trunc,
                          "wsb": int(_lib.cfm_workspace_bytes_masked(enc._h, N, C, L, R)), "len": n_frames})
             offset += kept

@@ -168,10 +168,11 @@ def layer_masked(x, sd, p, cfg, att_mask, mask_pad, pos, C, L, R, att_cache, cnn
     k = _lin(h, sd, a + "linear_k").view(N * C, H, dk)
     v = _lin(h, sd, a + "linear_v").view(N * C, H, dk)
     cache = att_cache if att_cache is not None else torch.zeros(L, H, 2 * dk)
-    flat = torch.cat([cache, torch.cat([k, v], -1), torch.zeros(R, H, 2 * dk)], 0)
+    flat = torch.cat([cache, torch.cat([k, v], -1)], 0)
     new_att = None
-    if att_cache is not None:
-        new_att = flat[: trunc + L][-L:].clone()
+    if att_cache is not None:   # before the right zero padding (attention.py:466-468): a stream shorter than
+        new_att = flat[: trunc + L][-L:].clone()   # trunc keeps its last L rows, not padding
+    flat = torch.cat([flat, torch.zeros(R, H, 2 * dk)], 0)
     rows = torch.arange(N)[:, None] * C + torch.arange(L + C + R)[None, :]
     win = flat[rows]                                          # [N, W, H, 2dk]
     P = F.linear(pos, sd[a + "linear_pos.weight"]).view(-1, H, dk)
@@ -184,10 +185,11 @@ def layer_masked(x, sd, p, cfg, att_mask, mask_pad, pos, C, L, R, att_cache, cnn
     g = F.linear(h, sd[c + "pointwise_conv1.weight"][:, :, 0], sd[c + "pointwise_conv1.bias"])
     glu = g[..., :d] * torch.sigmoid(g[..., d:])
     cc = cnn_cache.t() if cnn_cache is not None else torch.zeros(LORDER, d)
-    flat = torch.cat([cc, glu.reshape(N * C, d), torch.zeros(LORDER, d)], 0)
+    flat = torch.cat([cc, glu.reshape(N * C, d)], 0)
     new_cnn = None
-    if cnn_cache is not None:
+    if cnn_cache is not None:   # before the zero padding (convolution.py:228-233)
         new_cnn = flat[: trunc + LORDER][-LORDER:].t().contiguous()
+    flat = torch.cat([flat, torch.zeros(LORDER, d)], 0)
     rows = torch.arange(N)[:, None] * C + torch.arange(C + 2 * LORDER)[None, :]
     win = flat[rows] * mask_pad.unsqueeze(-1)                  # [N, C+14, d]
     wdw = sd[c + "depthwise_conv.weight"][:, 0, :]             # [d, 15]

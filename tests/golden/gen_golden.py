@@ -381,6 +381,28 @@ def gen_endless_tbd(path, cfg=SMALL, seed=1):
                         ids=ids.numpy().astype(np.int32), att=ac.numpy(), cnn=cc.numpy())
 
 
+ENDLESS_TAIL_LENS = (897, 900, 910, 911, 918, 1796)
+
+
+def gen_endless_tail(path, cfg=SMALL, seed=1):
+    """endless_decode (tbd 20, C 16, L = R = 32: 896-frame steps) on inputs whose LAST segment is
+    1-22 frames: calc_length of a segment under 15 frames is <= 0 (-1 below 7 frames), and the
+    reference's encoder_out[:, :encoder_len] (chunkformer_model.py:419) then keeps all but the
+    last row of the segment's padded chunk (-1) or nothing (0).  Pins that slicing for every
+    endless mode (a graph-replayed ragged last segment took -1 as a row count)."""
+    enc, ctc, sd = build_reference(cfg, seed)
+    out = {"sd_digest": sd_digest(sd), "seed": np.array(seed), "feat_seed": np.array(13),
+           "clrt": np.array([16, 32, 32, 20], np.int32), "lens": np.array(ENDLESS_TAIL_LENS, np.int32)}
+    with torch.no_grad():
+        for n in ENDLESS_TAIL_LENS:
+            x = feats([n], 13)[0]
+            eo, ids, ac, cc, nseg = endless_reference(enc, ctc, x, 16, 32, 32, tbd=20)
+            out.update({f"out_{n}": eo.numpy(), f"ids_{n}": ids.numpy().astype(np.int32), f"att_{n}": ac.numpy(),
+                        f"cnn_{n}": cc.numpy(), f"nseg_{n}": np.array(nseg)})
+            print(f"endless tail {n}: {nseg} segments, {eo.shape[0]} rows")
+    np.savez_compressed(path, **out)
+
+
 PEAK_SECTORS, PEAK_BLANK, PEAK_SCALE, PEAK_REST = 16, 0.8, 2.0, 0.1
 
 
@@ -664,7 +686,7 @@ def gen_rnnt_memory(path, seed=3, n_steps=64, dir_seed=11):
 
 if __name__ == "__main__":
     which = sys.argv[1:] or ["masks", "small", "large", "large_4h", "large_endless", "large_full", "text", "stream",
-                             "endless_tbd", "rnnt", "rows_neq", "small256", "rnnt_sparse", "rnnt_memory", "autocast"]
+                             "endless_tbd", "rnnt", "rows_neq", "small256", "rnnt_sparse", "rnnt_memory", "autocast", "endless_tail"]
     if "masks" in which:
         gen_masks(os.path.join(HERE, "masks.npz"))
     if "small" in which:
@@ -695,4 +717,6 @@ if __name__ == "__main__":
         gen_rnnt_memory(os.path.join(HERE, "rnnt_memory.npz"))
     if "autocast" in which:
         gen_autocast(os.path.join(HERE, "autocast.npz"))
+    if "endless_tail" in which:
+        gen_endless_tail(os.path.join(HERE, "endless_tail.npz"))
     print("ok", which)

@@ -113,6 +113,62 @@ def test_endless_graph_replay_equals_eager(small, dtype):
             assert runner.replayed == len(runner._keep) > 0, depth   # every segment replayed from a graph
 
 
+def test_endless_tiny_last_segment_matches_reference(small, golden_dir):
+    """A last endless segment of 1-22 frames (calc_length <= 0) in every endless mode, fp32, against
+    the reference (endless_tail.npz): the rows the reference's Python slice out[:encoder_len] keeps
+    (all but one row of the padded chunk at -1, none at 0), ids and final caches."""
+    from chunkformer_amd.model import ChunkFormerModel
+    from chunkformer_amd.config import SMALL
+    from chunkformer_amd.weights import synthetic_features, synthetic_state_dict
+    g = np.load(os.path.join(golden_dir, "endless_tail.npz"))
+    m = ChunkFormerModel(SMALL, synthetic_state_dict(SMALL, int(g["seed"])), dtype="fp32")
+    C, L, R, tbd = (int(v) for v in g["clrt"])
+    for n in g["lens"].tolist():
+        x = synthetic_features([n], int(g["feat_seed"]))[0]
+        for graph, pipe in ((False, False), (True, False), (False, True), (True, True)):
+            ids, eo = m.endless_decode(x, C, L, R, total_batch_duration=tbd, return_encoder_out=True, cuda_graph=graph,
+                                       pipeline=pipe)
+            eo = eo[0].cpu().numpy()
+            assert eo.shape == g[f"out_{n}"].shape, (n, graph, pipe)
+            np.testing.assert_allclose(eo, g[f"out_{n}"], atol=1e-4, rtol=0, err_msg=str((n, graph, pipe)))
+            assert (ids.reshape(-1).cpu().numpy() == g[f"ids_{n}"]).mean() >= 0.99, (n, graph, pipe)
+            att, cnn = m.last_endless_caches
+            np.testing.assert_allclose(att.cpu().numpy(), g[f"att_{n}"], atol=1e-4, rtol=0)
+            np.testing.assert_allclose(cnn.cpu().numpy(), g[f"cnn_{n}"], atol=1e-4, rtol=0)
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "fp32"])
+def test_endless_graph_pipeline_lengths(small, dtype):
+    """The graph-replayed pipeline over inputs of several lengths in a row on one model (streaming.py:
+    every segment -- the offset-0 first one, the shared middle plan, the ragged last one -- from captured
+    graphs keyed by their plans / lengths / kept rows; buffers growing and the old graphs retired):
+    each call bit-identical to the one-segment-at-a-time eager loop, a repeated length replaying
+    without a new capture, and every segment replayed from a graph."""
+    from chunkformer_amd.weights import synthetic_features
+    g, models = small
+    C, L, R, tbd = (int(v) for v in g["endless_clrt"])
+    m = models[dtype]
+    # a 4-frame last segment (900: calc_length -1, the reference keeps 15 rows of its padded chunk), three
+    # segments, a ragged tail, the fixture length, a longer one, then lengths again
+    seen = {}
+    for depth in (4, 3):
+        for n, seed in ((900, 1), (2100, 2), (4050, 3), (6000, 4), (9000, 5), (4050, 7), (6000, 6)):
+            x = synthetic_features([n], seed)[0]
+            ids_e, eo_e = m.endless_decode(x, C, L, R, total_batch_duration=tbd, return_encoder_out=True,
+                                           cuda_graph=False, pipeline=False)
+            ca_e = [c.clone() for c in m.last_endless_caches]
+            ids_p, eo_p = m.endless_decode(x, C, L, R, total_batch_duration=tbd, return_encoder_out=True,
+                                           pipeline=True, cuda_graph=True, pipeline_depth=depth)
+            assert torch.equal(eo_p, eo_e), (n, depth)
+            assert torch.equal(ids_p, ids_e), (n, depth)
+            for a_, b_ in zip(m.last_endless_caches, ca_e):
+                assert torch.equal(a_, b_), (n, depth)
+            runner = next(iter(m._endless_runners.values()))
+            assert runner.replayed == len(runner._keep) > 0, (n, depth)
+            if (depth, n) in seen:   # the same length again: its graphs are reused, none captured
+                assert len(runner.graphs) == seen[(depth, n)], (n, depth)
+            seen[(depth, n)] = len(runner.graphs)
+
 @pytest.mark.parametrize("dtype", ["fp32", "bf16", "fp16"])
 def test_endless_decode_larger_segments_match_reference(small, golden_dir, dtype):
     """The same input with total_batch_duration 80 (2 segments; the bench runs configs[3] with

@@ -197,6 +197,23 @@ def oracle_endless(sd, cfg, x, C, L, R, tbd):
     return torch.cat(outs), ac, cc, len(segs)
 
 
+def test_endless_tiny_last_segment_matches_reference(golden_dir):
+    """Inputs whose last endless segment is 1-22 frames (calc_length <= 0): the reference keeps
+    out[:encoder_len] with Python slicing, i.e. all but the last row of the padded chunk at -1
+    (endless_tail.npz, from the reference)."""
+    from chunkformer_amd.weights import synthetic_features
+    g = _load(golden_dir, "endless_tail.npz")
+    sd = synthetic_state_dict(SMALL, int(g["seed"]))
+    C, L, R, tbd = (int(v) for v in g["clrt"])
+    for n in g["lens"].tolist():
+        x = synthetic_features([n], int(g["feat_seed"]))[0]
+        eo, ac, cc, nseg = oracle_endless(sd, SMALL, x, C, L, R, tbd)
+        assert nseg == int(g[f"nseg_{n}"]), n
+        np.testing.assert_allclose(eo.numpy(), g[f"out_{n}"], atol=2e-5, rtol=0, err_msg=str(n))
+        np.testing.assert_allclose(ac.numpy(), g[f"att_{n}"], atol=2e-5, rtol=0, err_msg=str(n))
+        np.testing.assert_allclose(cc.numpy(), g[f"cnn_{n}"], atol=2e-5, rtol=0, err_msg=str(n))
+
+
 def test_large_endless_matches_reference(golden_dir):
     """configs[3] geometry (C=64, L=R=128, 12 layers), >= 3 segments with caches carried."""
     g = _load(golden_dir, "large_endless.npz")
