@@ -415,12 +415,17 @@ class ChunkFormerModel:
             lens = torch.tensor([x.shape[0] for x in xs], dtype=torch.int)
             offset = torch.zeros(len(xs), dtype=torch.int)
             eo, el, n_chunks, _, _, _ = self.encoder.forward_parallel_chunk(xs, lens, C, L, R, offset=offset)
+            # per-utterance rows as the reference slices them: hyp.flatten()[:x_len] (Python slice: an
+            # utterance under 7 frames has calc_length -1 and keeps all but the last row of its padded
+            # chunk) and, for the transducer, frames t < encoder_out_lens (none at <= 0)
+            el_ctc = [len(range(int(nc) * C)[: int(n)]) for nc, n in zip(n_chunks, el.tolist())]
+            el_rnnt = [max(0, int(n)) for n in el.tolist()]
             if self.model_type == "transducer":
                 # batch_greedy_search over each utterance's rows (chunkformer_model.py:533-543): the
                 # packed rows go straight in (no pad_sequence), one workgroup per utterance
                 starts = (np.cumsum([0] + list(n_chunks[:-1])) * C).tolist()
-                dense = self.rnnt.greedy_packed(eo.reshape(-1, eo.shape[-1]), starts, el.tolist()).cpu()
-                hyps = [dense[s0: s0 + int(n)].reshape(-1) for s0, n in zip(starts, el.tolist())]
+                dense = self.rnnt.greedy_packed(eo.reshape(-1, eo.shape[-1]), starts, el_rnnt).cpu()
+                hyps = [dense[s0: s0 + n].reshape(-1) for s0, n in zip(starts, el_rnnt)]
                 hyps = [h[h != self.rnnt.cfg.blank].tolist() for h in hyps]
                 if self.char_dict is not None:
                     decodes.extend(class2str(h, self.char_dict).strip() for h in hyps)
@@ -431,10 +436,10 @@ class ChunkFormerModel:
             if self.char_dict is not None:
                 # remove_duplicates_and_blank on the device, per utterance rows [64 * chunk0, +len)
                 starts = np.cumsum([0] + list(n_chunks[:-1])) * C
-                toks = self.encoder.ctc_collapse(hyp, starts.tolist(), el.tolist())
+                toks = self.encoder.ctc_collapse(hyp, starts.tolist(), el_ctc)
                 decodes.extend(class2str(t, self.char_dict).strip() for t, _ in toks)
             else:
-                decodes.extend(h.flatten()[: int(n)].long() for h, n in zip(hyp.split(n_chunks, dim=0), el.tolist()))
+                decodes.extend(h.flatten()[:n].long() for h, n in zip(hyp.split(n_chunks, dim=0), el_ctc))
         return decodes
 
 

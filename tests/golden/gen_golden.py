@@ -381,6 +381,43 @@ def gen_endless_tbd(path, cfg=SMALL, seed=1):
                         ids=ids.numpy().astype(np.int32), att=ac.numpy(), cnn=cc.numpy())
 
 
+TINY_BATCH_LENS = (5, 300, 3, 14, 15, 700, 6, 7)
+
+
+def gen_tiny_batch(path, cfg=SMALL, seed=1):
+    """batch_decode's asr branch (chunkformer_model.py:524-531) on a batch with utterances of 3-15
+    frames: calc_length -1 (< 7 frames) makes hyp.flatten()[:x_len] keep all but the last id of the
+    padded chunk, 0 keeps none; the ids and the get_output strings (model_utils.py:164-171, vocabulary
+    synthetic_vocab) of every utterance."""
+    ta = types.ModuleType("torchaudio")
+    taf = types.ModuleType("torchaudio.functional")
+    ta.functional = taf
+    sys.modules.setdefault("torchaudio", ta)
+    sys.modules.setdefault("torchaudio.functional", taf)
+    from chunkformer.utils import model_utils as mu
+    enc, ctc, sd = build_reference(cfg, seed)
+    lens = list(TINY_BATCH_LENS)
+    xs = feats(lens, 29)
+    with torch.no_grad():
+        eo, el, n_chunks, _, _, _ = enc.forward_parallel_chunk(
+            xs=xs, xs_origin_lens=torch.tensor(lens, dtype=torch.int), chunk_size=16, left_context_size=32,
+            right_context_size=32, offset=torch.zeros(len(lens), dtype=torch.int))
+        logp = ctc.log_softmax(eo)
+        hyps = torch.argmax(logp, dim=-1).split(n_chunks, dim=0)
+        hyps = [h.flatten()[:n] for h, n in zip(hyps, el)]
+        top2 = logp.topk(2, dim=-1).values
+        margin = (top2[..., 0] - top2[..., 1]).split(n_chunks, dim=0)
+        margin = [m.flatten()[:n] for m, n in zip(margin, el)]
+    texts = mu.get_output(hyps, synthetic_vocab(cfg.vocab), "asr_model")
+    np.savez_compressed(path, sd_digest=sd_digest(sd), seed=np.array(seed), feat_seed=np.array(29),
+                        clr=np.array([16, 32, 32], np.int32), lens=np.array(lens, np.int32),
+                        outlens=el.numpy().astype(np.int32), nchunks=np.array(n_chunks, np.int32),
+                        hyp_lens=np.array([h.numel() for h in hyps], np.int32),
+                        hyps=torch.cat(hyps).numpy().astype(np.int32), margins=torch.cat(margin).numpy(),
+                        texts=np.array(texts))
+    print("tiny batch:", el.tolist(), [h.numel() for h in hyps], texts)
+
+
 ENDLESS_TAIL_LENS = (897, 900, 910, 911, 918, 1796)
 
 
@@ -686,7 +723,7 @@ def gen_rnnt_memory(path, seed=3, n_steps=64, dir_seed=11):
 
 if __name__ == "__main__":
     which = sys.argv[1:] or ["masks", "small", "large", "large_4h", "large_endless", "large_full", "text", "stream",
-                             "endless_tbd", "rnnt", "rows_neq", "small256", "rnnt_sparse", "rnnt_memory", "autocast", "endless_tail"]
+                             "endless_tbd", "rnnt", "rows_neq", "small256", "rnnt_sparse", "rnnt_memory", "autocast", "endless_tail", "tiny_batch"]
     if "masks" in which:
         gen_masks(os.path.join(HERE, "masks.npz"))
     if "small" in which:
@@ -719,4 +756,6 @@ if __name__ == "__main__":
         gen_autocast(os.path.join(HERE, "autocast.npz"))
     if "endless_tail" in which:
         gen_endless_tail(os.path.join(HERE, "endless_tail.npz"))
+    if "tiny_batch" in which:
+        gen_tiny_batch(os.path.join(HERE, "tiny_batch.npz"))
     print("ok", which)

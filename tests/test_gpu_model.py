@@ -137,6 +137,30 @@ def test_endless_tiny_last_segment_matches_reference(small, golden_dir):
             np.testing.assert_allclose(cnn.cpu().numpy(), g[f"cnn_{n}"], atol=1e-4, rtol=0)
 
 
+def test_batch_decode_tiny_utterances_matches_reference(small, golden_dir):
+    """batch_decode with utterances of 3-15 frames (tiny_batch.npz): the reference's per-utterance
+    rows hyp.flatten()[:x_len] (calc_length -1 keeps all but the last id of the padded chunk, 0 none),
+    as ids and as get_output strings (fp32)."""
+    from chunkformer_amd.weights import synthetic_features, synthetic_vocab
+    g = np.load(os.path.join(golden_dir, "tiny_batch.npz"))
+    m = small[1]["fp32"]
+    C, L, R = (int(v) for v in g["clr"])
+    xs = synthetic_features(g["lens"].tolist(), int(g["feat_seed"]))
+    exp = np.split(g["hyps"], np.cumsum(g["hyp_lens"])[:-1])
+    mg = np.split(g["margins"], np.cumsum(g["hyp_lens"])[:-1])
+    saved = m.char_dict
+    try:
+        m.char_dict = None
+        hyps = m.batch_decode(xs, C, L, R, total_batch_duration=1800)
+        assert [h.numel() for h in hyps] == g["hyp_lens"].tolist()
+        for h, e, mm in zip(hyps, exp, mg):
+            assert (h.cpu().numpy()[mm > 1e-4] == e[mm > 1e-4]).all()
+        m.char_dict = synthetic_vocab(m.config.vocab)
+        assert m.batch_decode(xs, C, L, R, total_batch_duration=1800) == g["texts"].tolist()
+    finally:
+        m.char_dict = saved
+
+
 @pytest.mark.parametrize("dtype", ["bf16", "fp32"])
 def test_endless_graph_pipeline_lengths(small, dtype):
     """The graph-replayed pipeline over inputs of several lengths in a row on one model (streaming.py:

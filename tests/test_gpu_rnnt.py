@@ -182,6 +182,13 @@ def test_transducer_checkpoint_batch_and_endless(tmp_path, golden_dir, rnnt):
     assert m.batch_decode(xs, 64, 128, 128) == [class2str(h, cd).strip() for h in hyps]
     m.char_dict = None
     assert [list(h) for h in m.batch_decode(xs, 64, 128, 128)] == [h.tolist() for h in hyps]
+    # utterances of 5 / 3 / 14 frames in the same batch (calc_length -1 / -1 / 0): the reference's
+    # optimized_search takes frames t < encoder_out_lens, so they decode to nothing, and the other
+    # utterances' hyps do not change (batch composition)
+    tiny = synthetic_features([5, 3, 14], 3)
+    mixed = m.batch_decode([tiny[0], xs[0], tiny[1]] + list(xs[1:]) + [tiny[2]], 64, 128, 128)
+    assert mixed[0] == [] and mixed[2] == [] and mixed[-1] == []
+    assert [list(h) for h in [mixed[1]] + mixed[3:-1]] == [h.tolist() for h in hyps]
     n = int(g["n_steps"])
     tok = m.endless_decode(xs[0], 64, 128, 128, total_batch_duration=1800)
     T0 = int(g["batch_lens"][0])

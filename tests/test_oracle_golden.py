@@ -214,6 +214,30 @@ def test_endless_tiny_last_segment_matches_reference(golden_dir):
         np.testing.assert_allclose(cc.numpy(), g[f"cnn_{n}"], atol=2e-5, rtol=0, err_msg=str(n))
 
 
+def test_tiny_utterances_batch_matches_reference(golden_dir):
+    """batch_decode on utterances of 3-15 frames (tiny_batch.npz): n_chunks / calc_length (-1 below 7
+    frames) from the oracle, the reference's hyp.flatten()[:x_len] rows (all but one id of the padded
+    chunk at -1) from the oracle's CTC argmax, and the get_output strings from chunkformer_amd's host
+    get_output on the reference's own ids."""
+    from chunkformer_amd.model import get_output
+    from chunkformer_amd.weights import synthetic_vocab
+    g = _load(golden_dir, "tiny_batch.npz")
+    sd = synthetic_state_dict(SMALL, int(g["seed"]))
+    C, L, R = (int(v) for v in g["clr"])
+    lens = g["lens"].tolist()
+    xs = synthetic_features(lens, int(g["feat_seed"]))
+    out, olens, nch, _, _, _ = ref.forward_parallel_chunk(sd, SMALL, xs, lens, C, L, R)
+    assert olens.tolist() == g["outlens"].tolist() and list(nch) == g["nchunks"].tolist()
+    ids = ref.ctc_log_softmax(sd, out).argmax(-1).split(list(nch), dim=0)
+    hyps = [h.flatten()[: int(n)] for h, n in zip(ids, olens)]
+    assert [h.numel() for h in hyps] == g["hyp_lens"].tolist()
+    exp = np.split(g["hyps"], np.cumsum(g["hyp_lens"])[:-1])
+    mg = np.split(g["margins"], np.cumsum(g["hyp_lens"])[:-1])
+    for h, e, m in zip(hyps, exp, mg):
+        assert (h.numpy()[m > 1e-4] == e[m > 1e-4]).all()
+    assert get_output(exp, synthetic_vocab(SMALL.vocab)) == g["texts"].tolist()
+
+
 def test_large_endless_matches_reference(golden_dir):
     """configs[3] geometry (C=64, L=R=128, 12 layers), >= 3 segments with caches carried."""
     g = _load(golden_dir, "large_endless.npz")
