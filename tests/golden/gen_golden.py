@@ -381,6 +381,27 @@ def gen_endless_tbd(path, cfg=SMALL, seed=1):
                         ids=ids.numpy().astype(np.int32), att=ac.numpy(), cnn=cc.numpy())
 
 
+def gen_tiny_padded(path, cfg=SMALL, seed=1):
+    """The padded path (forward_encoder, chunked and full attention) on a batch with 5- and 3-frame
+    utterances (calc_length -1: a mask with no valid frame, every attention row of theirs fully masked)."""
+    enc, ctc, sd = build_reference(cfg, seed)
+    lens = [300, 5, 17, 3]
+    xs = feats(lens, 23)
+    xp = torch.zeros(len(lens), max(lens), 80)
+    for i, t in enumerate(xs):
+        xp[i, : t.shape[0]] = t
+    out = {"sd_digest": sd_digest(sd), "seed": np.array(seed), "feat_seed": np.array(23),
+           "lens": np.array(lens, np.int32)}
+    with torch.no_grad():
+        for name, (C, L, R) in {"pc": (16, 32, 32), "pf": (0, 0, 0)}.items():
+            y, masks = enc.forward_encoder(xp, torch.tensor(lens), C, L, R)
+            out[f"{name}_clr"] = np.array([C, L, R], np.int32)
+            out[f"{name}_out"] = y.numpy()
+            out[f"{name}_mask"] = masks.numpy()
+            print(name, tuple(y.shape), masks.squeeze(1).sum(-1).tolist(), bool(torch.isfinite(y).all()))
+    np.savez_compressed(path, **out)
+
+
 TINY_BATCH_LENS = (5, 300, 3, 14, 15, 700, 6, 7)
 
 
@@ -723,7 +744,7 @@ def gen_rnnt_memory(path, seed=3, n_steps=64, dir_seed=11):
 
 if __name__ == "__main__":
     which = sys.argv[1:] or ["masks", "small", "large", "large_4h", "large_endless", "large_full", "text", "stream",
-                             "endless_tbd", "rnnt", "rows_neq", "small256", "rnnt_sparse", "rnnt_memory", "autocast", "endless_tail", "tiny_batch"]
+                             "endless_tbd", "rnnt", "rows_neq", "small256", "rnnt_sparse", "rnnt_memory", "autocast", "endless_tail", "tiny_batch", "tiny_padded"]
     if "masks" in which:
         gen_masks(os.path.join(HERE, "masks.npz"))
     if "small" in which:
@@ -758,4 +779,6 @@ if __name__ == "__main__":
         gen_endless_tail(os.path.join(HERE, "endless_tail.npz"))
     if "tiny_batch" in which:
         gen_tiny_batch(os.path.join(HERE, "tiny_batch.npz"))
+    if "tiny_padded" in which:
+        gen_tiny_padded(os.path.join(HERE, "tiny_padded.npz"))
     print("ok", which)

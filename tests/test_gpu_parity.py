@@ -133,6 +133,31 @@ def test_padded_path(cfm, small_models, small_g, case, dtype):
         assert _rel_l2(o, g[f"{case}_out"]) <= RELL2[dtype]
 
 
+@pytest.mark.parametrize("case", ["pc", "pf"])
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_padded_path_tiny_utterances(cfm, small_models, small_g, golden_dir, case, dtype):
+    """The padded path with 5- and 3-frame utterances in the batch (tiny_padded.npz: calc_length -1,
+    masks without a valid frame, their attention rows fully masked -> the reference's NaN -> 0)."""
+    from chunkformer_amd.weights import synthetic_features
+    g = np.load(os.path.join(golden_dir, "tiny_padded.npz"))
+    assert int(g["seed"]) == int(small_g["seed"])
+    enc = small_models[dtype]
+    lens = g["lens"].tolist()
+    C, L, R = (int(v) for v in g[f"{case}_clr"])
+    xs = synthetic_features(lens, int(g["feat_seed"]))
+    xp = torch.zeros(len(lens), max(lens), 80)
+    for i, t in enumerate(xs):
+        xp[i, : t.shape[0]] = t
+    out, masks = enc.forward_encoder(xp, torch.tensor(lens), C, L, R)
+    np.testing.assert_array_equal(masks.cpu().numpy(), g[f"{case}_mask"])
+    o = out.cpu().numpy()
+    assert np.isfinite(o).all()
+    if dtype == "fp32":
+        np.testing.assert_allclose(o, g[f"{case}_out"], atol=FP32_ATOL, rtol=0)
+    else:
+        assert _rel_l2(o, g[f"{case}_out"]) <= RELL2[dtype]
+
+
 @pytest.fixture(scope="module")
 def large(cfm, golden_dir):
     from chunkformer_amd.config import LARGE

@@ -86,6 +86,22 @@ def test_padded_path_matches_reference(small, case):
     np.testing.assert_allclose(out.numpy(), g[f"{case}_out"], atol=2e-5, rtol=0)
 
 
+@pytest.mark.parametrize("case", ["pc", "pf"])
+def test_padded_path_tiny_utterances_matches_reference(golden_dir, case):
+    """tiny_padded.npz: 5- and 3-frame utterances (calc_length -1) in a padded batch."""
+    g = _load(golden_dir, "tiny_padded.npz")
+    sd = synthetic_state_dict(SMALL, int(g["seed"]))
+    lens = g["lens"].tolist()
+    C, L, R = (int(v) for v in g[f"{case}_clr"])
+    xs = synthetic_features(lens, int(g["feat_seed"]))
+    xp = torch.zeros(len(lens), max(lens), 80)
+    for i, t in enumerate(xs):
+        xp[i, : t.shape[0]] = t
+    out, masks = ref.forward_encoder(sd, SMALL, xp, lens, C, L, R)
+    np.testing.assert_array_equal(masks.numpy(), g[f"{case}_mask"])
+    np.testing.assert_allclose(out.numpy(), g[f"{case}_out"], atol=2e-5, rtol=0)
+
+
 def test_large_matches_reference(golden_dir):
     g = _load(golden_dir, "large.npz")
     sd = synthetic_state_dict(LARGE, int(g["seed"]))
