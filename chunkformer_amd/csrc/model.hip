@@ -192,6 +192,7 @@ struct ModelT : public cfm_model {
     const size_t per = (size_t)T2 * 19 * cfg.d_model * sizeof(T);
     int g = (int)std::max<size_t>(1, ((size_t)768 << 20) / per);
     if (fe_group_windows > 0) g = std::min(g, fe_group_windows);
+    g = std::min(g, 65535);   // the front-end kernels put a group's windows on gridDim.y / .z
     return std::min(g, h[PH_NWIN]);
   }
 
