@@ -268,3 +268,70 @@ def test_rows_differ_from_origin_lens(golden_dir, dtype):
         else:
             o = out.cpu().numpy().astype(np.float64)
             assert np.linalg.norm(o - g[pre + "out"]) / np.linalg.norm(g[pre + "out"]) <= 2e-2, pre
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_random_batches_match_oracle(cfm, small_models, seed):
+    """Seeded random masked batches (1-40 utterances of 1-2500 frames, random chunk / context sizes,
+    random offsets and carried caches) through the fp32 path against the oracle restatement
+    (oracle/encoder_ref.py, itself pinned by the reference fixtures): outputs at 1e-4, lengths,
+    chunk counts and the new caches."""
+    from oracle import encoder_ref as ref
+    from chunkformer_amd.config import SMALL
+    from chunkformer_amd.weights import synthetic_features, synthetic_state_dict
+    rng = np.random.default_rng(1000 + seed)
+    B = int(rng.integers(1, 41))
+    lens = [int(v) for v in np.minimum(rng.pareto(1.2, B) * 120 + 1, 2500).astype(int)]
+    C = int(rng.choice([4, 8, 16, 24, 32, 64]))
+    L, R = int(rng.choice([0, 8, 16, 40, 64])), int(rng.choice([0, 8, 16, 40, 64]))
+    caches = B == 1 or seed % 4 == 3
+    if caches:   # the cache path is single-utterance (endless_decode / forward_parallel_chunk with caches)
+        lens, L = lens[:1], max(L, 16)
+    xs = synthetic_features(lens, 500 + seed)
+    enc = small_models["fp32"]
+    sd = synthetic_state_dict(SMALL, 1)
+    kw, rkw = {}, {}
+    if caches:
+        g = torch.Generator().manual_seed(seed)
+        ac = torch.randn(SMALL.num_blocks, L, SMALL.n_heads, 2 * SMALL.head_dim, generator=g) * 0.5
+        cc = torch.randn(SMALL.num_blocks, SMALL.d_model, SMALL.conv_lorder, generator=g) * 0.5
+        off = int(rng.integers(0, 300))
+        trunc = C * int(rng.integers(1, 4))
+        kw = dict(att_cache=ac, cnn_cache=cc, truncated_context_size=trunc, offset=torch.tensor([off]))
+        rkw = dict(att_cache=ac, cnn_cache=cc, truncated_context_size=trunc, offset=[off])
+    out, olens, nch, ra, rc, _ = enc.forward_parallel_chunk(xs, torch.tensor(lens, dtype=torch.int32), C, L, R, **kw)
+    eo, el, enc_n, era, erc, _ = ref.forward_parallel_chunk(sd, SMALL, xs, lens, C, L, R, **rkw)
+    assert nch == list(enc_n) and olens.tolist() == el.tolist(), (B, C, L, R)
+    np.testing.assert_allclose(out.cpu().numpy(), eo.numpy(), atol=FP32_ATOL, rtol=0, err_msg=str((B, C, L, R)))
+    if caches:
+        np.testing.assert_allclose(ra.cpu().numpy(), era.numpy(), atol=FP32_ATOL, rtol=0)
+        np.testing.assert_allclose(rc.cpu().numpy(), erc.numpy(), atol=FP32_ATOL, rtol=0)
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_random_large_batches_match_oracle(cfm, large, seed):
+    """chunkformer-large (the fast kernels: ring attention, weight-stationary GEMMs, channel-stationary
+    front-end) on seeded random masked batches with random C in {16..64}, L, R in {0..128}: fp32 at
+    1e-4, bf16 and fp16 at their rel-L2 bars, against the oracle."""
+    from oracle import encoder_ref as ref
+    from chunkformer_amd.config import LARGE
+    from chunkformer_amd.weights import synthetic_features, synthetic_state_dict
+    g, models = large
+    rng = np.random.default_rng(2000 + seed)
+    B = int(rng.integers(1, 13))
+    lens = [int(v) for v in rng.integers(1, 1500, B)]
+    C = int(rng.choice([16, 32, 48, 64]))
+    L, R = int(rng.choice([0, 32, 64, 128])), int(rng.choice([0, 32, 64, 128]))
+    xs = synthetic_features(lens, 700 + seed)
+    sd = synthetic_state_dict(LARGE, int(g["seed"]))
+    eo, el, enc_n, _, _, _ = ref.forward_parallel_chunk(sd, LARGE, xs, lens, C, L, R)
+    exp = eo.numpy()
+    for dt in ("fp32", "bf16", "fp16"):
+        out, olens, nch, _, _, _ = models[dt].forward_parallel_chunk(xs, torch.tensor(lens, dtype=torch.int32), C, L, R)
+        assert nch == list(enc_n) and olens.tolist() == el.tolist()
+        o = out.cpu().numpy()
+        assert np.isfinite(o).all()
+        if dt == "fp32":
+            np.testing.assert_allclose(o, exp, atol=FP32_ATOL, rtol=0, err_msg=str((B, C, L, R)))
+        else:
+            assert _rel_l2(o, exp) <= RELL2[dt], (dt, B, C, L, R)
