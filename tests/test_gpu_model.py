@@ -244,3 +244,29 @@ def test_endless_trim_equals_full(small, dtype):
                 assert torch.equal(a, b), (graph, pipe)
     finally:
         m.endless_trim = True
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_random_endless_matches_oracle(small, seed):
+    """endless_decode on seeded random lengths, total_batch_duration and chunk / context sizes, in the
+    default mode (graph-replayed pipeline from 3 segments up) and the eager loop, fp32 against the
+    oracle's segment loop (tests/test_oracle_golden.py:oracle_endless): rows at 1e-4, final caches."""
+    from test_oracle_golden import oracle_endless
+    from chunkformer_amd.config import SMALL
+    from chunkformer_amd.weights import synthetic_features, synthetic_state_dict
+    rng = np.random.default_rng(4000 + seed)
+    n = int(rng.integers(200, 9000))
+    tbd = int(rng.choice([6, 10, 20, 35]))
+    C = int(rng.choice([8, 16, 32]))
+    L, R = int(rng.choice([8, 16, 32])), int(rng.choice([0, 8, 16, 32]))
+    x = synthetic_features([n], 1100 + seed)[0]
+    m = small[1]["fp32"]
+    exp, ac, cc, nseg = oracle_endless(synthetic_state_dict(SMALL, 1), SMALL, x, C, L, R, tbd)
+    for kw in ({}, dict(cuda_graph=False, pipeline=False), dict(cuda_graph=True, pipeline=True)):
+        _, eo = m.endless_decode(x, C, L, R, total_batch_duration=tbd, return_encoder_out=True, **kw)
+        assert eo.shape[1] == exp.shape[0], (n, tbd, C, L, R, nseg, kw)
+        np.testing.assert_allclose(eo[0].cpu().numpy(), exp.numpy(), atol=1e-4, rtol=0,
+                                   err_msg=str((n, tbd, C, L, R, nseg, kw)))
+        att, cnn = m.last_endless_caches
+        np.testing.assert_allclose(att.cpu().numpy(), ac.numpy(), atol=1e-4, rtol=0)
+        np.testing.assert_allclose(cnn.cpu().numpy(), cc.numpy(), atol=1e-4, rtol=0)

@@ -335,3 +335,26 @@ def test_random_large_batches_match_oracle(cfm, large, seed):
             np.testing.assert_allclose(o, exp, atol=FP32_ATOL, rtol=0, err_msg=str((B, C, L, R)))
         else:
             assert _rel_l2(o, exp) <= RELL2[dt], (dt, B, C, L, R)
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_random_padded_batches_match_oracle(cfm, small_models, seed):
+    """The padded path (forward_encoder) on seeded random batches: chunked (random C, L, R) and full
+    attention, utterances of 1-1500 frames, fp32 at 1e-4 and the masks exact, against the oracle."""
+    from oracle import encoder_ref as ref
+    from chunkformer_amd.config import SMALL
+    from chunkformer_amd.weights import synthetic_features, synthetic_state_dict
+    rng = np.random.default_rng(3000 + seed)
+    B = int(rng.integers(1, 9))
+    lens = [int(v) for v in rng.integers(1, 1500, B)]
+    C = 0 if seed % 4 == 0 else int(rng.choice([4, 8, 16, 32]))
+    L, R = (0, 0) if C == 0 else (int(rng.choice([0, 8, 16, 40])), int(rng.choice([0, 8, 16, 40])))
+    xs = synthetic_features(lens, 900 + seed)
+    xp = torch.zeros(B, max(lens), 80)
+    for i, t in enumerate(xs):
+        xp[i, : t.shape[0]] = t
+    sd = synthetic_state_dict(SMALL, 1)
+    y, masks = ref.forward_encoder(sd, SMALL, xp, lens, C, L, R)
+    out, m = small_models["fp32"].forward_encoder(xp, torch.tensor(lens), C, L, R)
+    np.testing.assert_array_equal(m.cpu().numpy(), masks.numpy())
+    np.testing.assert_allclose(out.cpu().numpy(), y.numpy(), atol=FP32_ATOL, rtol=0, err_msg=str((B, C, L, R)))
