@@ -95,3 +95,36 @@ def test_forward_chunk_matches_oracle_offsets():
         np.testing.assert_allclose(y.cpu().numpy(), ry.numpy(), atol=1e-4, rtol=0, err_msg=str((C, L, R, off)))
         np.testing.assert_allclose(a2.cpu().numpy(), ra.numpy(), atol=1e-4, rtol=0)
         np.testing.assert_allclose(c2.cpu().numpy(), rc.numpy(), atol=1e-4, rtol=0)
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_forward_chunk_random_matches_oracle(seed):
+    """forward_chunk on seeded random chunk / context sizes, batch 1-3, offsets and caches carried over
+    three consecutive calls (the realtime loop), fp32 against the oracle."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from chunkformer_amd.config import SMALL
+    from chunkformer_amd.encoder import ChunkFormerEncoder
+    from chunkformer_amd.weights import synthetic_features, synthetic_state_dict
+    from oracle import encoder_ref as ref
+    rng = np.random.default_rng(5000 + seed)
+    sd = synthetic_state_dict(SMALL, 1)
+    enc = ChunkFormerEncoder(SMALL, sd, dtype="fp32")
+    B = int(rng.integers(1, 4))
+    C = int(rng.choice([4, 8, 16, 32]))
+    L, R = int(rng.choice([8, 16, 32, 40])), int(rng.choice([0, 4, 8, 16]))
+    off = int(rng.integers(0, 2 * L))
+    gen = torch.Generator().manual_seed(seed)
+    att = torch.randn(2, B, SMALL.n_heads, L, 2 * SMALL.head_dim, generator=gen) * 0.5
+    cnn = torch.randn(2, B, SMALL.d_model, 7, generator=gen) * 0.5
+    ga, gc, ra_, rc_ = att.cuda(), cnn.cuda(), att, cnn
+    for step in range(3):
+        tp = C + R   # one chunk plus its right context, as the realtime app feeds it
+        x = torch.stack(synthetic_features([8 * (tp - 1) + 15] * B, 1300 + 10 * seed + step))
+        y, _, ga, gc = enc.forward_chunk(x, ga, gc, C, L, R, off)
+        ry, ra_, rc_ = ref.forward_chunk(sd, SMALL, x, ra_, rc_, C, L, R, off)
+        err = str((B, C, L, R, off, step))
+        np.testing.assert_allclose(y.cpu().numpy(), ry.numpy(), atol=1e-4, rtol=0, err_msg=err)
+        np.testing.assert_allclose(ga.cpu().numpy(), ra_.numpy(), atol=1e-4, rtol=0, err_msg=err)
+        np.testing.assert_allclose(gc.cpu().numpy(), rc_.numpy(), atol=1e-4, rtol=0, err_msg=err)
+        off += C
