@@ -175,6 +175,9 @@ namespace cfm {
 
 // 16-bit modes run the FFN SiLU and the conv module's GLU on -log2(e)-prescaled accumulators (ACT_SILU_L2E,
 // cfm_kernels.h): the weights are scaled once in build_model
+#ifndef CFM_LNB_PROBE
+#define CFM_LNB_PROBE 0   // timing probe builds only (tools/build_variant.py): see the macaron FFN below
+#endif
 #ifndef CFM_SILU_PRE
 #define CFM_SILU_PRE 1   // 0: the plain SiLU / GLU epilogues in the 16-bit modes too (A/B builds)
 #endif
@@ -416,11 +419,21 @@ struct ModelT : public cfm_model {
         if constexpr (std::is_same<T, bf16>::value) a.y_out = w.y;
         if (rowln(PC_FFN2, w.hid, ff, Lw.ff2m, a) < 0) return set_error(CFM_ERR_RUNTIME, "fused FFN w2 not eligible");
       } else {
+#if CFM_LNB_PROBE
+      // TIMING PROBE ONLY (wrong results): the macaron FFN's residual add in its w2 epilogue (f32 x read and
+      // written there) and no LN_mha launch -- the producer side of a "statistics side buffer" LayerNorm
+      // (QKV would normalise in its epilogue); LN_conv then adds only y_att
+      { EpiArgs e = E(SITE_FFN1); e.bias = Lw.b_ff1m; e.out = w.hid; e.ldo = ff;
+        PROF(PC_FFN1, gemm<T>(EPI_STORE, kActSilu<T>, w.h, d, (const T*)Lw.ff1m, d, rA, ff, d, e, st)); }
+      { EpiArgs e = E(SITE_FFN2); e.bias = Lw.b_ff2m; e.x = w.x; e.ldx = d; e.alpha = 0.5f;
+        PROF(PC_FFN2, gemm<T>(EPI_RESID, ACT_NONE, w.hid, ff, (const T*)Lw.ff2m, ff, rA, d, ff, e, st)); }
+#else
       // macaron FFN (x 0.5)
       { const cfm_status fs = ffn(Lw.ff1m, Lw.b_ff1m, Lw.ff2m, Lw.b_ff2m, w.y, rA); if (fs != CFM_OK) return fs; }
       // MHSA (x + 0.5 y_ffm is not stored: the conv LayerNorm re-applies it)
       { ResidAdd<T> r = resid(w.y, 0.5f, nullptr); r.defer = true;
         PROF(PC_LN, layernorm<T>(w.x, r, rA, d, Lw.ln_mha_w, Lw.ln_mha_b, eps, w.h, nullptr, st)); }
+#endif
       }
       if (aci && !cache_fuse) {
         if (stream) PROF(PC_CACHE, att_cache_in_hl<T>(aci + l * att_ls, H, L, dk, w.kv, st));
@@ -479,8 +492,13 @@ struct ModelT : public cfm_model {
       { EpiArgs e = E(SITE_OPROJ); e.bias = Lw.b_o; e.out = w.y2; e.ldo = d;
         PROF(PC_OPROJ, gemm<T>(EPI_STORE, ACT_NONE, w.ao, d, (const T*)Lw.wo, d, rB, d, d, e, st)); }
       // convolution module: x += 0.5 y_ffm + y_attn, stored
+#if CFM_LNB_PROBE
+      PROF(PC_LN, layernorm<T>(w.x, resid(w.y2, 1.f, nullptr), rB, d, Lw.ln_conv_w, Lw.ln_conv_b,
+                               eps, w.h, (masked || stream) ? nullptr : rmask, st));
+#else
       PROF(PC_LN, layernorm<T>(w.x, resid2(w.y, 0.5f, nullptr, w.y2, 1.f, nullptr), rB, d, Lw.ln_conv_w, Lw.ln_conv_b,
                                eps, w.h, (masked || stream) ? nullptr : rmask, st));
+#endif
       }
       if (cci && !cache_fuse) PROF(PC_CACHE, cnn_cache_in<T>(cci + l * cnn_ls, d, 7, w.glu, st));
       { EpiArgs e = E(SITE_PW1); e.bias = Lw.b_pw1; e.out = w.glu; e.ldo = d; e.row_off = gluoff;
