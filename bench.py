@@ -380,9 +380,8 @@ def main():
     rows = n_chunks * C
     d_, ff_ = cfg.d_model, cfg.ffn_dim
     roof_cls = "ffn_w1_gemm"
-    roof_name = ("ffn_w1_gemm (gemm_wsp_kernel<EPI_STORE,SiLU>: K=512 weight-stationary bf16 MFMA)"
-                 if args.dtype == "bf16" else f"ffn_w1_gemm (gemm_kernel<{'_Float16' if args.dtype == 'fp16' else 'float'},"
-                 "EPI_STORE,SiLU>)")
+    roof_name = (f"ffn_w1_gemm (gemm_wsp_kernel<EPI_STORE,SiLU>: K=512 weight-stationary {args.dtype[:2]}16 MFMA)"
+                 if args.dtype in ("bf16", "fp16") else "ffn_w1_gemm (gemm_kernel<float,EPI_STORE,SiLU>, exact-f32 MFMA)")
     # per step: one w_1 launch per layer and utterance group (enc.stream_split groups of the batch run
     # on their own streams, so a launch covers rows / groups rows); totals over the timed launches
     # (two FFNs per layer: the macaron and the final one)

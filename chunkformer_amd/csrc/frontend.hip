@@ -539,9 +539,19 @@ __global__ __launch_bounds__(256) void fe_dw2_kernel(const T* __restrict__ in, i
   load8(b + c, bias);
   const T* ib = in + (wn * T2 * FE_F2 + 2 * f3) * d + c;
   T* ob = out + (wn * T3 * FE_F3 + f3) * d + c;
+  // the 16-bit inputs are converted to f32 before the FMAs: pinned, so that hipcc does not fold an f16
+  // conversion into v_fma_mix_f32 (measured: its results differ from cvt + fma in the last f32 bit now
+  // and then, and the fused pw1 + dw2 kernel, gemm_wst.hip EPI_DW2, converts first)
+  auto pin8 = [](float (&x)[8]) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) asm volatile("" : "+v"(x[q]));
+  };
   float top[3][8];   // input row 2*t3 (carried from the previous output row)
 #pragma unroll
-  for (int v = 0; v < 3; ++v) load8(ib + (size_t)(2 * t3a) * FE_F2 * d + (size_t)v * d, top[v]);
+  for (int v = 0; v < 3; ++v) {
+    load8(ib + (size_t)(2 * t3a) * FE_F2 * d + (size_t)v * d, top[v]);
+    pin8(top[v]);
+  }
   for (int t3 = t3a; t3 < t3b; ++t3) {
     float mid[3][8], bot[3][8];
     const T* rb = ib + (size_t)(2 * t3 + 1) * FE_F2 * d;
@@ -549,6 +559,8 @@ __global__ __launch_bounds__(256) void fe_dw2_kernel(const T* __restrict__ in, i
     for (int v = 0; v < 3; ++v) {
       load8(rb + (size_t)v * d, mid[v]);
       load8(rb + (size_t)(FE_F2 + v) * d, bot[v]);
+      pin8(mid[v]);
+      pin8(bot[v]);
     }
     float a[8];
 #pragma unroll
@@ -562,6 +574,7 @@ __global__ __launch_bounds__(256) void fe_dw2_kernel(const T* __restrict__ in, i
       }
       a[q] = s;
     }
+    pin8(a);   // the f32 sums are rounded to f32 first (else the last FMA folds into v_fma_mix{lo,hi}_f16)
     store8(ob + (size_t)t3 * FE_F3 * d, a);
 #pragma unroll
     for (int v = 0; v < 3; ++v)

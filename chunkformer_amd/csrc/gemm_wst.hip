@@ -66,6 +66,9 @@ template <int EPI> constexpr int wst_depth() { return wst_nslot<EPI>() - wst_bar
 #define DW2_PIPE 2   // dw2 taps software-pipelined two deep (explicit LDS reads and waits; 2: rank + bias in one
                      // round trip). Bench A/B, 3 interleaved runs: front-end GEMMs 5.88 -> 5.58 ms/step
 #endif
+#ifndef DW2_UNPK_SCALAR
+#define DW2_UNPK_SCALAR 0
+#endif
 #ifndef DW2_DEFER
 #define DW2_DEFER 0  // dw2 outputs staged in LDS and stored at the start of the next phase (A/B)
 #endif
@@ -75,6 +78,20 @@ constexpr int DW2_RP = 528;                 // pw1 ring row pitch (256 bf16 + 16
 constexpr int DW2_RING = 128 * DW2_RP;      // two 64-row tiles
 constexpr int DW2_WB = (9 + 1) * 256 * 4;   // dw2 taps [9][256] + bias [256], f32
 template <int N> CFM_DEV void wst_vmcnt() { asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory"); }
+// a packed pair of 16-bit pw1 outputs (bf16 or f16) -> f32 (exact either way)
+template <int FMT> CFM_DEV f32x2 dw2_unpk2(unsigned x) {
+  if constexpr (FMT == 1) {
+#if DW2_UNPK_SCALAR
+    const f16 lo = __builtin_bit_cast(f16, (unsigned short)(x & 0xffffu)), hi = __builtin_bit_cast(f16, (unsigned short)(x >> 16));
+    return (f32x2){(float)lo, (float)hi};
+#else
+    typedef f16 h2 __attribute__((ext_vector_type(2)));
+    return __builtin_convertvector(__builtin_bit_cast(h2, x), f32x2);
+#endif
+  } else {
+    return (f32x2){__builtin_bit_cast(float, x << 16), __builtin_bit_cast(float, x & 0xffff0000u)};
+  }
+}
 }  // namespace
 
 #ifndef WSP_LGKM
@@ -712,7 +729,7 @@ __global__ __launch_bounds__(256, 1) void gemm_wsp_kernel(const bf16* __restrict
             const f32x2 wq[4] = {(f32x2){w0[0], w0[1]}, (f32x2){w0[2], w0[3]}, (f32x2){w1[0], w1[1]}, (f32x2){w1[2], w1[3]}};
 #pragma unroll
             for (int h = 0; h < 4; ++h) {
-              const f32x2 xv = {__builtin_bit_cast(float, x[h] << 16), __builtin_bit_cast(float, x[h] & 0xffff0000u)};
+              const f32x2 xv = dw2_unpk2<FMT>(x[h]);
               a[0][h] = __builtin_elementwise_fma(wq[h], xv, a[0][h]);
             }
             if constexpr (t + 2 < 9) issue(std::integral_constant<int, t + 2>{});
@@ -731,7 +748,7 @@ __global__ __launch_bounds__(256, 1) void gemm_wsp_kernel(const bf16* __restrict
               const u32x4 x = *reinterpret_cast<const u32x4*>(ring + ((rb[u] - off) & 127) * DW2_RP);
 #pragma unroll
               for (int h = 0; h < 4; ++h) {
-                const f32x2 xv = {__builtin_bit_cast(float, x[h] << 16), __builtin_bit_cast(float, x[h] & 0xffff0000u)};
+                const f32x2 xv = dw2_unpk2<FMT>(x[h]);
                 a[u][h] = __builtin_elementwise_fma(wq[h], xv, a[u][h]);
               }
             }
@@ -742,18 +759,15 @@ __global__ __launch_bounds__(256, 1) void gemm_wsp_kernel(const bf16* __restrict
           const int R = rtp * WST_MT + Rl[u];
           const int w_ = R / wrows, rem = R - w_ * wrows, t2 = rem / 19, f2 = rem - t2 * 19;
           const int t3 = (t2 - 2) >> 1, f3 = (f2 - 2) >> 1;
-          bf16x8 o8;
+          u32x4 o8;   // the same conversion as fe_dw2_kernel's store8 (round to nearest even)
 #pragma unroll
-          for (int h = 0; h < 4; ++h) {
-            o8[2 * h] = (bf16)a[u][h][0];
-            o8[2 * h + 1] = (bf16)a[u][h][1];
-          }
-          bf16x8* dst = reinterpret_cast<bf16x8*>(reinterpret_cast<bf16*>(ep.out) + ((size_t)(w_ * ep.t3n + t3) * 9 + f3) * ep.ldo +
-                                                  ct * 256 + cl);
+          for (int h = 0; h < 4; ++h) o8[h] = pack_h2<FMT>(a[u][h][0], a[u][h][1]);
+          u32x4* dst = reinterpret_cast<u32x4*>(reinterpret_cast<bf16*>(ep.out) + ((size_t)(w_ * ep.t3n + t3) * 9 + f3) * ep.ldo +
+                                                ct * 256 + cl);
           if constexpr (DW2_DIAG != 1) {
             if (defer) {
               const unsigned sb = dstg + (unsigned)(base >> 3) * 1280;
-              asm volatile("ds_write_b128 %0, %1 offset:0" ::"v"(sb + 16u * lane), "v"(__builtin_bit_cast(u32x4, o8)) : "memory");
+              asm volatile("ds_write_b128 %0, %1 offset:0" ::"v"(sb + 16u * lane), "v"(o8) : "memory");
               asm volatile("ds_write_b32 %0, %1 offset:1024" ::"v"(sb + 4u * lane),
                            "v"((unsigned)(((size_t)(w_ * ep.t3n + t3) * 9 + f3) * ep.ldo + ct * 256 + cl)) : "memory");
             } else if constexpr (DW2_NT) {
@@ -824,11 +838,9 @@ static int launch_wst(const bf16* A, int lda, const bf16* W, int ldw, int M, int
   // below 64 rows x ld), so outputs past 2 GiB (a 980-minute batch's FFN hidden: 3 GB) stay here
 #define WSP_LAUNCH(D)                                                                                         \
   do {                                                                                                        \
-    if constexpr (EPI != EPI_DW2) {                                                                           \
-      if (ep.f16) {                                                                                           \
-        hipLaunchKernelGGL((gemm_wsp_kernel<EPI, ACT, D, 1>), dim3(n_cu), dim3(256), 0, st, A, lda, W, ldw, M, N, ep); \
-        break;                                                                                                \
-      }                                                                                                       \
+    if (ep.f16) {                                                                                             \
+      hipLaunchKernelGGL((gemm_wsp_kernel<EPI, ACT, D, 1>), dim3(n_cu), dim3(256), 0, st, A, lda, W, ldw, M, N, ep); \
+      break;                                                                                                  \
     }                                                                                                         \
     hipLaunchKernelGGL((gemm_wsp_kernel<EPI, ACT, D, 0>), dim3(n_cu), dim3(256), 0, st, A, lda, W, ldw, M, N, ep); \
   } while (0)
@@ -881,8 +893,8 @@ int gemm_bf16_wst(int epi, int act, const bf16* A, int lda, const bf16* W, int l
       if (ep.bias == nullptr) return -1;
       if (act == ACT_SILU_L2E) return launch_wst<EPI_GLU, ACT_SILU_L2E>(A, lda, W, ldw, M, N, ep, st);
       return launch_wst<EPI_GLU, ACT_NONE>(A, lda, W, ldw, M, N, ep, st);
-    case EPI_DW2:   // front-end pw1 + ReLU + dw2 (N = 512, dw2 taps / bias / geometry in ep; bf16 only)
-      if (ep.f16 || act != ACT_RELU || N != 512 || !ep.dw_w || !ep.dw_b || ep.t2n < 3 || ep.ldo % 8) return -1;
+    case EPI_DW2:   // front-end pw1 + ReLU + dw2 (N = 512, dw2 taps / bias / geometry in ep; bf16 or f16)
+      if (act != ACT_RELU || N != 512 || !ep.dw_w || !ep.dw_b || ep.t2n < 3 || ep.ldo % 8) return -1;
       return launch_wst<EPI_DW2, ACT_RELU>(A, lda, W, ldw, M, N, ep, st);
   }
   return -1;

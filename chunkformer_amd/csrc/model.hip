@@ -304,13 +304,15 @@ struct ModelT : public cfm_model {
                                 fe.w1, fe.b1, fe.wpack, fe.wfrag, d, w.feA, st, tune.fe_conv));
       EpiArgs e1 = E(SITE_FE); e1.bias = fe.b_pw1; e1.out = w.feB; e1.ldo = d;
       T* dw2_rows = w.feA;   // the pw2 GEMM's input
-      if constexpr (std::is_same<T, bf16>::value) {
+      if constexpr (sizeof(T) == 2) {
         // pw1 + ReLU + dw2 in one weight-stationary kernel (so "gemm_wst" 0 turns it off too): dw2 rows
-        // straight into feB
+        // straight into feB (bf16 / f16: the kernel's 16-bit format in ef.f16)
         if (tune.fe_fuse_dw2 && tune.gemm_wst) {
           EpiArgs ef = e1; ef.dw_w = fe.w2; ef.dw_b = fe.b2; ef.t2n = T2; ef.t3n = T3;
+          ef.f16 = std::is_same<T, f16>::value;
           int r = -1;
-          PROF(PC_FE_GEMM, (r = gemm_bf16_wst(EPI_DW2, ACT_RELU, w.feA, d, (const bf16*)fe.pw1, d, ng * T2 * 19, d, d, ef, st),
+          PROF(PC_FE_GEMM, (r = gemm_bf16_wst(EPI_DW2, ACT_RELU, (const bf16*)w.feA, d, (const bf16*)fe.pw1, d, ng * T2 * 19,
+                                              d, d, ef, st),
                             r == -1 ? 0 : r));
           if (r != -1) dw2_rows = w.feB;
         }

@@ -164,14 +164,19 @@ def test_stream_split_bit_identical(large, dtype, minutes, parts):
         enc.stream_split, enc.split_min_chunks = saved
 
 
-@pytest.mark.parametrize("minutes,group", [(240, 0), (1, 2)])
-def test_frontend_fused_dw2_bit_identical(large, minutes, group):
-    """bf16 front-end option fe_fuse_dw2: pw1 + ReLU + dw2 in one weight-stationary GEMM (the dw2
+@pytest.mark.parametrize("minutes,group,dtype", [(240, 0, "bf16"), (1, 2, "bf16"), (240, 0, "fp16"), (1, 2, "fp16")])
+def test_frontend_fused_dw2_bit_identical(large, minutes, group, dtype):
+    """16-bit front-end option fe_fuse_dw2: pw1 + ReLU + dw2 in one weight-stationary GEMM (the dw2
     taps applied to the pw1 tile ring in LDS, gemm_wst.hip EPI_DW2) must give the rows of the
-    pw1 GEMM + fe_dw2_kernel pair bit for bit -- same bf16 pw1 values, same f32 taps and FMA order.
-    (1 minute, 2 windows per group: group offsets > 0 and blocks with a halo tile at range start.)"""
-    g, _, models = large
-    enc = models["bf16"]
+    pw1 GEMM + fe_dw2_kernel pair bit for bit -- same bf16 / f16 pw1 values, same f32 taps and FMA
+    order.  (1 minute, 2 windows per group: group offsets > 0 and blocks with a halo tile at range
+    start.)"""
+    g, sd, models = large
+    if dtype not in models:
+        from chunkformer_amd.config import LARGE
+        from chunkformer_amd.encoder import ChunkFormerEncoder
+        models[dtype] = ChunkFormerEncoder(LARGE, sd, dtype=dtype)
+    enc = models[dtype]
     xs, _ = _embedded_batch(g, minutes, enc.device)
     lens = torch.tensor([x.shape[0] for x in xs], dtype=torch.int32)
     try:
