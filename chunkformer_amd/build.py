@@ -54,7 +54,9 @@ def _compile(src: str, force: bool) -> str:
 
 def build(force: bool = False, jobs: int = 8) -> str:
     os.makedirs(OUT, exist_ok=True)
-    srcs = _sources()
+    # the weight-stationary GEMM's translation units take minutes each (heavily unrolled kernels): start
+    # them first so that the parallel build ends with the short ones
+    srcs = sorted(_sources(), key=lambda p: (0 if "gemm_wst_" in os.path.basename(p) else 1, -os.path.getsize(p)))
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
         objs = list(ex.map(lambda s: _compile(s, force), srcs))
     if force or not os.path.exists(LIB) or os.path.getmtime(LIB) < max(os.path.getmtime(o) for o in objs):
