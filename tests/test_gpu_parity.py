@@ -290,7 +290,10 @@ def test_random_batches_match_oracle(cfm, small_models, seed):
     xs = synthetic_features(lens, 500 + seed)
     enc = small_models["fp32"]
     sd = synthetic_state_dict(SMALL, 1)
-    kw, rkw = {}, {}
+    # per-utterance start offsets (forward_parallel_chunk's `offset`: masks and positions of a batch resumed
+    # mid-stream), random on the cache-free batches too
+    offs = [int(v) for v in rng.integers(0, 200, len(lens))]
+    kw, rkw = dict(offset=torch.tensor(offs)), dict(offset=offs)
     if caches:
         g = torch.Generator().manual_seed(seed)
         ac = torch.randn(SMALL.num_blocks, L, SMALL.n_heads, 2 * SMALL.head_dim, generator=g) * 0.5
