@@ -293,6 +293,8 @@ def main():
                          "(tests/test_gpu_model.py): 7200 s segments fill one MI355X better than the "
                          "reference's 1800 s default (DESIGN.md §8)")
     ap.add_argument("--batch", type=int, default=256, help="full: utterances of T=3000 frames")
+    ap.add_argument("--no-fe-reuse", action="store_true",
+                    help="endless (A/B): recompute every segment's first front-end windows instead of carrying them")
     ap.add_argument("--opt", action="append", default=[], metavar="KEY=VALUE",
                     help="per-model kernel option (cfm_model_set_option), A/B runs only")
     ap.add_argument("--heads", type=int, default=8, choices=[8, 4],
@@ -560,6 +562,7 @@ def bench_single(args):
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     model = ChunkFormerModel(LARGE, synthetic_state_dict(LARGE, 0), dtype=args.dtype, device=dev)
+    model.endless_fe_reuse = not args.no_fe_reuse
     enc = model.encoder
     apply_opts(enc, args.opt)
     g = torch.Generator(device=dev).manual_seed(1234)
@@ -592,6 +595,7 @@ def bench_single(args):
                      "graph": "middle segments replayed one at a time from one captured HIP graph (front-end + "
                               "12 blocks + after_norm + CTC argmax)"}[args.endless_mode])
         extra = {"segments": len(segs), "segment_frames": seg_len, "truncated_context_size": trunc,
+                 "fe_reuse": bool(model.endless_fe_reuse),
                  "endless_mode": args.endless_mode, "pipeline_depth": depth}
     else:
         B, T = args.batch, 3000

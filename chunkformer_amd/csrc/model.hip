@@ -104,6 +104,12 @@ struct cfm_model {
   bool use_fused_ctc = true;        // "ctc_fused": bf16 ids-only CTC head as one argmax kernel (ctc.hip), no [rows, V] logits
   int cache_fuse = 1;               // "cache_fuse": both caches of a layer in one launch at its start / end
   int trim_right = 0;               // "trim_right": this call's rows past `trunc` are dropped by the caller (encode)
+  // "fe_carry" / "fe_reuse" / "fe_save_from" (endless_decode's segments): the front-end output rows of the
+  // first fe_reuse windows are copied from the f32 buffer fe_carry instead of computed, and those of windows
+  // [fe_save_from, nwin) are copied into it after the front-end (a window's rows depend on its own frames
+  // only: the next segment's first windows are this segment's last ones)
+  float* fe_carry = nullptr;
+  int fe_reuse = 0, fe_save_from = -1;
   int attn_diag = 0;                // "attn_diag": 1 = ring kernel without compute (staging only)
   cfm::Tuning tune;                 // per-model kernel selection / diagnostics (cfm_model_set_option)
   // profiler: bitmask of PC_* classes to bracket with events on the launch stream
@@ -297,7 +303,8 @@ struct ModelT : public cfm_model {
     if (stage_lo < 0) {
     // ---------------- front-end
     const int G = fe_group(hh);
-    for (int g0 = 0; g0 < nwin; g0 += G) {
+    const int reuse = (fe_carry && masked) ? std::max(0, std::min(fe_reuse, nwin)) : 0;
+    for (int g0 = reuse; g0 < nwin; g0 += G) {
       const int ng = std::min(G, nwin - g0);
       PROF(PC_FE_CONV, frontend_conv0_dw<T>(feats, feats_tab, 8 * C, meta + (size_t)g0 * PLAN_REC, PLAN_REC, ng, Wn,
                                 fe.cm, fe.ci, fe.w0, fe.b0,
@@ -324,8 +331,15 @@ struct ModelT : public cfm_model {
       EpiArgs e2 = E(SITE_FE); e2.bias = fe.b_pw2; e2.out = w.feC + (size_t)g0 * T3 * 9 * d; e2.ldo = d;
       PROF(PC_FE_GEMM, gemm<T>(EPI_STORE, ACT_RELU, dw2_rows, d, (const T*)fe.pw2, d, ng * T3 * 9, d, d, e2, st));
     }
-    { EpiArgs e3 = E(); e3.bias = fe.b_out; e3.out = w.x; e3.ldo = d; e3.row_off = 0; e3.alpha = std::sqrt((float)d);
-      PROF(PC_FE_GEMM, gemm<T>(EPI_STORE_F32, ACT_NONE, w.feC, 9 * d, (const T*)fe.wout, 9 * d, nwin * T3, d, 9 * d, e3, st)); }
+    if (reuse > 0) HIPC(hipMemcpyAsync(w.x, fe_carry, (size_t)reuse * T3 * d * sizeof(float), hipMemcpyDeviceToDevice, st));
+    if (reuse < nwin) {
+      EpiArgs e3 = E(); e3.bias = fe.b_out; e3.out = w.x; e3.ldo = d; e3.row_off = reuse * T3; e3.alpha = std::sqrt((float)d);
+      PROF(PC_FE_GEMM, gemm<T>(EPI_STORE_F32, ACT_NONE, w.feC + (size_t)reuse * T3 * 9 * d, 9 * d, (const T*)fe.wout,
+                               9 * d, (nwin - reuse) * T3, d, 9 * d, e3, st));
+    }
+    if (fe_carry && masked && fe_save_from >= 0 && fe_save_from < nwin)
+      HIPC(hipMemcpyAsync(fe_carry, w.x + (size_t)fe_save_from * T3 * d, (size_t)(nwin - fe_save_from) * T3 * d * sizeof(float),
+                          hipMemcpyDeviceToDevice, st));
     // ---------------- relative positions: P_l = pos . W_pos_l^T for every layer in ONE GEMM against
     // the stacked weights: P is [p_rows, nb * d], layer l at column l * d (row stride nb * d)
     PROF(PC_POS, pos_table<T>(d, p_rows, hh[PH_PANCHOR], w.pos, st));
@@ -881,6 +895,9 @@ cfm_status cfm_model_set_option(cfm_model* m, const char* key, int64_t value) {
   if (!std::strcmp(key, "attn_diag")) { m->attn_diag = (int)value; return CFM_OK; }
   if (!std::strcmp(key, "cache_fuse")) { m->cache_fuse = (int)(value != 0); return CFM_OK; }
   if (!std::strcmp(key, "trim_right")) { m->trim_right = (int)(value != 0); return CFM_OK; }
+  if (!std::strcmp(key, "fe_carry")) { m->fe_carry = reinterpret_cast<float*>((intptr_t)value); return CFM_OK; }
+  if (!std::strcmp(key, "fe_reuse")) { m->fe_reuse = (int)std::max<int64_t>(0, value); return CFM_OK; }
+  if (!std::strcmp(key, "fe_save_from")) { m->fe_save_from = (int)value; return CFM_OK; }
   if (!std::strcmp(key, "profile_reset")) {
     m->prof_collect();
     for (int i = 0; i < PC_N; ++i) { m->prof_ms[i] = 0; m->prof_n[i] = 0; }

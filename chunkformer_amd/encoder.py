@@ -118,6 +118,14 @@ class ChunkFormerEncoder:
         rows past truncated_context_size are not computed -- the caller drops them)."""
         _lib.check(_lib.cfm_model_set_option(self._h, b"trim_right", int(bool(on))))
 
+    def _set_fe_carry(self, ptr: int, reuse: int, save_from: int) -> None:
+        """Native "fe_carry" / "fe_reuse" / "fe_save_from" for the next encode calls (endless_decode's
+        pipelined segments): the first `reuse` front-end windows' output rows come from the f32 buffer at
+        `ptr`, and the rows of windows [save_from, nwin) are copied into it (-1: none); ptr 0 = off."""
+        _lib.check(_lib.cfm_model_set_option(self._h, b"fe_carry", int(ptr)))
+        _lib.check(_lib.cfm_model_set_option(self._h, b"fe_reuse", int(reuse)))
+        _lib.check(_lib.cfm_model_set_option(self._h, b"fe_save_from", int(save_from)))
+
     # ------------------------------------------------------------------ helpers
     def _workspace(self, nbytes: int) -> torch.Tensor:
         if self._ws is None or self._ws.numel() < nbytes:

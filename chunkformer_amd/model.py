@@ -206,6 +206,9 @@ class ChunkFormerModel:
         # endless_decode: truncated segments compute only the rows their kept rows depend on (native
         # "trim_right"; the kept rows, ids and caches are unchanged -- test_endless_trim_equals_full)
         self.endless_trim = True
+        # endless_decode's graph pipeline: a segment's first front-end windows (the previous segment's last
+        # complete ones, the same frames) are carried over instead of recomputed (streaming.py; exact)
+        self.endless_fe_reuse = True
 
     def extract_features(self, samples, sample_rate: Optional[int] = None) -> torch.Tensor:
         """_load_audio_and_extract_features (chunkformer_model.py:276-318) after decoding:
@@ -333,11 +336,13 @@ class ChunkFormerModel:
         if pipeline_depth is None:
             pipeline_depth = 4 if cuda_graph else 3
         trim = bool(self.endless_trim)
-        key = (C, L, R, trunc, seg_len, want_eo, bool(cuda_graph), bool(pipeline), int(pipeline_depth), trim)
+        fe_reuse = bool(self.endless_fe_reuse)
+        key = (C, L, R, trunc, seg_len, want_eo, bool(cuda_graph), bool(pipeline), int(pipeline_depth), trim, fe_reuse)
         runner = self._endless_runners.get(key)
         if runner is None:   # graphs are captured once per segment geometry and reused across calls
             if pipeline:
-                runner = (EndlessGraphPipeline(enc, C, L, R, trunc, seg_len, want_eo, pipeline_depth, trim=trim)
+                runner = (EndlessGraphPipeline(enc, C, L, R, trunc, seg_len, want_eo, pipeline_depth, trim=trim,
+                                               fe_reuse=fe_reuse)
                           if cuda_graph else EndlessPipeline(enc, C, L, R, trunc, want_eo, pipeline_depth, trim=trim))
             else:
                 runner = EndlessGraphRunner(enc, C, L, R, trunc, seg_len, want_eo, use_graph=cuda_graph, trim=trim)

@@ -307,14 +307,20 @@ class EndlessGraphPipeline:
     without re-capture.  Inside a replay the segments overlap exactly as in the eager pipeline, with
     no drain between the first, middle and last segments; a block's first segment starts after the
     previous block (one drain per block).  The calls are the ones the eager pipeline makes, so the
-    result is bit-identical to the one-call-per-segment loop."""
+    result is bit-identical to the one-call-per-segment loop.  With `fe_reuse` a segment's first
+    front-end windows -- the previous segment's last complete ones, the same frames -- are copied from
+    a carry buffer the previous segment's stage -1 filled (native fe_carry), not recomputed."""
 
     def __init__(self, encoder, C: int, L: int, R: int, trunc: int, seg_len: int, want_out: bool, depth: int = 3,
-                 block: int = 128, trim: bool = False):
+                 block: int = 128, trim: bool = False, fe_reuse: bool = False):
         if depth < 1:
             raise ValueError(f"pipeline depth {depth} < 1")
         self.enc = encoder
         self.trim = trim
+        # the next segment's first front-end windows are this segment's last complete ones (same frames):
+        # their output rows are carried in self.carry instead of recomputed (native "fe_carry")
+        self.fe_reuse = fe_reuse
+        self.carry: Optional[torch.Tensor] = None
         cfg = encoder.cfg
         self.C, self.L, self.R, self.trunc, self.seg_len = C, L, R, trunc, seg_len
         self.want_out = want_out
@@ -358,7 +364,11 @@ class EndlessGraphPipeline:
         st = self.streams[p]
         cur = []
         enc._set_trim(self.trim and seg["keep"])
+        if self.fe_reuse:
+            enc._set_fe_carry(self.carry.data_ptr() if self.carry is not None else 0, seg["reuse"], seg["save_from"])
         for stage in range(-1, enc.cfg.num_blocks):
+            if stage == -1 and seg["reuse"] > 0 and prev is not None:
+                st.wait_event(prev[-1])   # the previous segment's front-end filled the carry
             if stage >= 0 and prev is not None:
                 st.wait_event(prev[stage])
             _lib.check(_lib.cfm_encode_masked_stages(
@@ -366,10 +376,12 @@ class EndlessGraphPipeline:
                 self.att[c].data_ptr(), self.cnn[c].data_ptr(), int(self.trunc), self.att[1 - c].data_ptr(),
                 self.cnn[1 - c].data_ptr(), self.out[p].data_ptr(), self.ws[p].data_ptr(), seg["wsb"], stage, stage,
                 st.cuda_stream))
-            if stage >= 0:
+            if stage >= 0 or self.fe_reuse:   # (the front-end's event last: prev[-1])
                 ev = torch.cuda.Event()
                 ev.record(st)
                 cur.append(ev)
+        if self.fe_reuse:
+            cur.append(cur.pop(0))
         rows = seg["rows"]
         if rows > 0:
             with torch.cuda.stream(st):
@@ -389,6 +401,8 @@ class EndlessGraphPipeline:
                 return self._run(xs_dev, segs)
             finally:
                 self.enc._set_trim(False)
+                if self.fe_reuse:
+                    self.enc._set_fe_carry(0, 0, -1)
 
     def _run(self, xs_dev: torch.Tensor, segs):
         enc, C, L, R, D = self.enc, self.C, self.L, self.R, self.depth
@@ -411,8 +425,24 @@ class EndlessGraphPipeline:
             n_rows = len(range(N * C)[: out_lens[0]])
             kept = min(n_rows, self.trunc) if keep_trunc else n_rows
             info.append({"k": k, "x": xs_dev[start:stop], "plan": plan, "N": N, "rows": kept, "keep": keep_trunc,
-                         "wsb": int(_lib.cfm_workspace_bytes_masked(enc._h, N, C, L, R)), "len": n_frames})
+                         "wsb": int(_lib.cfm_workspace_bytes_masked(enc._h, N, C, L, R)), "len": n_frames,
+                         "start": start, "reuse": 0, "save_from": -1})
             offset += kept
+        if self.fe_reuse:
+            for a, b in zip(info, info[1:]):
+                # segment b starts trunc rows (8 trunc frames) after a: a's windows trunc / C .. are b's first
+                # ones; only windows a holds whole (8C + 7 frames inside a) are carried
+                if not a["keep"] or self.trunc % C or b["start"] - a["start"] != 8 * self.trunc:
+                    continue
+                complete = min(a["N"], max(0, (a["len"] - 8 * C - 7) // (8 * C) + 1))
+                n_c = min(complete - self.trunc // C, b["N"])
+                if n_c > 0:
+                    a["save_from"], b["reuse"] = self.trunc // C, n_c
+            need = max([(s_["N"] - s_["save_from"]) * C * d for s_ in info if s_["save_from"] >= 0] + [0])
+            if need and (self.carry is None or self.carry.numel() < need):
+                self.carry = torch.empty(need, dtype=torch.float32, device=self.dev)
+                retire_graphs(self.graphs.values())   # captured graphs hold the old carry's address
+                self.graphs.clear()
         # every segment runs from a captured graph: device plans are kept per distinct plan (the middle
         # segments share one; the first, offset-0 segment and the ragged last one have their own), and a
         # block's graph is keyed by its phase and its segments' plans / lengths / kept rows, so the middle
@@ -447,7 +477,8 @@ class EndlessGraphPipeline:
             for i in range(cnt):
                 s = info[k0 + i]
                 self.g_feats[i][: s["len"] * enc.cfg.input_dim].view(s["len"], -1).copy_(s["x"])
-            key = (phase, tuple((s["pid"], s["len"], s["rows"], s["keep"]) for s in info[k0: k0 + cnt]))
+            key = (phase, tuple((s["pid"], s["len"], s["rows"], s["keep"], s["reuse"], s["save_from"])
+                                for s in info[k0: k0 + cnt]))
             entry = self.graphs.get(key)
             if entry is None:
                 g = torch.cuda.CUDAGraph()

@@ -270,3 +270,31 @@ def test_random_endless_matches_oracle(small, seed):
         att, cnn = m.last_endless_caches
         np.testing.assert_allclose(att.cpu().numpy(), ac.numpy(), atol=1e-4, rtol=0)
         np.testing.assert_allclose(cnn.cpu().numpy(), cc.numpy(), atol=1e-4, rtol=0)
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_endless_fe_reuse_equals_recompute(small, dtype):
+    """The graph pipeline carrying each segment's last complete front-end windows into the next
+    segment (native fe_carry / fe_reuse / fe_save_from, model.endless_fe_reuse) gives exactly the rows,
+    ids and caches of recomputing them, over several input lengths."""
+    from chunkformer_amd.weights import synthetic_features
+    g, models = small
+    C, L, R, tbd = (int(v) for v in g["endless_clrt"])
+    m = models[dtype]
+    try:
+        for n in (6000, 2100, 9000):
+            x = synthetic_features([n], 40 + n)[0]
+            res = []
+            for reuse in (False, True):
+                m.endless_fe_reuse = reuse
+                ids, eo = m.endless_decode(x, C, L, R, total_batch_duration=tbd, return_encoder_out=True,
+                                           cuda_graph=True, pipeline=True)
+                res.append((ids, eo, [c.clone() for c in m.last_endless_caches]))
+                if reuse:
+                    runner = next(iter(m._endless_runners.values()))
+                    assert sum(s_["reuse"] for s_ in runner._keep) > 0, n   # windows were carried
+            assert torch.equal(res[0][1], res[1][1]) and torch.equal(res[0][0], res[1][0]), n
+            for a, b in zip(res[0][2], res[1][2]):
+                assert torch.equal(a, b), n
+    finally:
+        m.endless_fe_reuse = True
