@@ -293,6 +293,8 @@ def main():
                          "(tests/test_gpu_model.py): 7200 s segments fill one MI355X better than the "
                          "reference's 1800 s default (DESIGN.md §8)")
     ap.add_argument("--batch", type=int, default=256, help="full: utterances of T=3000 frames")
+    ap.add_argument("--pipe-opt", action="append", default=[], metavar="KEY=VALUE",
+                    help="endless (A/B): override a launch parameter of the segments in flight (streaming.PIPELINE_OPTS)")
     ap.add_argument("--no-fe-reuse", action="store_true",
                     help="endless (A/B): recompute every segment's first front-end windows instead of carrying them")
     ap.add_argument("--opt", action="append", default=[], metavar="KEY=VALUE",
@@ -563,6 +565,11 @@ def bench_single(args):
     torch.cuda.set_device(dev)
     model = ChunkFormerModel(LARGE, synthetic_state_dict(LARGE, 0), dtype=args.dtype, device=dev)
     model.endless_fe_reuse = not args.no_fe_reuse
+    if args.pipe_opt:
+        from chunkformer_amd import streaming
+        for kv in args.pipe_opt:
+            k_, v_ = kv.split("=")
+            streaming.PIPELINE_OPTS[k_] = int(v_)
     enc = model.encoder
     apply_opts(enc, args.opt)
     g = torch.Generator(device=dev).manual_seed(1234)
@@ -596,6 +603,7 @@ def bench_single(args):
                               "12 blocks + after_norm + CTC argmax)"}[args.endless_mode])
         extra = {"segments": len(segs), "segment_frames": seg_len, "truncated_context_size": trunc,
                  "fe_reuse": bool(model.endless_fe_reuse),
+                 "pipeline_opts": dict(__import__("chunkformer_amd.streaming", fromlist=["x"]).PIPELINE_OPTS),
                  "endless_mode": args.endless_mode, "pipeline_depth": depth}
     else:
         B, T = args.batch, 3000
