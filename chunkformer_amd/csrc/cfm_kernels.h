@@ -245,6 +245,8 @@ int masks_from_plan(const int32_t* meta, int n, int C, int L, int R, uint8_t* at
 bool ctc_argmax_eligible(int V, int d);
 int ctc_argmax_bf16(const float* enc, int M, const bf16* W, const float* bias, int V, int d, int32_t* ids,
                     hipStream_t st);
+int ctc_argmax_f16(const float* enc, int M, const f16* W, const float* bias, int V, int d, int32_t* ids,
+                   hipStream_t st);
 int ctc_collapse(const int32_t* ids, const int32_t* row_start, const int32_t* row_len, int B, int blank, int max_sil,
                  int32_t* tok, int32_t* tok_frame, int32_t* n_tok, int32_t* seg, int32_t* n_seg, hipStream_t st);
 int log_softmax_rows(float* logits, int M, int V, int write_logp, int32_t* ids, hipStream_t st);

@@ -3,8 +3,9 @@
 // ctc_argmax_kernel: ids[m] = argmax_v (enc[m] . W[v] + b[v])  -- the argmax of CTC.log_softmax
 //   (ctc.py:73-81; chunkformer_model.py:437-438, 526-527: log_softmax is monotone per row, so its
 //   argmax is the logits' argmax) with NO [rows, V] logit tensor: every logit lives only in
-//   registers.  bf16 MFMA, f32 accumulate, the same operands as the two-pass path (enc rounded to
-//   bf16 RNE, W bf16); ties resolve to the lowest index like torch.argmax.
+//   registers.  bf16 (or, for the fp16 model, f16) MFMA, f32 accumulate, the same operands as the
+//   two-pass path (enc rounded to the 16-bit format RNE, W in it); ties resolve to the lowest index
+//   like torch.argmax.
 //     * block = 4 waves, 256 rows (64 per wave); the wave's rows stay in AGPRs for the whole
 //       launch as MFMA B fragments (enc is read from HBM once, f32 -> bf16 in registers);
 //     * the vocabulary streams through a 2 x 64 KiB LDS ring in 64-column tiles (LDS-DMA, one
@@ -47,8 +48,13 @@ CFM_DEV void cfor(F&& f) {
 
 // acc += W fragment (VGPR, MFMA A: 16 vocabulary columns) x enc fragment (AGPR, MFMA B: 16 rows):
 // lane (fr, g) of acc holds logit[row 16 mb + fr][column 16 nb + 4 g + r]
+// (FMT 1: f16 operands, v_mfma_f32_16x16x32_f16, the fp16 model's head)
+template <int FMT>
 CFM_DEV void ctc_mfma(f32x4& acc, const bf16x8& w, const bf16x8& a) {
-  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(acc) : "v"(w), "a"(a));
+  if constexpr (FMT == 1)
+    asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, %0" : "+v"(acc) : "v"(w), "a"(a));
+  else
+    asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(acc) : "v"(w), "a"(a));
 }
 // running argmax, 3 VALU per logit: if (x > best) { best = x; slot = SLOT; } with the tile-local
 // column SLOT (< 64) as an inline constant (VOP2 v_cndmask reads VCC, so an SGPR column would not
@@ -84,6 +90,7 @@ CFM_DEV void ctc_lds_read(bf16x8& v, unsigned addr) {
   asm volatile("ds_read_b128 %0, %1 offset:%2" : "+v"(v) : "v"(addr), "i"(OFF));
 }
 
+template <int FMT>
 __global__ __launch_bounds__(256, 1) void ctc_argmax_kernel(const float* __restrict__ enc, int M,
                                                             const bf16* __restrict__ W /*[nt*64, 512]*/,
                                                             const float* __restrict__ bias, int V,
@@ -123,8 +130,12 @@ __global__ __launch_bounds__(256, 1) void ctc_argmax_kernel(const float* __restr
     for (int s = 0; s < 16; ++s) {
       const f32x4 lo = *reinterpret_cast<const f32x4*>(ap + 32 * s);
       const f32x4 hi = *reinterpret_cast<const f32x4*>(ap + 32 * s + 4);
-      af[mb][s] = (bf16x8){(bf16)lo[0], (bf16)lo[1], (bf16)lo[2], (bf16)lo[3],
-                           (bf16)hi[0], (bf16)hi[1], (bf16)hi[2], (bf16)hi[3]};
+      if constexpr (FMT == 1)   // the 16-bit format's raw lanes in the bf16x8 fragment type
+        af[mb][s] = __builtin_bit_cast(bf16x8, (f16x8){(f16)lo[0], (f16)lo[1], (f16)lo[2], (f16)lo[3],
+                                                       (f16)hi[0], (f16)hi[1], (f16)hi[2], (f16)hi[3]});
+      else
+        af[mb][s] = (bf16x8){(bf16)lo[0], (bf16)lo[1], (bf16)lo[2], (bf16)lo[3],
+                             (bf16)hi[0], (bf16)hi[1], (bf16)hi[2], (bf16)hi[3]};
     }
   }
 
@@ -189,7 +200,7 @@ __global__ __launch_bounds__(256, 1) void ctc_argmax_kernel(const float* __restr
       cfor<0, 16>([&](auto Ic) {
         constexpr int i = decltype(Ic)::value;
         constexpr int nb = i >> 2, mb = i & 3;
-        ctc_mfma(acc[A][nb][mb], cur[nb], af[mb][s]);
+        ctc_mfma<FMT>(acc[A][nb][mb], cur[nb], af[mb][s]);
         // next K-step's W fragments (the next tile's K-step 0 from the other buffer at s = 15)
         if constexpr ((i & 3) == 1) {
           constexpr int rn = i >> 2;
@@ -276,7 +287,16 @@ int ctc_argmax_bf16(const float* enc, int M, const bf16* W, const float* bias, i
                     hipStream_t st) {
   if (!ctc_argmax_eligible(V, d)) return -1;
   if (M <= 0) return 0;
-  hipLaunchKernelGGL(ctc_argmax_kernel, dim3((M + CT_ROWS - 1) / CT_ROWS), dim3(256), 0, st, enc, M, W, bias, V, ids);
+  hipLaunchKernelGGL(ctc_argmax_kernel<0>, dim3((M + CT_ROWS - 1) / CT_ROWS), dim3(256), 0, st, enc, M, W, bias, V, ids);
+  CFM_CHECK_LAUNCH();
+  return 0;
+}
+int ctc_argmax_f16(const float* enc, int M, const f16* W, const float* bias, int V, int d, int32_t* ids,
+                   hipStream_t st) {
+  if (!ctc_argmax_eligible(V, d)) return -1;
+  if (M <= 0) return 0;
+  hipLaunchKernelGGL(ctc_argmax_kernel<1>, dim3((M + CT_ROWS - 1) / CT_ROWS), dim3(256), 0, st, enc, M,
+                     reinterpret_cast<const bf16*>(W), bias, V, ids);
   CFM_CHECK_LAUNCH();
   return 0;
 }

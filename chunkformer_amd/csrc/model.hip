@@ -267,7 +267,7 @@ struct ModelT : public cfm_model {
   size_t ctc_ws_bytes(int rows) const override {
     return align_up((size_t)rows * cfg.vocab * sizeof(float)) + align_up((size_t)rows * cfg.d_model * sizeof(T)) + 4096;
   }
-  bool fused_ctc_ok() const { return std::is_same<T, bf16>::value && use_fused_ctc && ctc_argmax_eligible(cfg.vocab, cfg.d_model); }
+  bool fused_ctc_ok() const { return sizeof(T) == 2 && use_fused_ctc && ctc_argmax_eligible(cfg.vocab, cfg.d_model); }
   size_t ctc_ids_ws_bytes(int rows) const override { return fused_ctc_ok() ? 0 : ctc_ws_bytes(rows); }
 
   cfm_status encode(const float* feats, const int32_t* plan_dev, const int32_t* hh, const float* aci, const float* cci,
@@ -564,11 +564,14 @@ struct ModelT : public cfm_model {
                  hipStream_t st) const override {
     if (!fe.ctc_w) return set_error(CFM_ERR_ASSERT, "model has no CTC head (vocab == 0)");
     const int d = cfg.d_model, V = cfg.vocab;
-    if constexpr (std::is_same<T, bf16>::value) {
+    if constexpr (sizeof(T) == 2) {
       // ids only: the fused argmax head (ctc.hip) keeps every logit in registers
       if (!logp && ids && fused_ctc_ok()) {
         int r;
-        PROF(PC_CTC, (r = ctc_argmax_bf16(enc, rows, (const bf16*)fe.ctc_w, fe.ctc_b, V, d, ids, st)) < 0 ? 0 : r);
+        if constexpr (std::is_same<T, bf16>::value)
+          PROF(PC_CTC, (r = ctc_argmax_bf16(enc, rows, (const bf16*)fe.ctc_w, fe.ctc_b, V, d, ids, st)) < 0 ? 0 : r);
+        else
+          PROF(PC_CTC, (r = ctc_argmax_f16(enc, rows, (const f16*)fe.ctc_w, fe.ctc_b, V, d, ids, st)) < 0 ? 0 : r);
         if (r == 0) return CFM_OK;
       }
     }

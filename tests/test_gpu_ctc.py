@@ -33,10 +33,11 @@ def _model(V, seed=0, dtype="bf16"):
     return ChunkFormerEncoder(cfg, sd, dtype=dtype), sd
 
 
-def _torch_logits(enc_rows, sd):
-    w = sd["ctc.ctc_lo.weight"].to(enc_rows.device).bfloat16().float()
+def _torch_logits(enc_rows, sd, dtype="bf16"):
+    t = torch.float16 if dtype == "fp16" else torch.bfloat16
+    w = sd["ctc.ctc_lo.weight"].to(enc_rows.device).to(t).float()
     b = sd["ctc.ctc_lo.bias"].to(enc_rows.device).float()
-    return enc_rows.bfloat16().float() @ w.t() + b
+    return enc_rows.to(t).float() @ w.t() + b
 
 
 @pytest.fixture(scope="module")
@@ -46,14 +47,18 @@ def gen():
     return torch.Generator(device="cuda").manual_seed(5)
 
 
-@pytest.mark.parametrize("V,rows", [(5000, 3001), (5000, 256), (37, 700), (64, 513), (65, 1000), (128, 255),
-                                    (7808, 1200)])
-def test_fused_ids_match_fp32_argmax(gen, V, rows):
-    enc, sd = _model(V, seed=V)
+@pytest.mark.parametrize("V,rows,dtype", [(5000, 3001, "bf16"), (5000, 256, "bf16"), (37, 700, "bf16"),
+                                          (64, 513, "bf16"), (65, 1000, "bf16"), (128, 255, "bf16"),
+                                          (7808, 1200, "bf16"), (5000, 3001, "fp16"), (37, 700, "fp16"),
+                                          (65, 1000, "fp16"), (7808, 1200, "fp16")])
+def test_fused_ids_match_fp32_argmax(gen, V, rows, dtype):
+    """The fused head (bf16, or f16 for the fp16 model) against a torch fp32 argmax of the same
+    16-bit-rounded operands."""
+    enc, sd = _model(V, seed=V, dtype=dtype)
     assert enc.ctc_ws_bytes(rows, False) == 0   # the fused head: no logit workspace
     x = torch.randn(rows, 512, generator=gen, device="cuda") * 1.5
     _, ids = enc.ctc_log_softmax(x, want_logp=False)
-    logits = _torch_logits(x, sd)
+    logits = _torch_logits(x, sd, dtype)
     top2 = logits.topk(2, dim=-1).values
     margin = (top2[:, 0] - top2[:, 1]).cpu()
     ref = logits.argmax(-1).int().cpu()
