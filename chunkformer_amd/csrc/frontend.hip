@@ -300,7 +300,14 @@ typedef bf16 bf16x2v __attribute__((ext_vector_type(2)));
 #ifndef FE2_CLAMP
 #define FE2_CLAMP 1   // ReLU as the clamp modifier of the conversion (see fe2_relu_pk); 0: v_pk_max_i16
 #endif
+template <typename E>
 __device__ __forceinline__ unsigned fe2_relu_pk(float a, float b) {
+  if constexpr (std::is_same<E, f16>::value) {   // f16: RNE pack, then the ReLU as a packed int16 max
+    typedef f16 h2v __attribute__((ext_vector_type(2)));
+    short2v v = __builtin_bit_cast(short2v, __builtin_convertvector((f32x2v){a, b}, h2v));
+    v = __builtin_elementwise_max(v, (short2v){0, 0});
+    return __builtin_bit_cast(unsigned, v);
+  }
 #if FE2_CLAMP
   // W0 and b0 enter the fragments scaled by 2^-24 and w1 by 2^24 (exact: powers of two), so conv0's
   // accumulator is the true value times 2^-24 and, for |conv0| < 2^24, the conversion's clamp to
@@ -317,13 +324,28 @@ __device__ __forceinline__ unsigned fe2_relu_pk(float a, float b) {
   return __builtin_bit_cast(unsigned, v);
 }
 
+// 8 f32 -> the 16-bit format (RNE), as a bf16x8 container of raw lanes
+template <typename E>
+__device__ __forceinline__ bf16x8 pk8(float a, float b, float c, float d_, float e, float f, float g, float h) {
+  typedef E e8v __attribute__((ext_vector_type(8)));
+  return __builtin_bit_cast(bf16x8, (e8v){(E)a, (E)b, (E)c, (E)d_, (E)e, (E)f, (E)g, (E)h});
+}
+// 32x32x16 MFMA on the 16-bit format's raw lanes (bf16x8 containers)
+template <typename E>
+__device__ __forceinline__ f32x16 fe2_mfma(const bf16x8& a, const bf16x8& b, const f32x16& c) {
+  if constexpr (std::is_same<E, f16>::value)
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
+  else
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+template <typename E>
 __global__ __launch_bounds__(FE2_NT, 8 / FE2_WAVES) void fe_conv0_dw_mfma2_kernel(const float* __restrict__ feats,
                                                                 const float* const* __restrict__ tab, int step,
                                                                 const int32_t* __restrict__ meta, int meta_stride,
                                                                 int W, int T2, const float* __restrict__ cm,
                                                                 const float* __restrict__ ci,
                                                                 const float* __restrict__ wfrag, int d,
-                                                                bf16* __restrict__ out) {
+                                                                E* __restrict__ out) {
   __shared__ __attribute__((aligned(16))) char im2col[2 * FE2_IMG];
   // the chunk's input rows (f32, CMVN applied) while im2col is built; then the waves' output staging
   constexpr int XBYTES = FE2_XROWS * FE_F0 * 4, OBYTES = FE2_STG * FE2_WAVES * 32 * FE2_OPITCH;   // output staging
@@ -409,22 +431,20 @@ __global__ __launch_bounds__(FE2_NT, 8 / FE2_WAVES) void fe_conv0_dw_mfma2_kerne
       const int tl = idx / FE2_SLOTS, i = idx - tl * FE2_SLOTS;
       const float* xr = reinterpret_cast<const float*>(xstage) + (2 * tl) * FE_F0 + 4 * i;
       f32x4 A[3];
-      float E[3];
+      float Ex[3];
 #pragma unroll
       for (int a = 0; a < 3; ++a) {
         A[a] = *reinterpret_cast<const f32x4*>(xr + a * FE_F0);
-        E[a] = i + 1 < FE2_SLOTS ? xr[a * FE_F0 + 4] : 0.f;   // column 4i+4 (odd parity only)
+        Ex[a] = i + 1 < FE2_SLOTS ? xr[a * FE_F0 + 4] : 0.f;   // column 4i+4 (odd parity only)
       }
-      const bf16x8 lo0 = {(bf16)A[0][0], (bf16)A[0][1], (bf16)A[0][2], (bf16)A[1][0],
-                          (bf16)A[1][1], (bf16)A[1][2], (bf16)A[2][0], (bf16)A[2][1]};
-      const bf16x8 hi0 = {(bf16)A[2][2], (bf16)1.f, (bf16)0.f, (bf16)0.f, (bf16)0.f, (bf16)0.f, (bf16)0.f, (bf16)0.f};
+      const bf16x8 lo0 = pk8<E>(A[0][0], A[0][1], A[0][2], A[1][0], A[1][1], A[1][2], A[2][0], A[2][1]);
+      const bf16x8 hi0 = pk8<E>(A[2][2], 1.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f);
       const int s0 = fe2_slot(tl, i) * 16, s1 = (FE2_PLANE + fe2_slot(tl, i)) * 16;
       *reinterpret_cast<bf16x8*>(im2col + s0) = lo0;
       *reinterpret_cast<bf16x8*>(im2col + FE2_IMG + s0) = hi0;
       if (2 * i + 1 < FE_F1) {
-        const bf16x8 lo1 = {(bf16)A[0][2], (bf16)A[0][3], (bf16)E[0], (bf16)A[1][2],
-                            (bf16)A[1][3], (bf16)E[1], (bf16)A[2][2], (bf16)A[2][3]};
-        const bf16x8 hi1 = {(bf16)E[2], (bf16)1.f, (bf16)0.f, (bf16)0.f, (bf16)0.f, (bf16)0.f, (bf16)0.f, (bf16)0.f};
+        const bf16x8 lo1 = pk8<E>(A[0][2], A[0][3], Ex[0], A[1][2], A[1][3], Ex[1], A[2][2], A[2][3]);
+        const bf16x8 hi1 = pk8<E>(Ex[2], 1.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f);
         *reinterpret_cast<bf16x8*>(im2col + s1) = lo1;
         *reinterpret_cast<bf16x8*>(im2col + FE2_IMG + s1) = hi1;
       }
@@ -470,20 +490,20 @@ __global__ __launch_bounds__(FE2_NT, 8 / FE2_WAVES) void fe_conv0_dw_mfma2_kerne
       const char* xbn = patch_base(pt + 32 < pend ? pt + 32 : pt);
       char* sb = os + (FE2_STG == 2 ? (it & 1) : 0) * (FE2_WAVES * 32 * FE2_OPITCH);
       f32x16 y = seed;
-      f32x16 acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, pb[0], zero, 0, 0, 0);
+      f32x16 acc = fe2_mfma<E>(a0, pb[0], zero);
 #pragma unroll
       for (int s = 0; s < 9; ++s) {
         f32x16 nxt;
-        if (s + 1 < 9) nxt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, pb[s + 1], zero, 0, 0, 0);
+        if (s + 1 < 9) nxt = fe2_mfma<E>(a0, pb[s + 1], zero);
         __builtin_amdgcn_sched_barrier(0);   // conv0 of tap s+1 runs under tap s's VALU work
         u32x4 r0, r1;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          r0[q] = fe2_relu_pk(acc[2 * q], acc[2 * q + 1]);
-          r1[q] = fe2_relu_pk(acc[8 + 2 * q], acc[9 + 2 * q]);
+          r0[q] = fe2_relu_pk<E>(acc[2 * q], acc[2 * q + 1]);
+          r1[q] = fe2_relu_pk<E>(acc[8 + 2 * q], acc[9 + 2 * q]);
         }
-        y = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1[s][0], __builtin_bit_cast(bf16x8, r0), y, 0, 0, 0);
-        y = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1[s][1], __builtin_bit_cast(bf16x8, r1), y, 0, 0, 0);
+        y = fe2_mfma<E>(a1[s][0], __builtin_bit_cast(bf16x8, r0), y);
+        y = fe2_mfma<E>(a1[s][1], __builtin_bit_cast(bf16x8, r1), y);
         if (FE2_STG == 2 && s == 1 && it > 0) flush(os + ((it - 1) & 1) * (FE2_WAVES * 32 * FE2_OPITCH), pt - 32);
         if (s == 3) {
 #pragma unroll
@@ -500,8 +520,9 @@ __global__ __launch_bounds__(FE2_NT, 8 / FE2_WAVES) void fe_conv0_dw_mfma2_kerne
       // y: lane (h, position n), register r -> channel (r&3) + 8(r>>2) + 4h; staged [32 pos][32 ch]
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
-        const bf16x2v lo = __builtin_convertvector((f32x2v){y[4 * g], y[4 * g + 1]}, bf16x2v);
-        const bf16x2v hi = __builtin_convertvector((f32x2v){y[4 * g + 2], y[4 * g + 3]}, bf16x2v);
+        typedef E e2v __attribute__((ext_vector_type(2)));
+        const e2v lo = __builtin_convertvector((f32x2v){y[4 * g], y[4 * g + 1]}, e2v);
+        const e2v hi = __builtin_convertvector((f32x2v){y[4 * g + 2], y[4 * g + 3]}, e2v);
         const unsigned long long u = (unsigned long long)__builtin_bit_cast(unsigned, lo) |
                                      ((unsigned long long)__builtin_bit_cast(unsigned, hi) << 32);
         *reinterpret_cast<unsigned long long*>(sb + n * FE2_OPITCH + (8 * g + 4 * h) * 2) = u;
@@ -593,27 +614,27 @@ int frontend_conv0_dw(const float* feats, const float* const* tab, int step, con
   const int T1 = (W - 3) / 2 + 1, T2 = (T1 - 3) / 2 + 1;
   if (T2 <= 0 || d % FE_CG) return (int)hipErrorInvalidValue;
   const dim3 grid((T2 + FE_T2_TILE - 1) / FE_T2_TILE, nwin);
-  if constexpr (std::is_same<T, bf16>::value) {
+  if constexpr (sizeof(T) == 2) {
     // one window's dw1 output is addressed by 32-bit byte offsets (buffer stores)
-    if (d % 64 || (size_t)T2 * FE_F2 * d * sizeof(bf16) >= ((size_t)1 << 31)) return (int)hipErrorInvalidValue;
+    if (d % 64 || (size_t)T2 * FE_F2 * d * sizeof(T) >= ((size_t)1 << 31)) return (int)hipErrorInvalidValue;
     if (var >= 2 && wfrag) {
       // "fe_conv" 2 + k: about k + 1 chunks of FE2_POS positions per workgroup, balanced per window
+      // (bf16: fragments scaled by 2^-24 / 2^24, the ReLU as the conversion's clamp; f16: unscaled
+      // fragments, the ReLU as a packed max)
       const int nck = (T2 * FE_F2 + FE2_POS - 1) / FE2_POS, nch = std::max(1, var - 1);
       const int nb = (nck + nch - 1) / nch;
-      hipLaunchKernelGGL(fe_conv0_dw_mfma2_kernel, dim3(nb, (d + 32 * FE2_WAVES - 1) / (32 * FE2_WAVES), nwin), dim3(FE2_NT),
-                         0, st, feats, tab, step,
+      hipLaunchKernelGGL(fe_conv0_dw_mfma2_kernel<T>, dim3(nb, (d + 32 * FE2_WAVES - 1) / (32 * FE2_WAVES), nwin),
+                         dim3(FE2_NT), 0, st, feats, tab, step,
                          meta, meta_stride, W, T2, cmvn_mean, cmvn_istd, wfrag, d, out);
       CFM_CHECK_LAUNCH();
       return 0;
     }
-    hipLaunchKernelGGL(fe_conv0_dw_mfma_kernel<bf16>, dim3((T2 * FE_F2 + FE_POS_BLOCK - 1) / FE_POS_BLOCK, nwin), dim3(256),
-                       0, st, feats, tab, step, meta, meta_stride, W, T2, cmvn_mean, cmvn_istd, wpack, d, out);
-  } else if (std::is_same<T, f16>::value && var >= 1 && d % 64 == 0 && (size_t)T2 * FE_F2 * d * 2 < ((size_t)1 << 31)) {
-    // fp16 mode: the position-stationary MFMA kernel on f16 (the channel-stationary one's 2^-24 scaling is
-    // bf16-only: f16 has no exponent range for it)
-    hipLaunchKernelGGL(fe_conv0_dw_mfma_kernel<f16>, dim3((T2 * FE_F2 + FE_POS_BLOCK - 1) / FE_POS_BLOCK, nwin), dim3(256),
-                       0, st, feats, tab, step, meta, meta_stride, W, T2, cmvn_mean, cmvn_istd, wpack, d,
-                       reinterpret_cast<f16*>(out));
+    if (var >= 1 || std::is_same<T, bf16>::value)   // the position-stationary MFMA kernel (bf16: also at 0)
+      hipLaunchKernelGGL(fe_conv0_dw_mfma_kernel<T>, dim3((T2 * FE_F2 + FE_POS_BLOCK - 1) / FE_POS_BLOCK, nwin), dim3(256),
+                         0, st, feats, tab, step, meta, meta_stride, W, T2, cmvn_mean, cmvn_istd, wpack, d, out);
+    else
+      hipLaunchKernelGGL((fe_conv0_dw_kernel<T>), grid, dim3(256), 0, st, feats, tab, step, meta, meta_stride, W, T2,
+                         cmvn_mean, cmvn_istd, w0, b0, w1, b1, d, out);
   } else {
     hipLaunchKernelGGL((fe_conv0_dw_kernel<T>), grid, dim3(256), 0, st, feats, tab, step, meta, meta_stride, W, T2,
                        cmvn_mean,

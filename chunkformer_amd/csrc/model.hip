@@ -692,7 +692,20 @@ static cfm_status build_model(const cfm_config& cfg, const HostW& hw, int device
       // accumulator carries 2^-24 x its value: the ReLU can then be a clamp to [0, 1] (frontend.hip FE2_CLAMP)
       if (d % 32 == 0) {
         std::vector<uint32_t> fr((size_t)(d / 32) * FE2_NFRAG * 64 * 4, 0u);
-        auto bf = [](float x) { return (uint32_t)bf16_bits_rne(x); };
+        // fp16 model: f16 fragments, unscaled (f16 has no exponent range for 2^-24; its kernel takes the
+        // ReLU as a packed max instead of the clamp)
+        constexpr bool H16 = std::is_same<T, f16>::value;
+        auto bf = [](float x) -> uint32_t {
+          if constexpr (H16) {
+            const f16 h = (f16)x;
+            uint16_t u;
+            std::memcpy(&u, &h, 2);
+            return u;
+          } else {
+            return (uint32_t)bf16_bits_rne(x);
+          }
+        };
+        const int sc0 = H16 ? 0 : -24, sc1 = H16 ? 0 : 24;
         for (int ct = 0; ct < d / 32; ++ct)
           for (int lane = 0; lane < 64; ++lane) {
             const int h = lane >> 5, n = lane & 31, c = ct * 32 + n;
@@ -700,7 +713,7 @@ static cfm_status build_model(const cfm_config& cfg, const HostW& hw, int device
             uint16_t a0[8];
             for (int j = 0; j < 8; ++j) {
               const int k = 8 * h + j;
-              a0[j] = (uint16_t)bf(std::ldexp(k < 9 ? a[c * 9 + k] : k == 9 ? ab[c] : 0.f, -24));
+              a0[j] = (uint16_t)bf(std::ldexp(k < 9 ? a[c * 9 + k] : k == 9 ? ab[c] : 0.f, sc0));
             }
             std::memcpy(slot(0), a0, 16);
             const bool own = h == ((n >> 2) & 1);
@@ -708,7 +721,7 @@ static cfm_status build_model(const cfm_config& cfg, const HostW& hw, int device
             for (int sp = 0; sp < 9; ++sp)
               for (int t = 0; t < 2; ++t) {
                 uint16_t a1[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-                if (own && t == town) a1[j0] = (uint16_t)bf(std::ldexp(b[c * 9 + sp], 24));
+                if (own && t == town) a1[j0] = (uint16_t)bf(std::ldexp(b[c * 9 + sp], sc1));
                 std::memcpy(slot(1 + 2 * sp + t), a1, 16);
               }
             for (int r = 0; r < 16; ++r) {

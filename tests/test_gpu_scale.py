@@ -220,15 +220,21 @@ def test_frontend_window_groups_forced(large):
         assert _rel_l2(o, ref_out.cpu().numpy()) <= (1e-6 if tol else 5e-3)
 
 
-@pytest.mark.parametrize("minutes", [1, 240])
-def test_frontend_conv_kernels_agree(large, minutes):
-    """bf16 conv0 + ReLU + dw1: the channel-stationary kernel (fe_conv 6, the default: dw1 on MFMA,
-    conv0's ReLU output rounded to bf16 as autocast does, the ReLU as the conversion's clamp on
-    2^-24-scaled values) and the position-stationary one (fe_conv 1: dw1 in f32 on the VALU) both
-    stay at the golden's bf16 bar and agree with each other to bf16 rounding (1 minute: partial last
-    blocks; 240 minutes: the bench batch)."""
-    g, _, models = large
-    enc = models["bf16"]
+@pytest.mark.parametrize("minutes,dtype", [(1, "bf16"), (240, "bf16"), (1, "fp16"), (240, "fp16")])
+def test_frontend_conv_kernels_agree(large, minutes, dtype):
+    """16-bit conv0 + ReLU + dw1: the channel-stationary kernel (fe_conv 6, the default: dw1 on MFMA,
+    conv0's ReLU output rounded to the 16-bit format as autocast does; bf16: the ReLU as the
+    conversion's clamp on 2^-24-scaled values, f16: unscaled and a packed max) and the
+    position-stationary one (fe_conv 1: dw1 in f32 on the VALU) both stay at the golden's bar and
+    agree with each other to the format's rounding (1 minute: partial last blocks; 240 minutes: the
+    bench batch)."""
+    g, sd, models = large
+    if dtype not in models:
+        from chunkformer_amd.config import LARGE
+        from chunkformer_amd.encoder import ChunkFormerEncoder
+        models[dtype] = ChunkFormerEncoder(LARGE, sd, dtype=dtype)
+    enc = models[dtype]
+    bar = BF16_RELL2 if dtype == "bf16" else 5e-3
     xs, pos = _embedded_batch(g, minutes, enc.device)
     lens = torch.tensor([x.shape[0] for x in xs], dtype=torch.int32)
     outs = {}
@@ -245,9 +251,9 @@ def test_frontend_conv_kernels_agree(large, minutes):
         for k, u in enumerate(pos):
             o = _rows_of(outs[v], nch, u).cpu().numpy()
             exp = g["out"][gstart[k]: gstart[k + 1]]
-            assert _rel_l2(o, exp) <= BF16_RELL2, (v, k, _rel_l2(o, exp))
+            assert _rel_l2(o, exp) <= bar, (v, k, _rel_l2(o, exp))
     a, b = outs[1].cpu().numpy(), outs[6].cpu().numpy()
-    print(f"fe_conv 6 vs 1: rel-L2 {_rel_l2(b, a):.2e}")
+    print(f"{dtype} fe_conv 6 vs 1: rel-L2 {_rel_l2(b, a):.2e}")
     assert _rel_l2(b, a) <= 5e-3
 
 
