@@ -265,6 +265,10 @@ CFM_DEV void attn_static_prio(int half) {
   if constexpr (ATTN_PRIO == 2) { if (!half) __builtin_amdgcn_s_setprio(1); }
   (void)half;
 }
+#ifndef ATTN_SKEW_RD
+#define ATTN_SKEW_RD 0   // ring kernel rel_shift: 1 = unsheared aligned ds_write_b64 rows and the shear on the read
+                         // side (ds_read2_b32 + ds_read_b32 + two v_alignbit per 4 values); 0 = sheared writes
+#endif
 #ifndef ATTN_STAGGER
 #define ATTN_STAGGER 0   // A/B: waves 4-7 store their output rows one pair late (see the ring kernel)
 #endif
@@ -532,23 +536,49 @@ __global__ __launch_bounds__(512, 1) void chunk_attention_ring_kernel(
               // rel_shift by the reshape trick: row fr is written at pitch 49 (+1) and read back at
               // pitch 48, so query fr's band for key jj starts 16 - fr elements later: the reads
               // are aligned 8-B vectors (4 keys), the writes 2-B aligned, as four ds_write_b16
-              const unsigned waddr = scr_base + 2u * (unsigned)(fr * SCR_PITCH + 1 + 16 * pt + 4 * g);
               const unsigned lo = pack_e2<E>(a[0], a[1]), hi = pack_e2<E>(a[2], a[3]);
-              if (diag & 16)   // A/B: one unaligned ds_write_b64 (replayed by the LDS)
+              if constexpr (ATTN_SKEW_RD) {   // unsheared rows at pitch 48: one aligned ds_write_b64
+                const unsigned waddr = scr_base + 2u * (unsigned)(fr * (SCR_PITCH - 1) + 16 * pt + 4 * g);
                 asm volatile("ds_write_b64 %0, %1" ::"v"(waddr), "v"((u32x2_a){lo, hi}) : "memory");
-              else
-                lds_store_4bf16_a2(waddr, lo, hi);
+              } else {
+                const unsigned waddr = scr_base + 2u * (unsigned)(fr * SCR_PITCH + 1 + 16 * pt + 4 * g);
+                if (diag & 16)   // A/B: one unaligned ds_write_b64 (replayed by the LDS)
+                  asm volatile("ds_write_b64 %0, %1" ::"v"(waddr), "v"((u32x2_a){lo, hi}) : "memory");
+                else
+                  lds_store_4bf16_a2(waddr, lo, hi);
+              }
             }
             // band of (query fr, key j0+32hh+16st2+4g+rr) = scratch[fr][16st2 + 4g + rr + 15 - fr]
             typedef E ex4 __attribute__((ext_vector_type(4)));
             ex4 bdv4[2];
+            if constexpr (ATTN_SKEW_RD) {
+              // the shear on the read side: the 4 values start at a 2-B aligned element, so three dwords
+              // from the 4-B aligned address at or below it, funnel-shifted by 0 or 16 bits
+              // (tools/probe/skew_probe.hip)
+              u32x2_a d01[2];
+              unsigned d2[2], sh[2];
 #pragma unroll
-            for (int st2 = 0; st2 < 2; ++st2)
-              asm volatile("ds_read_b64 %0, %1"
-                           : "=v"(bdv4[st2])
-                           : "v"(scr_base + 2u * (unsigned)(fr * (SCR_PITCH - 1) + 16 + 16 * st2 + 4 * g))
-                           : "memory");
-            asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(bdv4[0]), "+v"(bdv4[1])::"memory");
+              for (int st2 = 0; st2 < 2; ++st2) {
+                const unsigned ra = scr_base + 2u * (unsigned)(fr * (SCR_PITCH - 1) + 15 - fr + 16 * st2 + 4 * g);
+                const unsigned al = ra & ~3u;
+                sh[st2] = (ra & 2u) << 3;
+                asm volatile("ds_read2_b32 %0, %1 offset0:0 offset1:1" : "=v"(d01[st2]) : "v"(al) : "memory");
+                asm volatile("ds_read_b32 %0, %1 offset:8" : "=v"(d2[st2]) : "v"(al) : "memory");
+              }
+              asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(d01[0]), "+v"(d01[1]), "+v"(d2[0]), "+v"(d2[1])::"memory");
+#pragma unroll
+              for (int st2 = 0; st2 < 2; ++st2)
+                bdv4[st2] = __builtin_bit_cast(ex4, (u32x2_a){__builtin_amdgcn_alignbit(d01[st2].y, d01[st2].x, sh[st2]),
+                                                             __builtin_amdgcn_alignbit(d2[st2], d01[st2].y, sh[st2])});
+            } else {
+#pragma unroll
+              for (int st2 = 0; st2 < 2; ++st2)
+                asm volatile("ds_read_b64 %0, %1"
+                             : "=v"(bdv4[st2])
+                             : "v"(scr_base + 2u * (unsigned)(fr * (SCR_PITCH - 1) + 16 + 16 * st2 + 4 * g))
+                             : "memory");
+              asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(bdv4[0]), "+v"(bdv4[1])::"memory");
+            }
             // S^T[key 16st + 4g + rr][query fr] = band + K.(q+u)
 #pragma unroll
             for (int st2 = 0; st2 < 2; ++st2) {
