@@ -11,6 +11,13 @@
 #include "cfm_common.h"
 #include "cfm_kernels.h"
 
+#ifndef LN_RPW
+#define LN_RPW 1    // A/B: rows per wave of the pre-norm LayerNorm kernel (1 or 2)
+#endif
+#ifndef LN2_RPW
+#define LN2_RPW 2   // rows per wave of the fused norm_final + next LayerNorm kernel: 2 interleaves two rows' loads and
+                    // reductions (8.13 -> 8.06 ms/step for the LayerNorm class, profiles/r05_ab_ln2_rpw.txt); 1 = one
+#endif
 #ifndef LN_Y16
 #define LN_Y16 0   // A/B: 16-bit rows (d = 512) as one 16-B load / store per lane instead of two 8-B ones
 #endif
@@ -131,9 +138,39 @@ __global__ __launch_bounds__(256) void ln_kernel(float* __restrict__ x, ResidAdd
                                                  const float* __restrict__ b, float eps, T* __restrict__ out,
                                                  const uint8_t* __restrict__ rowmask) {
   const int lane = threadIdx.x & 63;
+  constexpr int d = VPL * 64;
+  if constexpr (LN_RPW == 2) {   // A/B: two rows per wave (as ln2_kernel)
+    const int row0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 2;
+    if (row0 >= M) return;
+    const int row1 = row0 + 1 < M ? row0 + 1 : row0;
+    float v0[VPL], v1[VPL];
+    float* xp0 = x + (size_t)row0 * d + lane * VPL;
+    float* xp1 = x + (size_t)row1 * d + lane * VPL;
+    load_row(xp0, v0);
+    load_row(xp1, v1);
+    if (ra.y) {
+      resid_terms<T, VPL>(v0, ra, row0, lane);
+      resid_terms<T, VPL>(v1, ra, row1, lane);
+      if (!ra.defer) {
+        store_row(xp0, v0);
+        if (row1 != row0) store_row(xp1, v1);
+      }
+    }
+    ln_row<VPL>(v0, d, w, b, eps, lane);
+    ln_row<VPL>(v1, d, w, b, eps, lane);
+    if (rowmask) {
+#pragma unroll
+      for (int e = 0; e < VPL; ++e) {
+        if (!rowmask[row0]) v0[e] = 0.f;
+        if (!rowmask[row1]) v1[e] = 0.f;
+      }
+    }
+    store_row(out + (size_t)row0 * d + lane * VPL, v0);
+    if (row1 != row0) store_row(out + (size_t)row1 * d + lane * VPL, v1);
+    return;
+  }
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= M) return;
-  constexpr int d = VPL * 64;
   float v[VPL];
   float* xp = x + (size_t)row * d + lane * VPL;
   load_row(xp, v);
@@ -152,9 +189,34 @@ __global__ __launch_bounds__(256) void ln2_kernel(float* __restrict__ x, ResidAd
                                                   const float* __restrict__ w2, const float* __restrict__ b2, float eps,
                                                   TO* __restrict__ out) {
   const int lane = threadIdx.x & 63;
+  constexpr int d = VPL * 64;
+  if constexpr (LN2_RPW == 2) {   // A/B: two rows per wave, their loads and reductions interleaved
+    const int row0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 2;
+    if (row0 >= M) return;
+    const int row1 = row0 + 1 < M ? row0 + 1 : row0;
+    float v0[VPL], v1[VPL];
+    float* xp0 = x + (size_t)row0 * d + lane * VPL;
+    float* xp1 = x + (size_t)row1 * d + lane * VPL;
+    load_row(xp0, v0);
+    load_row(xp1, v1);
+    if (ra.y) {
+      resid_terms<TY, VPL>(v0, ra, row0, lane);
+      resid_terms<TY, VPL>(v1, ra, row1, lane);
+    }
+    ln_row<VPL>(v0, d, w1, b1, eps, lane);
+    ln_row<VPL>(v1, d, w1, b1, eps, lane);
+    store_row(xp0, v0);
+    if (row1 != row0) store_row(xp1, v1);
+    if (w2) {
+      ln_row<VPL>(v0, d, w2, b2, eps, lane);
+      ln_row<VPL>(v1, d, w2, b2, eps, lane);
+    }
+    store_row(out + (size_t)row0 * d + lane * VPL, v0);
+    if (row1 != row0) store_row(out + (size_t)row1 * d + lane * VPL, v1);
+    return;
+  }
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= M) return;
-  constexpr int d = VPL * 64;
   float v[VPL];
   float* xp = x + (size_t)row * d + lane * VPL;
   load_row(xp, v);
@@ -169,9 +231,10 @@ template <typename T>
 int layernorm(float* x, const ResidAdd<T>& ra, int M, int d, const float* w, const float* b, float eps, T* out,
               const uint8_t* rowmask, hipStream_t st) {
   if (M <= 0) return 0;
-  if (d == 128) hipLaunchKernelGGL((ln_kernel<T, 2>), dim3((M + 3) / 4), dim3(256), 0, st, x, ra, M, w, b, eps, out, rowmask);
-  else if (d == 256) hipLaunchKernelGGL((ln_kernel<T, 4>), dim3((M + 3) / 4), dim3(256), 0, st, x, ra, M, w, b, eps, out, rowmask);
-  else if (d == 512) hipLaunchKernelGGL((ln_kernel<T, 8>), dim3((M + 3) / 4), dim3(256), 0, st, x, ra, M, w, b, eps, out, rowmask);
+  const int nblk = (M + 4 * LN_RPW - 1) / (4 * LN_RPW);
+  if (d == 128) hipLaunchKernelGGL((ln_kernel<T, 2>), dim3(nblk), dim3(256), 0, st, x, ra, M, w, b, eps, out, rowmask);
+  else if (d == 256) hipLaunchKernelGGL((ln_kernel<T, 4>), dim3(nblk), dim3(256), 0, st, x, ra, M, w, b, eps, out, rowmask);
+  else if (d == 512) hipLaunchKernelGGL((ln_kernel<T, 8>), dim3(nblk), dim3(256), 0, st, x, ra, M, w, b, eps, out, rowmask);
   else return (int)hipErrorInvalidValue;
   CFM_CHECK_LAUNCH();
   return 0;
@@ -181,9 +244,10 @@ template <typename TY, typename TO>
 static int ln2_launch(float* x, const ResidAdd<TY>& ra, int M, int d, const float* w1, const float* b1, const float* w2,
                       const float* b2, float eps, TO* out, hipStream_t st) {
   if (M <= 0) return 0;
-  if (d == 128) hipLaunchKernelGGL((ln2_kernel<TY, TO, 2>), dim3((M + 3) / 4), dim3(256), 0, st, x, ra, M, w1, b1, w2, b2, eps, out);
-  else if (d == 256) hipLaunchKernelGGL((ln2_kernel<TY, TO, 4>), dim3((M + 3) / 4), dim3(256), 0, st, x, ra, M, w1, b1, w2, b2, eps, out);
-  else if (d == 512) hipLaunchKernelGGL((ln2_kernel<TY, TO, 8>), dim3((M + 3) / 4), dim3(256), 0, st, x, ra, M, w1, b1, w2, b2, eps, out);
+  const int nblk = (M + 4 * LN2_RPW - 1) / (4 * LN2_RPW);
+  if (d == 128) hipLaunchKernelGGL((ln2_kernel<TY, TO, 2>), dim3(nblk), dim3(256), 0, st, x, ra, M, w1, b1, w2, b2, eps, out);
+  else if (d == 256) hipLaunchKernelGGL((ln2_kernel<TY, TO, 4>), dim3(nblk), dim3(256), 0, st, x, ra, M, w1, b1, w2, b2, eps, out);
+  else if (d == 512) hipLaunchKernelGGL((ln2_kernel<TY, TO, 8>), dim3(nblk), dim3(256), 0, st, x, ra, M, w1, b1, w2, b2, eps, out);
   else return (int)hipErrorInvalidValue;
   CFM_CHECK_LAUNCH();
   return 0;
