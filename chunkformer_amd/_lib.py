@@ -101,15 +101,15 @@ cfm_rnnt_create = _sig("cfm_rnnt_create", I32, ctypes.POINTER(CfmRnntConfig), ct
 cfm_rnnt_destroy = _sig("cfm_rnnt_destroy", None, P)
 cfm_rnnt_workspace_bytes = _sig("cfm_rnnt_workspace_bytes", SZ, P, I32)
 cfm_rnnt_greedy = _sig("cfm_rnnt_greedy", I32, P, P, I32, P, P, I32, I32, P, P, SZ, P)
+cfm_rnnt_greedy_ex = _sig("cfm_rnnt_greedy_ex", I32, P, P, I32, P, P, I32, I32, P, P, SZ, I32, P)
+CFM_RNNT_ONE_WORKGROUP = 1
 cfm_rnnt_set_option = _sig("cfm_rnnt_set_option", I32, P, ctypes.c_char_p, I64)
 cfm_rnnt_grid_blocks = _sig("cfm_rnnt_grid_blocks", I32, P, I32)
 cfm_rnnt_error = _sig("cfm_rnnt_error", I32, P, P, I32)
 # include/cfm_ops.h
 cfm_op_gemm = _sig("cfm_op_gemm", I32, I32, I32, I32, P, I32, P, I32, I32, I32, I32, P, ctypes.c_float, P, I32, I32, P,
                    I32, P, I32, P, I32, P)
-cfm_op_gemm_rowln = _sig("cfm_op_gemm_rowln", I32, P, I32, P, I32, I32, I32, P, ctypes.c_float, P, P, P,
-                         ctypes.c_float, P, P, P, P, P, P, P, P, P, P, P, ctypes.c_float, I32, P)
-EXPORTED_OPS = ["cfm_op_gemm", "cfm_op_gemm_rowln"]
+EXPORTED_OPS = ["cfm_op_gemm"]
 
 EXPORTED = ["cfm_version", "cfm_last_error", "cfm_model_create", "cfm_model_destroy", "cfm_model_set_option",
             "cfm_plan_masked", "cfm_plan_masked_ex", "cfm_plan_padded", "cfm_workspace_bytes_masked", "cfm_workspace_bytes_padded",
@@ -118,7 +118,7 @@ EXPORTED = ["cfm_version", "cfm_last_error", "cfm_model_create", "cfm_model_dest
             "cfm_plan_stream", "cfm_workspace_bytes_stream", "cfm_encode_stream",
             "cfm_fbank_create", "cfm_fbank_destroy", "cfm_fbank_num_frames", "cfm_fbank_compute",
             "cfm_rnnt_create", "cfm_rnnt_destroy", "cfm_rnnt_workspace_bytes", "cfm_rnnt_greedy",
-            "cfm_rnnt_set_option", "cfm_rnnt_grid_blocks", "cfm_rnnt_error"]
+            "cfm_rnnt_greedy_ex", "cfm_rnnt_set_option", "cfm_rnnt_grid_blocks", "cfm_rnnt_error"]
 
 
 def profile_read(h):

@@ -23,11 +23,7 @@ FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wno-unused-re
 # frontend.hip: ReLU on MFMA outputs as a single v_max_f32 (no IEEE-mode canonicalisation);
 # the front-end never sees NaN inputs it would have to propagate; no SLP packing of the ReLU.w1
 # FMAs into v_pk_fma_f32 (slower issue beside MFMAs)
-# attention_q32.hip: MFMA accumulators in VGPRs (its AGPRs hold the relative-position fragments); max
-# of MFMA outputs as single v_max / v_max3 (no IEEE-mode canonicalisation: scores are never NaN, masked
-# ones are -inf)
-FILE_FLAGS = {"frontend.hip": ["-fno-honor-nans", "-mno-amdgpu-ieee", "-fno-slp-vectorize"],
-              "attention_q32.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1", "-fno-honor-nans", "-mno-amdgpu-ieee"]}
+FILE_FLAGS = {"frontend.hip": ["-fno-honor-nans", "-mno-amdgpu-ieee", "-fno-slp-vectorize"]}
 
 
 def _sources():

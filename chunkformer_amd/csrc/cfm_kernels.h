@@ -41,7 +41,6 @@ struct EpiArgs {
   int wsp_small_div = 1;         // weight-stationary kernel below wsp_small_rows rows: grid = CUs / this
                                  // (leaves CUs to the other streams of a pipelined caller)
   int wsp_small_rows = 32768;
-  int n512 = 0;                  // N = 512, K >= 1024: the full-row 128 x 512 kernel (gemm_rowln.hip, plain form)
   int f16 = 0;                   // 16-bit operands / outputs are f16 (v_mfma_f32_16x16x32_f16), not bf16
   // DW2 (front-end pw1 + ReLU + dw2, K = N = 512 weight-stationary only): dw2 taps tap-major [9][N]
   // f32, bias [N]; the pw1 rows are (window, t2 < t2n, f2 < 19); out = dw2 rows (window, t3 < t3n, f3 < 9)
@@ -52,37 +51,6 @@ struct EpiArgs {
 
 int gemm_bf16_wst(int epi, int act, const bf16* A, int lda, const bf16* W, int ldw, int M, int N, int K,
                   const EpiArgs& ep, hipStream_t st);
-
-// Row-owning GEMM with the sub-block's residual add and LayerNorm(s) in its epilogue (gemm_rowln.hip),
-// N = 512, K % 64 == 0, bf16 operands.  With v = bf16(A . W^T + bias) per row:
-//   xn = x + a1 * y1mask[row] * y1 + alpha * accmask[row] * v     (fmaf, y1 term first; y1 optional)
-//   y_out = v (bf16)                                              (optional: a deferred branch)
-//   one LayerNorm (g2 == null):  x_out = xn;          z = LN(xn; g1, b1)
-//   two LayerNorms:              x_out = LN(xn; g1, b1); z = LN(x_out; g2, b2)
-//   h_out = bf16(z) (rows with hmask 0 -> 0)  or  f_out = z (f32);  x_out may alias x
-// (encoder_layer.py:155-248: the four branch outputs of a layer and the LayerNorm that follows each)
-struct RowLnArgs {
-  const float* bias = nullptr;
-  float alpha = 1.f;
-  const uint8_t* accmask = nullptr;
-  const float* x = nullptr;
-  const bf16* y1 = nullptr;
-  float a1 = 1.f;
-  const uint8_t* y1mask = nullptr;
-  bf16* y_out = nullptr;
-  float* x_out = nullptr;
-  const float *g1 = nullptr, *b1 = nullptr, *g2 = nullptr, *b2 = nullptr;
-  bf16* h_out = nullptr;
-  float* f_out = nullptr;
-  const uint8_t* hmask = nullptr;
-  bf16* ybuf = nullptr;   // [M, 512] bf16 scratch for v when y_out is null (the LayerNorm reads it back)
-  float eps = 1e-5f;
-  int diag = 0;   // timing diagnostics (cfm_op_gemm_rowln variant, CFM_GEMM_DIAG builds): 1 = GEMM only, no LayerNorm
-  int nt = 0;     // plain form: non-temporal y_out stores
-};
-// -1 = not eligible (shape / alignment, K < 512); otherwise a hipError_t.  With g1 == null the same
-// kernel is a plain GEMM: y_out = bf16(acc + bias) or f_out = alpha (acc + bias) (the N = 512 GEMMs of K >= 2048)
-int gemm_rowln_bf16(const bf16* A, int lda, const bf16* W, int ldw, int M, int K, const RowLnArgs& ra, hipStream_t st);
 
 enum { SITE_QKV = 1, SITE_OPROJ = 2, SITE_PW2 = 4, SITE_FFN2 = 8, SITE_FFN1 = 16, SITE_PW1 = 32, SITE_FE = 64 };
 
@@ -100,9 +68,6 @@ struct Tuning {
   int fe_fuse_dw2 = 1;           // front-end: pw1 + ReLU + dw2 in one weight-stationary GEMM (bf16; bench A/B
                                  // 50.85 -> 50.15 ms/step, 3 interleaved pairs; 0 = pw1 GEMM + fe_dw2_kernel)
   int attn128_var = 1;           // head_dim 128 attention kernel variant (A/B)
-  int attn_q32 = 0;              // dk 64, C 64: the 32-queries-per-wave kernel (attention_q32.hip; 1 = half after
-                                 // half, 2 = software-pipelined by one half, 3 = pipelined with a branch-free
-                                 // rescale); 0 = the 8-wave ring kernel
   // GEMM sites whose bf16 outputs are stored non-temporally ("nt_sites" bit mask, SITE_* below).
   // Default: FFN w2 (its y goes straight to the LayerNorm; bench A/B 52.2 -> 51.4 ms/step); nt on
   // the front-end pointwise outputs (+0.45 ms) or FFN w1's hidden (w1 slower) measured worse.
@@ -112,12 +77,6 @@ struct Tuning {
   int wsp_small_div = 1;         // "wsp_small_div" / "wsp_small_rows" (see EpiArgs)
   int wsp_small_rows = 32768;
   int attn_min_chunks = 2;       // ring attention: chunks per block at least this ("attn_min_chunks")
-  // "gemm_n512": N = 512, K >= 1024 GEMMs on full-row 128 x 512 tiles (gemm_rowln.hip plain form; in the
-  // 240-min step FFN w2 8.20 -> 9.87 ms/step, so off: its A ring is one K-step deep, 160 KiB of LDS)
-  int gemm_n512 = 0;
-  // "ln_fuse": bf16, d = 512: the residual adds and LayerNorms in the four N = 512 GEMMs of a layer (gemm_rowln.hip;
-  // correct, but 47.3 -> 51.9 ms/step in the 240-min step: off, the LayerNorm kernels of norm.hip run)
-  int ln_fuse = 0;
   void apply(EpiArgs& e, int site = 0) const {
     e.diag = gemm_diag;
     e.big_min_tiles = big_min_tiles;
@@ -126,7 +85,6 @@ struct Tuning {
     e.wst = gemm_wst;
     e.store_mode = (nt_sites & site) ? 2 : store_mode;
     e.col_group = col_group;
-    e.n512 = gemm_n512;
   }
 };
 
@@ -187,12 +145,6 @@ int chunk_attention_masked_f16(const f16* q, const f16* kv, int kv_rows, const f
 // masked-batch attention for head_dim 128 (attention128.hip): V^T copy of the KV stream, then the
 // band / score / P.V kernel; -1 when the shape is not eligible (C = 64, W <= 320, W % 64 == 0)
 bool attention_a128_eligible(int C, int W, int p_rows, int dk);
-// dk = 64, C = 64, W % 32 == 0, W <= 320: 32 queries per wave, P in AGPRs, K / V rings by LDS-DMA
-// (attention_q32.hip); -1 when not eligible
-bool attention_q32_eligible(int C, int W, int p_rows);
-int chunk_attention_masked_q32(const bf16* q, const bf16* kv, int kv_rows, const bf16* P, int p_rows, int p_ld,
-                               const float* pos_u, const float* pos_v, const int32_t* desc, int n_chunks, int H, int C,
-                               int W, bf16* out, hipStream_t st, int diag = 0, int pipe = 3);
 int vt_transpose_bf16(const bf16* kv, int kv_rows, int H, bf16* vt, int vt_ld, hipStream_t st);
 int chunk_attention_masked_a128(const bf16* q, const bf16* kv, int kv_rows, const bf16* vt, int vt_ld, const bf16* P,
                                 int p_rows, int p_ld, const float* pos_u, const float* pos_v, const int32_t* desc,

@@ -257,20 +257,6 @@ int gemm_bf16_big(int epi, int act, const bf16* A, int lda, const bf16* W, int l
   }
   if (N % 256 || K % 64 || lda % 8 || ldw % 8) return -1;
   if (((M + 255) / 256) * (N / 256) < ep.big_min_tiles) return -1;   // too few tiles to fill the chip
-  // N = 512, K >= 1024 (FFN w2, the front-end output Linear) on full-row 128 x 512 tiles (gemm_rowln.hip): A read
-  // once, W from L2.  Option "gemm_n512", off: random operands 394-413 vs 360-435 us, in the 240-min step FFN w2
-  // 8.20 -> 9.87 ms/step (its A ring is one K-step deep: the full-row W slot takes 128 of the 160 KiB)
-  if (ep.n512 && !ep.f16 && N == 512 && K >= 1024 && ep.ldo == 512 && act == ACT_NONE && (epi == EPI_STORE || epi == EPI_STORE_F32)) {
-    RowLnArgs ra;
-    ra.bias = ep.bias;
-    ra.alpha = ep.alpha;
-    if (epi == EPI_STORE) ra.y_out = reinterpret_cast<bf16*>(ep.out) + (size_t)ep.row_off * 512;
-    else ra.f_out = reinterpret_cast<float*>(ep.out) + (size_t)ep.row_off * 512;
-    ra.nt = ep.store_mode == 2;
-    ra.diag = ep.diag;
-    const int r = gemm_rowln_bf16(A, lda, W, ldw, M, K, ra, st);
-    if (r != -1) return r;
-  }
   if (epi == EPI_GLU && ep.bias == nullptr) return -1;
   switch (epi) {
     case EPI_STORE:

@@ -181,9 +181,6 @@ namespace cfm {
 
 // 16-bit modes run the FFN SiLU and the conv module's GLU on -log2(e)-prescaled accumulators (ACT_SILU_L2E,
 // cfm_kernels.h): the weights are scaled once in build_model
-#ifndef CFM_LNB_PROBE
-#define CFM_LNB_PROBE 0   // timing probe builds only (tools/build_variant.py): see the macaron FFN below
-#endif
 #ifndef CFM_SILU_PRE
 #define CFM_SILU_PRE 1   // 0: the plain SiLU / GLU epilogues in the 16-bit modes too (A/B builds)
 #endif
@@ -379,29 +376,13 @@ struct ModelT : public cfm_model {
         PROF(PC_FFN2, gemm<T>(EPI_STORE, ACT_NONE, w.hid, ff, (const T*)w2, ff, M, d, ff, e, st)); }
       return CFM_OK;
     };
-    // Fused form (bf16, d = 512, "ln_fuse"): each N = 512 GEMM of the layer owns whole rows
-    // (gemm_rowln.hip) and applies the residual add and the LayerNorm(s) after it in its epilogue, with
-    // the same deferrals as the LayerNorm kernels below: FFN_mac w2 writes y_mac and h = LN_mha(x + 0.5
-    // y_mac) but not x; linear_out writes x += 0.5 y_mac + y_att and h = LN_conv; pointwise_conv2 writes
-    // y_conv and h = LN_ff(x + y_conv) but not x; FFN w2 writes x = LN_fin(x + y_conv + 0.5 y_ffn) and
-    // h = LN_ffm of the next layer (or the after_norm output)
-    bool fused = false;
-    if constexpr (std::is_same<T, bf16>::value) fused = tune.ln_fuse && d == 512;
-    auto rowln = [&](int cls, const T* Ain, int K, const void* Wm, const RowLnArgs& a) -> int {
-      int r = -1;
-      if constexpr (std::is_same<T, bf16>::value) PROF(cls, (r = gemm_rowln_bf16(Ain, K, (const bf16*)Wm, K, rows, K, a, st), r < 0 ? 0 : r));
-      return r;
-    };
-    auto ln_args = [&](const float* bias, float alpha, const float* g1, const float* b1) {
-      RowLnArgs a; a.bias = bias; a.alpha = alpha; a.x = w.x; a.g1 = g1; a.b1 = b1; a.eps = eps;
-      if constexpr (std::is_same<T, bf16>::value) a.h_out = w.h;
-      return a;
-    };
     // "cache_fuse": the layer's two cache copies in one launch at the layer start (into the KV / GLU stream rows
     // that QKV / pw1 leave alone) and one at the layer end (the KV / GLU rows stay intact after attention / the
     // conv module); 0 = four separate launches next to QKV and pw1
+    // (the fused copies ride on the attention cache: a conv cache alone takes the separate launches)
+    const bool cfuse_in = cache_fuse && aci, cfuse_out = cache_fuse && aci && aco;
     auto caches_out = [&](int l) -> cfm_status {
-      if (cache_fuse && aci && aco)
+      if (cfuse_out)
         PROF(PC_CACHE, cache_io<T>(false, stream, aco + l * att_ls, H, L, dk, w.kv + (size_t)cache_start * 2 * d,
                                    cci && cco ? cco + l * cnn_ls : nullptr, d, 7, w.glu + (size_t)cache_start * d, st));
       return CFM_OK;
@@ -415,7 +396,7 @@ struct ModelT : public cfm_model {
     // unchanged (row-wise kernels, per-chunk attention / conv blocks), so the kept rows and the caches are
     // as without it; the rows past them are left unwritten.
     const int n_ch = rows / C, keep_ch = C > 0 ? trunc / C : 0;
-    const bool trim = trim_right && masked && !fused && aco && trunc > 0 && trunc % C == 0 && trunc < rows &&
+    const bool trim = trim_right && masked && aco && trunc > 0 && trunc % C == 0 && trunc < rows &&
                       rows % C == 0 && natt == n_ch && nconv == n_ch && hh[PH_NWIN] == n_ch;
     // chunks of right reach per layer: the conv module's 7 rows, then attention's R keys past those
     const int reach_conv = (7 + C - 1) / C, reach_att = (hh[PH_R] + C - 1) / C;
@@ -425,39 +406,21 @@ struct ModelT : public cfm_model {
       const int cB = trim ? std::min(n_ch, n_l + reach_conv) : n_ch, cA = trim ? std::min(n_ch, cB + reach_att) : n_ch;
       const int rA = trim ? cA * C : rows, rB = trim ? cB * C : rows, rN = trim ? n_l * C : rows;
       const int aB = trim ? cB : natt, vN = trim ? n_l : nconv;   // attention / conv descriptor counts
-      if (cache_fuse && aci)
+      if (cfuse_in)
         PROF(PC_CACHE, cache_io<T>(true, stream, const_cast<float*>(aci + l * att_ls), H, L, dk, w.kv,
                                    cci ? const_cast<float*>(cci + l * cnn_ls) : nullptr, d, 7, w.glu, st));
-      if (fused) {   // macaron FFN: w1 + SiLU, then w2 -> y_mac, h = LN_mha(x + 0.5 y_mac)
-        { EpiArgs e = E(SITE_FFN1); e.bias = Lw.b_ff1m; e.out = w.hid; e.ldo = ff;
-          PROF(PC_FFN1, gemm<T>(EPI_STORE, kActSilu<T>, w.h, d, (const T*)Lw.ff1m, d, rows, ff, d, e, st)); }
-        RowLnArgs a = ln_args(Lw.b_ff2m, 0.5f, Lw.ln_mha_w, Lw.ln_mha_b);
-        if constexpr (std::is_same<T, bf16>::value) a.y_out = w.y;
-        if (rowln(PC_FFN2, w.hid, ff, Lw.ff2m, a) < 0) return set_error(CFM_ERR_RUNTIME, "fused FFN w2 not eligible");
-      } else {
-#if CFM_LNB_PROBE
-      // TIMING PROBE ONLY (wrong results): the macaron FFN's residual add in its w2 epilogue (f32 x read and
-      // written there) and no LN_mha launch -- the producer side of a "statistics side buffer" LayerNorm
-      // (QKV would normalise in its epilogue); LN_conv then adds only y_att
-      { EpiArgs e = E(SITE_FFN1); e.bias = Lw.b_ff1m; e.out = w.hid; e.ldo = ff;
-        PROF(PC_FFN1, gemm<T>(EPI_STORE, kActSilu<T>, w.h, d, (const T*)Lw.ff1m, d, rA, ff, d, e, st)); }
-      { EpiArgs e = E(SITE_FFN2); e.bias = Lw.b_ff2m; e.x = w.x; e.ldx = d; e.alpha = 0.5f;
-        PROF(PC_FFN2, gemm<T>(EPI_RESID, ACT_NONE, w.hid, ff, (const T*)Lw.ff2m, ff, rA, d, ff, e, st)); }
-#else
       // macaron FFN (x 0.5)
       { const cfm_status fs = ffn(Lw.ff1m, Lw.b_ff1m, Lw.ff2m, Lw.b_ff2m, w.y, rA); if (fs != CFM_OK) return fs; }
       // MHSA (x + 0.5 y_ffm is not stored: the conv LayerNorm re-applies it)
       { ResidAdd<T> r = resid(w.y, 0.5f, nullptr); r.defer = true;
         PROF(PC_LN, layernorm<T>(w.x, r, rA, d, Lw.ln_mha_w, Lw.ln_mha_b, eps, w.h, nullptr, st)); }
-#endif
-      }
-      if (aci && !cache_fuse) {
+      if (aci && !cfuse_in) {
         if (stream) PROF(PC_CACHE, att_cache_in_hl<T>(aci + l * att_ls, H, L, dk, w.kv, st));
         else PROF(PC_CACHE, att_cache_in<T>(aci + l * att_ls, L, 2 * d, w.kv, st));
       }
       { EpiArgs e = E(SITE_QKV); e.bias = Lw.b_qkv; e.out = w.q; e.out2 = w.kv; e.row_off = kvoff; e.d = d; e.dk = dk;
         PROF(PC_QKV, gemm<T>(EPI_QKV, ACT_NONE, w.h, d, (const T*)Lw.qkv, d, rA, 3 * d, d, e, st)); }
-      if (aci && aco && !cache_fuse) {
+      if (aci && aco && !cfuse_out) {
         if (stream) PROF(PC_CACHE, att_cache_out_hl<T>(w.kv, cache_start, H, L, dk, aco + l * att_ls, st));
         else PROF(PC_CACHE, att_cache_out<T>(w.kv, cache_start, L, 2 * d, aco + l * att_ls, st));
       }
@@ -466,11 +429,7 @@ struct ModelT : public cfm_model {
         hipEvent_t pb_;
         prof_begin(PC_ATTN, st, &pb_);
         if constexpr (std::is_same<T, bf16>::value) {
-          if (masked && use_ring_attention && dk == 64 && tune.attn_q32)
-            r = chunk_attention_masked_q32(w.q, w.kv, kv_rows, w.P + (size_t)l * d, p_rows, p_ld, Lw.pu, Lw.pv, attd,
-                                           aB, H, C, hh[PH_L] + C + hh[PH_R], w.ao, st,
-                                           attn_diag >= 64 ? attn_diag - 64 : 0, tune.attn_q32);
-          if (r == -1 && masked && use_ring_attention && dk == 64)
+          if (masked && use_ring_attention && dk == 64)
             r = chunk_attention_masked_bf16(w.q, w.kv, kv_rows, w.P + (size_t)l * d, p_rows, Lw.pu, Lw.pv,
                                             attd, aB, H, C, hh[PH_L] + C + hh[PH_R], w.ao, st, attn_diag, p_ld,
                                             tune.attn_reuse, tune.attn_min_chunks);
@@ -498,50 +457,17 @@ struct ModelT : public cfm_model {
         KCHK(r);
         prof_end(PC_ATTN, st, pb_);
       }
-      if (fused) {   // linear_out: x += 0.5 y_mac + y_att (stored), h = LN_conv(x)
-        RowLnArgs a = ln_args(Lw.b_o, 1.f, Lw.ln_conv_w, Lw.ln_conv_b);
-        a.y1 = reinterpret_cast<const bf16*>(w.y); a.a1 = 0.5f; a.x_out = w.x;
-        a.ybuf = reinterpret_cast<bf16*>(w.y2);
-        a.hmask = (masked || stream) ? nullptr : rmask;
-        if (rowln(PC_OPROJ, w.ao, d, Lw.wo, a) < 0) return set_error(CFM_ERR_RUNTIME, "fused linear_out not eligible");
-      } else {
       { EpiArgs e = E(SITE_OPROJ); e.bias = Lw.b_o; e.out = w.y2; e.ldo = d;
         PROF(PC_OPROJ, gemm<T>(EPI_STORE, ACT_NONE, w.ao, d, (const T*)Lw.wo, d, rB, d, d, e, st)); }
       // convolution module: x += 0.5 y_ffm + y_attn, stored
-#if CFM_LNB_PROBE
-      PROF(PC_LN, layernorm<T>(w.x, resid(w.y2, 1.f, nullptr), rB, d, Lw.ln_conv_w, Lw.ln_conv_b,
-                               eps, w.h, (masked || stream) ? nullptr : rmask, st));
-#else
       PROF(PC_LN, layernorm<T>(w.x, resid2(w.y, 0.5f, nullptr, w.y2, 1.f, nullptr), rB, d, Lw.ln_conv_w, Lw.ln_conv_b,
                                eps, w.h, (masked || stream) ? nullptr : rmask, st));
-#endif
-      }
-      if (cci && !cache_fuse) PROF(PC_CACHE, cnn_cache_in<T>(cci + l * cnn_ls, d, 7, w.glu, st));
+      if (cci && !cfuse_in) PROF(PC_CACHE, cnn_cache_in<T>(cci + l * cnn_ls, d, 7, w.glu, st));
       { EpiArgs e = E(SITE_PW1); e.bias = Lw.b_pw1; e.out = w.glu; e.ldo = d; e.row_off = gluoff;
         PROF(PC_PW1, gemm<T>(EPI_GLU, kSiluPre<T> ? ACT_SILU_L2E : ACT_NONE, w.h, d, (const T*)Lw.pw1, d, rB, 2 * d, d, e, st)); }
-      if (cci && cco && !cache_fuse) PROF(PC_CACHE, cnn_cache_out<T>(w.glu, cache_start, d, 7, cco + l * cnn_ls, st));
+      if (cci && cco && !cfuse_out) PROF(PC_CACHE, cnn_cache_out<T>(w.glu, cache_start, d, 7, cco + l * cnn_ls, st));
       PROF(PC_CONV, conv_dw_ln_silu<T>(w.glu, convd, vN, d, Lw.dw_t, Lw.b_dw, Lw.cn_w, Lw.cn_b, eps, w.cv, st,
                                         tune.conv_dot2, tune.conv_dma));
-      if (fused) {   // pointwise_conv2 -> y_conv, h = LN_ff(x + y_conv) (x not stored)
-        RowLnArgs a = ln_args(Lw.b_pw2, 1.f, Lw.ln_ff_w, Lw.ln_ff_b);
-        a.accmask = rmask;
-        if constexpr (std::is_same<T, bf16>::value) a.y_out = w.y;
-        if (rowln(PC_PW2, w.cv, d, Lw.pw2, a) < 0) return set_error(CFM_ERR_RUNTIME, "fused pointwise_conv2 not eligible");
-        // FFN: w1 + SiLU, then w2: x = LN_fin(x + y_conv + 0.5 y_ffn), h = next LN_ffm (or after_norm -> out)
-        { EpiArgs e = E(SITE_FFN1); e.bias = Lw.b_ff1; e.out = w.hid; e.ldo = ff;
-          PROF(PC_FFN1, gemm<T>(EPI_STORE, kActSilu<T>, w.h, d, (const T*)Lw.ff1, d, rows, ff, d, e, st)); }
-        RowLnArgs f = ln_args(Lw.b_ff2, 0.5f, Lw.ln_fin_w, Lw.ln_fin_b);
-        f.y1 = reinterpret_cast<const bf16*>(w.y); f.a1 = 1.f; f.y1mask = rmask;
-        f.ybuf = reinterpret_cast<bf16*>(w.y2);
-        if (l + 1 < nl) {
-          f.x_out = w.x; f.g2 = layers[l + 1].ln_ffm_w; f.b2 = layers[l + 1].ln_ffm_b;
-        } else {
-          f.g2 = fe.an_w; f.b2 = fe.an_b; f.h_out = nullptr; f.f_out = out;
-        }
-        if (rowln(PC_FFN2, w.hid, ff, Lw.ff2, f) < 0) return set_error(CFM_ERR_RUNTIME, "fused FFN w2 not eligible");
-        { const cfm_status cs = caches_out(l); if (cs != CFM_OK) return cs; }
-        continue;
-      }
       { EpiArgs e = E(SITE_PW2); e.bias = Lw.b_pw2; e.out = w.y; e.ldo = d;
         PROF(PC_PW2, gemm<T>(EPI_STORE, ACT_NONE, w.cv, d, (const T*)Lw.pw2, d, rN, d, d, e, st)); }
       // FFN (x 0.5); x + y_conv is not stored: norm_final re-applies it
@@ -900,11 +826,10 @@ cfm_status cfm_model_set_option(cfm_model* m, const char* key, int64_t value) {
         {"col_group", &m->tune.col_group}, {"attn_reuse", &m->tune.attn_reuse}, {"conv_dot2", &m->tune.conv_dot2},
         {"conv_dma", &m->tune.conv_dma},   {"dw2_seg", &m->tune.dw2_seg},   {"nt_sites", &m->tune.nt_sites},
         {"fe_fuse_dw2", &m->tune.fe_fuse_dw2}, {"fe_conv", &m->tune.fe_conv},
-        {"attn128_var", &m->tune.attn128_var}, {"attn_q32", &m->tune.attn_q32},
+        {"attn128_var", &m->tune.attn128_var},
         {"gemm_big_min", &m->tune.big_min_tiles}, {"wsp_small_div", &m->tune.wsp_small_div},
         {"wsp_small_rows", &m->tune.wsp_small_rows},
-        {"attn_min_chunks", &m->tune.attn_min_chunks}, {"ln_fuse", &m->tune.ln_fuse},
-        {"gemm_n512", &m->tune.gemm_n512}};
+        {"attn_min_chunks", &m->tune.attn_min_chunks}};
     for (auto& k : knobs)
       if (!std::strcmp(key, k.first)) { *k.second = (int)value; return CFM_OK; }
   }
@@ -1044,7 +969,6 @@ cfm_status cfm_op_gemm(int32_t dtype, int32_t epi, int32_t act, const void* A, i
   e.rowmask = rowmask; e.d = d; e.small_tiles = variant & 1; e.diag = (variant >> 8) & 0xff;
   e.store_mode = (variant >> 16) & 3;
   if ((variant >> 18) & 7) e.wst = ((variant >> 18) & 7) == 7 ? 0 : (variant >> 18) & 7;
-  if ((variant >> 21) & 1) e.n512 = 1;
   int r;
   if (dtype == CFM_DTYPE_F32)
     r = gemm<float>(epi, act, (const float*)A, lda, (const float*)W, ldw, M, N, K, e, (hipStream_t)stream);
@@ -1053,23 +977,6 @@ cfm_status cfm_op_gemm(int32_t dtype, int32_t epi, int32_t act, const void* A, i
   else
     r = gemm<bf16>(epi, act, (const bf16*)A, lda, (const bf16*)W, ldw, M, N, K, e, (hipStream_t)stream);
   if (r) return set_error(CFM_ERR_RUNTIME, std::string("gemm: ") + hipGetErrorString((hipError_t)r));
-  return CFM_OK;
-}
-
-cfm_status cfm_op_gemm_rowln(const void* A, int32_t lda, const void* W, int32_t ldw, int32_t M, int32_t K,
-                             const float* bias, float alpha, const uint8_t* accmask, const float* x, const void* y1,
-                             float a1, const uint8_t* y1mask, void* y_out, float* x_out, const float* g1,
-                             const float* b1, const float* g2, const float* b2, void* h_out, float* f_out,
-                             const uint8_t* hmask, void* ybuf, float eps, int32_t variant, cfm_stream stream) {
-  RowLnArgs a;
-  a.diag = variant;
-  a.ybuf = (bf16*)ybuf;
-  a.bias = bias; a.alpha = alpha; a.accmask = accmask; a.x = x; a.y1 = (const bf16*)y1; a.a1 = a1; a.y1mask = y1mask;
-  a.y_out = (bf16*)y_out; a.x_out = x_out; a.g1 = g1; a.b1 = b1; a.g2 = g2; a.b2 = b2; a.h_out = (bf16*)h_out;
-  a.f_out = h_out ? nullptr : f_out; a.hmask = hmask; a.eps = eps;
-  const int r = gemm_rowln_bf16((const bf16*)A, lda, (const bf16*)W, ldw, M, K, a, (hipStream_t)stream);
-  if (r == -1) return set_error(CFM_ERR_VALUE, "gemm_rowln: shape or arguments not eligible");
-  if (r) return set_error(CFM_ERR_RUNTIME, std::string("gemm_rowln: ") + hipGetErrorString((hipError_t)r));
   return CFM_OK;
 }
 

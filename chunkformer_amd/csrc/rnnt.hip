@@ -897,6 +897,12 @@ int32_t cfm_rnnt_error(const cfm_rnnt* h, const void* ws, int32_t rows) {
 cfm_status cfm_rnnt_greedy(const cfm_rnnt* h, const float* enc, int32_t rows, const int32_t* row_start,
                            const int32_t* row_len, int32_t B, int32_t n_steps, int32_t* out, void* ws, size_t wsb,
                            cfm_stream stream) {
+  return cfm_rnnt_greedy_ex(h, enc, rows, row_start, row_len, B, n_steps, out, ws, wsb, 0, stream);
+}
+
+cfm_status cfm_rnnt_greedy_ex(const cfm_rnnt* h, const float* enc, int32_t rows, const int32_t* row_start,
+                              const int32_t* row_len, int32_t B, int32_t n_steps, int32_t* out, void* ws, size_t wsb,
+                              int32_t flags, cfm_stream stream) {
   if (!h) return set_error(CFM_ERR_VALUE, "null handle");
   if (B < 0 || rows < 0 || n_steps < 1) return set_error(CFM_ERR_VALUE, "bad B / rows / n_steps");
   if (B == 0 || rows == 0) return CFM_OK;
@@ -910,7 +916,7 @@ cfm_status cfm_rnnt_greedy(const cfm_rnnt* h, const float* enc, int32_t rows, co
   int r = gemm<float>(EPI_STORE, ACT_NONE, enc, h->cfg.enc_dim, h->we, h->cfg.enc_dim, rows, h->cfg.join_dim,
                       h->cfg.enc_dim, e, st);
   if (r) return set_error(CFM_ERR_RUNTIME, std::string("rnnt enc_ffn gemm: ") + hipGetErrorString((hipError_t)r));
-  const int G = cfm_rnnt_grid_blocks(h, B);
+  const int G = (flags & CFM_RNNT_ONE_WORKGROUP) ? 0 : cfm_rnnt_grid_blocks(h, B);
   if (G > 0) {
     // grid path: zeroed state slots, counters and error word, then G workgroups per utterance
     const size_t proj_b = ((size_t)rows * h->cfg.join_dim * sizeof(float) + 255) / 256 * 256;

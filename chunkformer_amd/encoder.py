@@ -94,7 +94,7 @@ class ChunkFormerEncoder:
         self._native_opts[key] = int(value)
 
     # the native options' values before any set_option (csrc/cfm_kernels.h Tuning)
-    _NATIVE_DEFAULTS = {"wsp_small_div": 1, "wsp_small_rows": 32768, "attn_min_chunks": 2, "attn_q32": 0,
+    _NATIVE_DEFAULTS = {"wsp_small_div": 1, "wsp_small_rows": 32768, "attn_min_chunks": 2,
                         "gemm_big_min": 0}
 
     @contextlib.contextmanager

@@ -35,7 +35,7 @@ import torch
 
 from .config import EncoderConfig
 from .encoder import ChunkFormerEncoder
-from .streaming import EndlessGraphPipeline, EndlessGraphRunner, EndlessPipeline, retire_graphs
+from .streaming import EndlessGraphPipeline, EndlessGraphRunner, EndlessPipeline
 from .transducer import RNNTConfig, RNNTGreedy
 
 Features = Union[torch.Tensor, np.ndarray, str]
@@ -340,15 +340,15 @@ class ChunkFormerModel:
         key = (C, L, R, trunc, seg_len, want_eo, bool(cuda_graph), bool(pipeline), int(pipeline_depth), trim, fe_reuse)
         runner = self._endless_runners.get(key)
         if runner is None:   # graphs are captured once per segment geometry and reused across calls
+            for old in self._endless_runners.values():   # the replaced runner's graphs are destroyed
+                old.close()
+            self._endless_runners = {}
             if pipeline:
                 runner = (EndlessGraphPipeline(enc, C, L, R, trunc, seg_len, want_eo, pipeline_depth, trim=trim,
                                                fe_reuse=fe_reuse)
                           if cuda_graph else EndlessPipeline(enc, C, L, R, trunc, want_eo, pipeline_depth, trim=trim))
             else:
                 runner = EndlessGraphRunner(enc, C, L, R, trunc, seg_len, want_eo, use_graph=cuda_graph, trim=trim)
-            for old in self._endless_runners.values():   # their captured graphs outlive them (streaming.py)
-                g = getattr(old, "graphs", None) or []
-                retire_graphs(g.values() if isinstance(g, dict) else g)
             self._endless_runners = {key: runner}
         if pipeline:
             tids, teos, cur = runner.run(xs_dev, segs)

@@ -20,23 +20,23 @@ instead of replaying the wrong masks.
 """
 from __future__ import annotations
 
+from collections import OrderedDict
 from typing import List, Optional
 
 import torch
 
 from . import _lib
 
-# Captured graphs are never destroyed while the process runs: on ROCm 7.2 a HIP graph of this multi-stream
-# pipeline destroyed (its runner replaced by another segment geometry or pipeline mode) was followed by a host
-# segfault inside a LATER graph launch (the test sequence of three models' endless_decode modes in one process,
-# any dtypes; keeping the runners alive or parking their graphs here removes it).  A retired graph keeps only
-# its node parameters and its (empty) capture pool; the runner's buffers are freed, and it is never replayed.
-_RETIRED_GRAPHS: list = []
-
-
-def retire_graphs(graphs) -> None:
-    """Park `graphs` (CUDAGraph objects, or tuples holding them) so that they are never destroyed."""
-    _RETIRED_GRAPHS.extend(g for g in graphs if g is not None)
+def destroy_graphs(entries, device) -> None:
+    """Destroy captured graphs (CUDAGraph objects, or (graph, events) tuples): the device is synchronised
+    first, so no replay of them is still in flight when hipGraphExecDestroy runs, then each graph is reset
+    before the events recorded during its capture (kept beside it) are released."""
+    entries = [e for e in entries if e is not None]
+    if not entries:
+        return
+    torch.cuda.synchronize(device)
+    for e in entries:
+        (e[0] if isinstance(e, tuple) else e).reset()
 
 
 class EndlessGraphRunner:
@@ -67,6 +67,12 @@ class EndlessGraphRunner:
         self.cur = 0
         self.att[0].zero_()
         self.cnn[0].zero_()
+
+    def close(self) -> None:
+        """Destroy the captured graphs (the runner is being replaced); the buffers go with the runner."""
+        destroy_graphs(self.graphs, self.dev)
+        self.graphs = [None, None]
+        self.g_plan = None
 
     # ------------------------------------------------------------------ eager step
     def _eager(self, x: torch.Tensor, offset: int, keep_trunc: bool):
@@ -205,6 +211,10 @@ class EndlessPipeline:
         self.ws: List[Optional[torch.Tensor]] = [None] * depth
         self.out: List[Optional[torch.Tensor]] = [None] * depth
 
+    def close(self) -> None:
+        """Nothing captured: the streams' last work is joined so the buffers can go."""
+        torch.cuda.synchronize(self.dev)
+
     def _buf(self, lst, i, nbytes, dtype, shape=None):
         t = lst[i]
         need = nbytes if shape is None else int(torch.Size(shape).numel())
@@ -311,8 +321,12 @@ class EndlessGraphPipeline:
     front-end windows -- the previous segment's last complete ones, the same frames -- are copied from
     a carry buffer the previous segment's stage -1 filled (native fe_carry), not recomputed."""
 
+    # captured block graphs kept per runner (least recently replayed destroyed first): a service decoding
+    # inputs of many lengths holds at most this many, each with its events and no allocations
+    MAX_GRAPHS = 8
+
     def __init__(self, encoder, C: int, L: int, R: int, trunc: int, seg_len: int, want_out: bool, depth: int = 3,
-                 block: int = 128, trim: bool = False, fe_reuse: bool = False):
+                 block: int = 128, trim: bool = False, fe_reuse: bool = False, max_graphs: int = MAX_GRAPHS):
         if depth < 1:
             raise ValueError(f"pipeline depth {depth} < 1")
         self.enc = encoder
@@ -340,17 +354,26 @@ class EndlessGraphPipeline:
         self.g_feats: List[Optional[torch.Tensor]] = [None] * self.block
         self.g_ids: List[Optional[torch.Tensor]] = [None] * self.block
         self.g_eo: List[Optional[torch.Tensor]] = [None] * self.block
-        self.graphs: dict = {}
+        # block key -> (graph, events recorded in its capture), least recently replayed first
+        self.graphs: "OrderedDict[tuple, tuple]" = OrderedDict()
+        self.max_graphs = max(1, int(max_graphs))
         self.plans: dict = {}   # plan bytes -> (host plan, device plan, id): the graphs' plan inputs
+        self._next_pid = 0
         self.vocab = cfg.vocab
         self.replayed = 0   # segments replayed from graphs in the last run (tests / bench)
+        self.captures = 0   # graphs captured over the runner's life (tests)
+
+    def close(self) -> None:
+        """Destroy every captured graph (runner replaced, or a buffer the graphs point at reallocated)."""
+        destroy_graphs(list(self.graphs.values()), self.dev)
+        self.graphs.clear()
 
     def _buf(self, lst, i, n, dtype) -> torch.Tensor:
         t = lst[i]
         if t is None or t.numel() < n:
+            self.close()   # the captured graphs hold the old buffer's address (and may still run on it)
+            lst[i] = None
             lst[i] = torch.empty(n, dtype=dtype, device=self.dev)
-            retire_graphs(self.graphs.values())   # captured graphs hold the old buffer's address
-            self.graphs.clear()
         return lst[i]
 
     def _segment(self, seg: dict, prev, ids_dst, eo_dst):
@@ -440,9 +463,9 @@ class EndlessGraphPipeline:
                     a["save_from"], b["reuse"] = self.trunc // C, n_c
             need = max([(s_["N"] - s_["save_from"]) * C * d for s_ in info if s_["save_from"] >= 0] + [0])
             if need and (self.carry is None or self.carry.numel() < need):
+                self.close()   # the captured graphs hold the old carry's address
+                self.carry = None
                 self.carry = torch.empty(need, dtype=torch.float32, device=self.dev)
-                retire_graphs(self.graphs.values())   # captured graphs hold the old carry's address
-                self.graphs.clear()
         # every segment runs from a captured graph: device plans are kept per distinct plan (the middle
         # segments share one; the first, offset-0 segment and the ragged last one have their own), and a
         # block's graph is keyed by its phase and its segments' plans / lengths / kept rows, so the middle
@@ -451,7 +474,8 @@ class EndlessGraphPipeline:
             pk = s["plan"].numpy().tobytes()
             ent = self.plans.get(pk)
             if ent is None:
-                ent = (s["plan"], enc._upload(s["plan"]), len(self.plans))
+                ent = (s["plan"], enc._upload(s["plan"]), self._next_pid)
+                self._next_pid += 1
                 self.plans[pk] = ent
             s["plan"], s["plan_dev"], s["pid"] = ent
         max_rows = max([s["rows"] for s in info] + [1])
@@ -480,6 +504,9 @@ class EndlessGraphPipeline:
             key = (phase, tuple((s["pid"], s["len"], s["rows"], s["keep"], s["reuse"], s["save_from"])
                                 for s in info[k0: k0 + cnt]))
             entry = self.graphs.get(key)
+            if entry is None and len(self.graphs) >= self.max_graphs:
+                # the least recently replayed graph goes (after a device sync: it may still be running)
+                destroy_graphs([self.graphs.popitem(last=False)[1]], self.dev)
             if entry is None:
                 g = torch.cuda.CUDAGraph()
                 cap = self.streams[0]
@@ -509,7 +536,9 @@ class EndlessGraphPipeline:
                         edge(cap, st)
                 entry = (g, keep)
                 self.graphs[key] = entry
+                self.captures += 1
                 caller.wait_stream(cap)
+            self.graphs.move_to_end(key)
             entry[0].replay()
             self.replayed += cnt
             for i in range(cnt):
@@ -523,4 +552,8 @@ class EndlessGraphPipeline:
         for st in self.streams:
             caller.wait_stream(st)
         self._keep = info
+        # device plans no live graph and no segment of this run refers to are released
+        live = {p for key in self.graphs for p, *_ in key[1]} | {s["pid"] for s in info}
+        for pk in [pk for pk, ent in self.plans.items() if ent[2] not in live]:
+            del self.plans[pk]
         return ids_out, eo_out, n % 2

@@ -252,19 +252,16 @@ class RNNTGreedy:
         if G:
             # the multi-CU search stops early if a grid barrier timed out (its workgroups were not all resident:
             # CUs held by another stream's kernels): never return that partial result, run the search again
-            # on the one-workgroup kernel, which needs no co-residency
+            # on the one-workgroup kernel, which needs no co-residency (a per-call flag: the handle's options and
+            # grid weight image stay as they are, so no device sync and no other caller is disturbed)
             torch.cuda.current_stream(self.device).synchronize()
             if int(_lib.cfm_rnnt_error(self._h, ws.data_ptr(), rows)) != 0:
                 self.grid_fallbacks += 1
-                self.set_option("grid_blocks", 0)
-                try:
-                    out.zero_()
-                    _lib.check(_lib.cfm_rnnt_greedy(self._h, enc.data_ptr(), rows, rs_d.data_ptr(), rl_d.data_ptr(),
-                                                    B, int(n_steps), out.data_ptr(), ws.data_ptr(), nbytes,
-                                                    torch.cuda.current_stream(self.device).cuda_stream))
-                    torch.cuda.current_stream(self.device).synchronize()
-                finally:
-                    self.set_option("grid_blocks", G)
+                out.zero_()
+                _lib.check(_lib.cfm_rnnt_greedy_ex(self._h, enc.data_ptr(), rows, rs_d.data_ptr(), rl_d.data_ptr(),
+                                                   B, int(n_steps), out.data_ptr(), ws.data_ptr(), nbytes,
+                                                   _lib.CFM_RNNT_ONE_WORKGROUP,
+                                                   torch.cuda.current_stream(self.device).cuda_stream))
         return out
 
     @torch.no_grad()

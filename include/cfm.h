@@ -288,6 +288,13 @@ size_t cfm_rnnt_workspace_bytes(const cfm_rnnt* h, int32_t rows);
 cfm_status cfm_rnnt_greedy(const cfm_rnnt* h, const float* enc_dev, int32_t rows, const int32_t* row_start_dev,
                            const int32_t* row_len_dev, int32_t B, int32_t n_steps, int32_t* out_dev, void* workspace,
                            size_t workspace_bytes, cfm_stream stream);
+/* cfm_rnnt_greedy with per-call flags: CFM_RNNT_ONE_WORKGROUP runs this call on the one-workgroup kernel
+ * whatever "grid_blocks" says (the caller's rerun after a grid barrier timed out), leaving the handle's
+ * options and its grid weight image untouched. */
+#define CFM_RNNT_ONE_WORKGROUP 1
+cfm_status cfm_rnnt_greedy_ex(const cfm_rnnt* h, const float* enc_dev, int32_t rows, const int32_t* row_start_dev,
+                              const int32_t* row_len_dev, int32_t B, int32_t n_steps, int32_t* out_dev, void* workspace,
+                              size_t workspace_bytes, int32_t flags, cfm_stream stream);
 /* Options: "grid_lds" (default 1) caches each workgroup's weight slices in LDS when they fit;
  * "grid_atomic" (default 1) exchanges the shared vectors by agent-scope atomics instead of fences;
  * "grid_blocks" = workgroups per utterance of the multi-CU search (default 32; 0 = one

@@ -27,27 +27,11 @@ typedef enum { CFM_ACT_NONE = 0, CFM_ACT_RELU = 1, CFM_ACT_SILU = 2 } cfm_act;
  * variant (A/B testing): bit 0 forces the 128x128 kernel; bits 8-15 select a timing diagnostic of
  * the bf16 kernels (1 no MFMA, 2 no DMA in the loop, 3 no epilogue, 5 no stores; 0 = normal; only
  * in a library built with -DCFM_GEMM_DIAG); bits 16-17 the bf16 store policy (2 = nt); bits 18-20 the
- * K = 512 weight-stationary kernel (0 = model default, 1 = on, 2 = on at any M, 7 = off); bit 21 runs the
- * N = 512, K >= 1024 shapes on the full-row 128 x 512 kernel (gemm_rowln.hip, plain form). */
+ * K = 512 weight-stationary kernel (0 = model default, 1 = on, 2 = on at any M, 7 = off). */
 cfm_status cfm_op_gemm(int32_t dtype, int32_t epi, int32_t act, const void* A, int32_t lda, const void* W, int32_t ldw,
                        int32_t M, int32_t N, int32_t K, const float* bias, float alpha, void* out, int32_t ldo,
                        int32_t row_off, void* out2, int32_t d, float* x, int32_t ldx, const uint8_t* rowmask,
                        int32_t variant, cfm_stream stream);
-
-/* Row-owning bf16 GEMM with the residual add and LayerNorm(s) of an encoder sub-block in its epilogue
- * (N = 512, K % 64 == 0; replaces a branch's last Linear plus the nn.LayerNorm after it,
- * encoder_layer.py:155-248).  With v = bf16(A . W^T + bias):
- *   xn = x + a1 * y1mask[m] * y1 + alpha * accmask[m] * v        (y1 / masks optional: NULL)
- *   y_out = v;  one LayerNorm (g2 NULL): x_out = xn, z = LN(xn; g1, b1)
- *               two:  x_out = LN(xn; g1, b1), z = LN(x_out; g2, b2)
- *   h_out = bf16(z) with rows of hmask 0 zeroed, or f_out = z (f32); x_out may equal x.
- * x, x_out, f_out: [M, 512] f32; y1, y_out, h_out, ybuf: [M, 512] bf16 (ybuf: scratch for v when y_out is
- * NULL).  K >= 512.  variant (timing diagnostics, libraries built with CFM_GEMM_DIAG): 1 = GEMM only. */
-cfm_status cfm_op_gemm_rowln(const void* A, int32_t lda, const void* W, int32_t ldw, int32_t M, int32_t K,
-                             const float* bias, float alpha, const uint8_t* accmask, const float* x, const void* y1,
-                             float a1, const uint8_t* y1mask, void* y_out, float* x_out, const float* g1,
-                             const float* b1, const float* g2, const float* b2, void* h_out, float* f_out,
-                             const uint8_t* hmask, void* ybuf, float eps, int32_t variant, cfm_stream stream);
 
 #ifdef __cplusplus
 }

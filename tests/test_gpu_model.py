@@ -190,8 +190,38 @@ def test_endless_graph_pipeline_lengths(small, dtype):
             runner = next(iter(m._endless_runners.values()))
             assert runner.replayed == len(runner._keep) > 0, (n, depth)
             if (depth, n) in seen:   # the same length again: its graphs are reused, none captured
-                assert len(runner.graphs) == seen[(depth, n)], (n, depth)
-            seen[(depth, n)] = len(runner.graphs)
+                assert runner.captures == seen[(depth, n)], (n, depth)
+            seen[(depth, n)] = runner.captures
+            assert len(runner.graphs) <= runner.max_graphs
+
+
+def test_endless_graphs_bounded_over_many_lengths(small):
+    """A long-lived process decoding many distinct input lengths (a service) holds a bounded number of
+    captured graphs and device plans: the least recently replayed graph is destroyed once the runner
+    holds max_graphs, a replaced runner destroys its own, and every call stays bit-identical to the
+    eager loop.  Replacing runners in between (pipeline depth / mode changes) destroys their graphs too."""
+    from chunkformer_amd.weights import synthetic_features
+    g, models = small
+    C, L, R, tbd = (int(v) for v in g["endless_clrt"])
+    m = models["fp32"]
+    lens = [2100 + 97 * i for i in range(14)]
+    xs = [synthetic_features([n], 300 + i)[0] for i, n in enumerate(lens)]
+    for depth in (4, 2):
+        res = []
+        for n, x in zip(lens, xs):   # one runner throughout: its graphs are evicted, not the runner replaced
+            res.append(m.endless_decode(x, C, L, R, total_batch_duration=tbd, return_encoder_out=True,
+                                        cuda_graph=True, pipeline=True, pipeline_depth=depth))
+            runner = next(iter(m._endless_runners.values()))
+            assert runner.replayed == len(runner._keep) > 0
+            assert len(runner.graphs) <= runner.max_graphs, (n, depth)
+            live = {p for key in runner.graphs for p, *_ in key[1]}
+            assert {e[2] for e in runner.plans.values()} <= live | {s_["pid"] for s_ in runner._keep}
+        assert runner.captures >= len(lens) > runner.max_graphs   # graphs were destroyed along the way
+        for n, x, (ids_p, eo_p) in zip(lens, xs, res):   # (replaces the graph runner: its graphs destroyed)
+            ids_e, eo_e = m.endless_decode(x, C, L, R, total_batch_duration=tbd, return_encoder_out=True,
+                                           cuda_graph=False, pipeline=False)
+            assert torch.equal(eo_p, eo_e) and torch.equal(ids_p, ids_e), (n, depth)
+
 
 @pytest.mark.parametrize("dtype", ["fp32", "bf16", "fp16"])
 def test_endless_decode_larger_segments_match_reference(small, golden_dir, dtype):
@@ -226,22 +256,25 @@ def test_endless_trim_equals_full(small, dtype):
     computation, in the one-segment-at-a-time loop and in the graph-replayed pipeline."""
     from chunkformer_amd.weights import synthetic_features
     g, models = small
-    C, L, R, tbd = (int(v) for v in g["endless_clrt"])
     x = synthetic_features([6000], int(g["endless_seed"]))[0]
     m = models[dtype]
+    # the fixture geometry, R not a multiple of C (24 / 16, 20 / 8), and short segments (tbd 4 / 3: 5-7
+    # chunks, so the per-layer reach kept + (nb - 1 - l)(ceil(7/C) + ceil(R/C)) is clamped by n_ch)
+    geoms = [tuple(int(v) for v in g["endless_clrt"]), (16, 32, 24, 4), (8, 16, 20, 3)]
     try:
-        for graph, pipe in ((False, False), (True, False), (True, True)):
-            res = {}
-            for trim in (False, True):
-                m.endless_trim = trim
-                ids, eo = m.endless_decode(x, C, L, R, total_batch_duration=tbd, return_encoder_out=True,
-                                           cuda_graph=graph, pipeline=pipe)
-                res[trim] = (ids, eo, [c.clone() for c in m.last_endless_caches])
-            (i0, e0, c0), (i1, e1, c1) = res[False], res[True]
-            assert torch.equal(e0, e1), (graph, pipe)
-            assert torch.equal(i0, i1), (graph, pipe)
-            for a, b in zip(c0, c1):
-                assert torch.equal(a, b), (graph, pipe)
+        for C, L, R, tbd in geoms:
+            for graph, pipe in ((False, False), (True, False), (True, True)):
+                res = {}
+                for trim in (False, True):
+                    m.endless_trim = trim
+                    ids, eo = m.endless_decode(x, C, L, R, total_batch_duration=tbd, return_encoder_out=True,
+                                               cuda_graph=graph, pipeline=pipe)
+                    res[trim] = (ids, eo, [c.clone() for c in m.last_endless_caches])
+                (i0, e0, c0), (i1, e1, c1) = res[False], res[True]
+                assert torch.equal(e0, e1), (C, L, R, tbd, graph, pipe)
+                assert torch.equal(i0, i1), (C, L, R, tbd, graph, pipe)
+                for a, b in zip(c0, c1):
+                    assert torch.equal(a, b), (C, L, R, tbd, graph, pipe)
     finally:
         m.endless_trim = True
 
@@ -272,7 +305,7 @@ def test_random_endless_matches_oracle(small, seed):
         np.testing.assert_allclose(cnn.cpu().numpy(), cc.numpy(), atol=1e-4, rtol=0)
 
 
-@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+@pytest.mark.parametrize("dtype", ["fp32", "bf16", "fp16"])
 def test_endless_fe_reuse_equals_recompute(small, dtype):
     """The graph pipeline carrying each segment's last complete front-end windows into the next
     segment (native fe_carry / fe_reuse / fe_save_from, model.endless_fe_reuse) gives exactly the rows,

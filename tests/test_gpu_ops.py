@@ -37,14 +37,13 @@ def _close(got, exp, tol):
 
 
 SHAPES = [(1000, 512, 512), (700, 2048, 512), (513, 512, 2048), (256, 256, 4608), (300, 48, 128),
-          (70001, 512, 2048), (2000, 512, 4608), (129, 512, 1024),   # full-row 128 x 512 tiles (N = 512, K >= 1024)
+          (70001, 512, 2048), (2000, 512, 4608), (129, 512, 1024),   # N = 512, K >= 1024 (FFN w2, front-end out)
           (70001, 512, 512), (33000, 2048, 512),   # these two run the K = 512 weight-in-registers kernel
           (40000, 1536, 512),
           (1000, 256, 128), (4097, 768, 384)]      # shortest ring K (4 steps); K % 128 != 0 (K-64 kernel)
 # variant bits (include/cfm_ops.h): 1 = 128x128 tiles; 7 << 18 = K = 512 weight-stationary kernel off
-# (the 256 x 256 kernel takes its shapes); 2 << 16 = nt stores; 1 << 21 = the N = 512, K >= 1024 shapes on the
-# full-row 128 x 512 kernel (gemm_rowln.hip) instead of 256 x 256 tiles
-MODES = [("bf16", 0), ("bf16", 1), ("fp32", 0), ("bf16", 7 << 18), ("bf16", 2 << 16), ("bf16", 1 << 21),
+# (the 256 x 256 kernel takes its shapes); 2 << 16 = nt stores
+MODES = [("bf16", 0), ("bf16", 1), ("fp32", 0), ("bf16", 7 << 18), ("bf16", 2 << 16),
          ("fp16", 0), ("fp16", 1), ("fp16", 7 << 18)]   # fp16: the same kernels on f16 MFMA (EpiArgs::f16)
 
 

@@ -421,23 +421,6 @@ def test_ring_kernel_shapes_vs_generic(large, C, L, R):
     assert rel <= 5e-3
 
 
-@pytest.mark.parametrize("C,L,R,variant", [(64, 128, 128, 3), (64, 128, 128, 2), (64, 128, 128, 1), (64, 64, 64, 3),
-                                           (64, 0, 0, 3), (64, 128, 0, 3), (64, 16, 16, 3), (64, 96, 32, 3)])
-def test_q32_kernel_vs_generic(large, C, L, R, variant):
-    """The 32-queries-per-wave dk = 64 kernel (attention_q32.hip, model option attn_q32 = 1 / 2 / 3:
-    half after half, software-pipelined, pipelined with the branch-free rescale) against the generic
-    kernel over the window sizes it accepts (C = 64, W = L + 64 + R = 64 .. 320, W % 32 == 0)."""
-    _, _, models = large
-    enc = models["bf16"]
-    enc.set_option("attn_q32", variant)
-    try:
-        rel = _fast_vs_generic(enc, [20_000, 519, 3000, 7, 1100, 9000], 23, C, L, R)
-    finally:
-        enc.set_option("attn_q32", 0)
-    print(f"q32 kernel ({variant}) vs generic (C={C} L={L} R={R}): rel-L2 {rel:.2e}")
-    assert rel <= 5e-3
-
-
 @pytest.mark.parametrize("dtype", ["fp32", "bf16"])
 def test_small256_recipe_shape(dtype):
     """The reference's shipped small recipes (d=256, 4 heads, ff 2048, 12 blocks, bpe1024;
