@@ -153,17 +153,30 @@ def cpu_baseline(lens_all, budget_s: float = 12.0):
                                       "ms_per_utterance": round(t1 / reps * 1e3, 1), "reps": reps}}
 
 
+def newest_profile(kind: str):
+    """The committed profile summary profiles/r<NN>[_final]_<kind>.json of the latest round (the round's
+    final-build profile over its earlier ones): ordered by round number, not by name ('f' < 't' made a
+    name sort pick an earlier build's file); None if absent."""
+    import glob
+    import re
+    best, key = None, None
+    for f in glob.glob(os.path.join(ROOT, "profiles", f"r*_{kind}.json")):
+        m = re.match(r"r(\d+)(_final)?_" + kind + r"\.json$", os.path.basename(f))
+        if m and (key is None or (int(m.group(1)), bool(m.group(2))) > key):
+            best, key = f, (int(m.group(1)), bool(m.group(2)))
+    return best
+
+
 def committed_traffic(cls: str = "ffn_w1_gemm"):
     """HBM bytes per launch of the roofline kernel from the newest committed PMC summary
     (profiles/<round>_traffic.json, made by tools/profile_round.sh with rocprofv3
     FETCH_SIZE/WRITE_SIZE passes on this same workload); None if absent."""
-    import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_traffic.json")))
-    if not files:
+    f = newest_profile("traffic")
+    if not f:
         return None, None
     try:
-        ent = json.load(open(files[-1]))["kernels"].get(cls)
-        return (float(ent[0]["hbm_bytes_per_launch"]), os.path.relpath(files[-1], ROOT)) if ent else (None, None)
+        ent = json.load(open(f))["kernels"].get(cls)
+        return (float(ent[0]["hbm_bytes_per_launch"]), os.path.relpath(f, ROOT)) if ent else (None, None)
     except (OSError, ValueError, KeyError, IndexError):
         return None, None
 
@@ -172,13 +185,12 @@ def committed_mfma_busy(cls: str = "ffn_w1_gemm"):
     """MFMA busy fraction and effective clock of the roofline kernel from the newest committed PMC
     summary (profiles/<round>_mfma_busy.json, tools/profile_round.sh: GRBM_GUI_ACTIVE +
     SQ_VALU_MFMA_BUSY_CYCLES over this same workload); (None, None, None) if absent."""
-    import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_mfma_busy.json")))
-    if not files:
+    f = newest_profile("mfma_busy")
+    if not f:
         return None, None, None
     try:
-        ent = json.load(open(files[-1]))["kernels"].get(cls)
-        return ((ent["mfma_busy"], ent["clock_ghz"], os.path.relpath(files[-1], ROOT)) if ent else (None, None, None))
+        ent = json.load(open(f))["kernels"].get(cls)
+        return ((ent["mfma_busy"], ent["clock_ghz"], os.path.relpath(f, ROOT)) if ent else (None, None, None))
     except (OSError, ValueError, KeyError):
         return None, None, None
 
@@ -201,11 +213,10 @@ def class_rooflines(prof, n_chunks: int, cfg, dtype: str, profiled: bool):
            "conv_dw_ln_silu": ("conv_dw_ln_silu",), "frontend_conv0_dw": ("frontend_conv0_dw",)}
     traffic = {}
     if profiled:
-        import glob
-        files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_traffic.json")))
-        if files:
+        f = newest_profile("traffic")
+        if f:
             try:
-                traffic = json.load(open(files[-1]))["kernels"]
+                traffic = json.load(open(f))["kernels"]
             except (OSError, ValueError, KeyError):
                 traffic = {}
     out = {}

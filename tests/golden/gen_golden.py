@@ -271,6 +271,30 @@ def gen_large_full(path, seed=0):
                         lens=np.array(lens, np.int32), out=y.numpy(), mask=masks.numpy())
 
 
+FULL_MIXED_LENS = [3000, 2987, 2456, 1900, 1333, 1001, 640, 333, 96]
+
+
+def gen_large_full_mixed(path, seed=0):
+    """configs[4] as the bench runs it, at 9 utterances: full attention (chunk_size 0) over a padded batch
+    of mixed lengths (30 s down to 1 s: every key-padding case of the dense kernel, T' = 374 .. 11), 12
+    layers, with the CTC head's ids and top-2 margins; only the valid rows are stored."""
+    cfg = LARGE
+    enc, ctc, sd = build_reference(cfg, seed)
+    lens = FULL_MIXED_LENS
+    xs = feats(lens, 17)
+    xp = torch.zeros(len(lens), max(lens), 80)
+    for i, t in enumerate(xs):
+        xp[i, : t.shape[0]] = t
+    with torch.no_grad():
+        y, masks = enc.forward_encoder(xp, torch.tensor(lens), 0, 0, 0)
+        logp = ctc.log_softmax(y)
+    valid = masks[:, 0, :].numpy()
+    top2 = torch.topk(logp, 2, dim=-1).values.numpy()[valid]
+    np.savez_compressed(path, sd_digest=sd_digest(sd), seed=np.array(seed), feat_seed=np.array(17),
+                        lens=np.array(lens, np.int32), mask=masks.numpy(), out=y.numpy()[valid],
+                        ids=logp.argmax(-1).numpy()[valid].astype(np.int32), margin=top2[:, 0] - top2[:, 1])
+
+
 def gen_text(path):
     """Text post-processing of the reference (utils/model_utils.py: get_output 164-171,
     get_output_with_timestamps 174-221) on (a) seeded id streams with long blank runs and repeats,
@@ -744,7 +768,8 @@ def gen_rnnt_memory(path, seed=3, n_steps=64, dir_seed=11):
 
 if __name__ == "__main__":
     which = sys.argv[1:] or ["masks", "small", "large", "large_4h", "large_endless", "large_full", "text", "stream",
-                             "endless_tbd", "rnnt", "rows_neq", "small256", "rnnt_sparse", "rnnt_memory", "autocast", "endless_tail", "tiny_batch", "tiny_padded"]
+                             "endless_tbd", "rnnt", "rows_neq", "small256", "rnnt_sparse", "rnnt_memory", "autocast", "endless_tail", "tiny_batch", "tiny_padded",
+                             "large_full_mixed"]
     if "masks" in which:
         gen_masks(os.path.join(HERE, "masks.npz"))
     if "small" in which:
@@ -781,4 +806,6 @@ if __name__ == "__main__":
         gen_tiny_batch(os.path.join(HERE, "tiny_batch.npz"))
     if "tiny_padded" in which:
         gen_tiny_padded(os.path.join(HERE, "tiny_padded.npz"))
+    if "large_full_mixed" in which:
+        gen_large_full_mixed(os.path.join(HERE, "large_full_mixed.npz"))
     print("ok", which)

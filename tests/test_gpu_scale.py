@@ -296,6 +296,47 @@ def test_large_endless_decode(large, dtype):
     assert torch.equal(m.last_endless_caches[0], ac) and torch.equal(m.last_endless_caches[1], cc)
 
 
+def test_large_endless_multi_block_graphs_equal_eager(large):
+    """configs[3] as the bench runs it (chunkformer-large, bf16, C=64 L=R=128, the graph-replayed pipeline
+    with trim_right and fe_reuse), on an input long enough for TWO block graphs: 1.3 M frames at tbd 200 =
+    134 segments = a 128-segment block + a 6-segment block.  Rows, CTC ids and the final caches equal the
+    one-segment-at-a-time eager loop with trim_right off bit for bit, and so do the graph pipeline with
+    trim / fe_reuse off and the eager pipeline (chunkformer_model.py:344-435 is the eager loop's model)."""
+    from chunkformer_amd.config import LARGE
+    from chunkformer_amd.model import ChunkFormerModel
+    from chunkformer_amd.weights import synthetic_features
+    _, sd, _ = large
+    m = ChunkFormerModel(LARGE, sd, dtype="bf16")
+    x = synthetic_features([1_300_000], 91)[0]
+    kw = dict(total_batch_duration=200, return_encoder_out=True)
+
+    def run(trim, reuse, **mode):
+        m.endless_trim, m.endless_fe_reuse = trim, reuse
+        ids, eo = m.endless_decode(x, 64, 128, 128, **kw, **mode)
+        return ids, eo, [c.clone() for c in m.last_endless_caches]
+
+    try:
+        ids0, eo0, c0 = run(False, False, cuda_graph=False, pipeline=False)
+        assert eo0.shape[1] > 150_000
+        for trim, reuse, mode in ((True, True, dict(cuda_graph=True, pipeline=True)),
+                                  (False, False, dict(cuda_graph=True, pipeline=True)),
+                                  (True, True, dict(cuda_graph=False, pipeline=True))):
+            ids, eo, c = run(trim, reuse, **mode)
+            tag = (trim, reuse, mode)
+            assert torch.equal(eo, eo0), tag
+            assert torch.equal(ids, ids0), tag
+            assert all(torch.equal(a, b) for a, b in zip(c, c0)), tag
+            if mode["cuda_graph"]:
+                runner = next(iter(m._endless_runners.values()))
+                assert runner.replayed == len(runner._keep) == 134, tag   # every segment from a graph
+                assert len(runner.graphs) == 2, tag                        # two blocks: 128 + 6
+                if reuse:
+                    assert sum(s_["reuse"] for s_ in runner._keep) > 0
+            del ids, eo, c
+    finally:
+        m.endless_trim, m.endless_fe_reuse = True, True
+
+
 @pytest.mark.parametrize("dtype", ["fp32", "bf16"])
 def test_large_full_attention(large, dtype):
     """configs[4] geometry: full attention (chunk_size 0), padded 30 s + 21 s batch, 12 layers."""
@@ -317,6 +358,44 @@ def test_large_full_attention(large, dtype):
         np.testing.assert_allclose(o, exp, atol=1e-4, rtol=0)
     else:
         assert _rel_l2(o, exp) <= BF16_RELL2
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_large_full_attention_mixed_batch(large, dtype):
+    """configs[4] as the bench runs it (dense bf16 kernel, padded batch of utterances <= 30 s), pinned at 9
+    utterances of 30 s down to 1 s (large_full_mixed.npz, reference-generated): masks bit-exact, valid rows
+    (fp32 1e-4; bf16 rel-L2 per utterance), CTC ids (fp32: where the reference's margin > 1e-3; bf16: >= 99%
+    overall and every id whose margin exceeds BF16_MARGIN)."""
+    from chunkformer_amd.weights import synthetic_features
+    from conftest import GOLDEN
+    _, _, models = large
+    g = np.load(os.path.join(GOLDEN, "large_full_mixed.npz"))
+    lens = g["lens"].tolist()
+    xs = synthetic_features(lens, int(g["feat_seed"]))
+    xp = torch.zeros(len(lens), max(lens), 80)
+    for i, t in enumerate(xs):
+        xp[i, : t.shape[0]] = t
+    enc = models[dtype]
+    y, masks = enc.forward_encoder(xp, torch.tensor(lens), 0, 0, 0)
+    np.testing.assert_array_equal(masks.cpu().numpy(), g["mask"])
+    valid = torch.from_numpy(g["mask"][:, 0, :]).to(y.device)
+    rows = y[valid].contiguous()
+    _, ids = enc.ctc_log_softmax(rows, want_logp=False)
+    o, ids = rows.cpu().numpy(), ids.cpu().numpy()
+    if dtype == "fp32":
+        np.testing.assert_allclose(o, g["out"], atol=1e-4, rtol=0)
+        sure = g["margin"] > 1e-3
+        np.testing.assert_array_equal(ids[sure], g["ids"][sure])
+    else:
+        starts = np.cumsum([0] + g["mask"][:, 0, :].sum(-1).tolist())
+        for u in range(len(lens)):
+            r = _rel_l2(o[starts[u]: starts[u + 1]], g["out"][starts[u]: starts[u + 1]])
+            assert r <= BF16_RELL2, (u, lens[u], r)
+        agree = (ids == g["ids"]).mean()
+        print(f"bf16 full attention, 9 utterances: rel-L2 {_rel_l2(o, g['out']):.2e}, CTC argmax agreement {agree:.4f}")
+        assert agree >= 0.99
+        big = g["margin"] > BF16_MARGIN
+        np.testing.assert_array_equal(ids[big], g["ids"][big])
 
 
 @pytest.mark.parametrize("dtype", ["fp32", "bf16"])

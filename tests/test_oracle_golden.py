@@ -281,6 +281,25 @@ def test_large_full_attention_matches_reference(golden_dir):
     np.testing.assert_allclose(y.numpy(), g["out"], atol=1e-4, rtol=0)
 
 
+def test_large_full_mixed_matches_reference(golden_dir):
+    """configs[4] as benched, at 9 padded utterances of 30 s .. 1 s (large_full_mixed.npz): full attention,
+    12 layers, valid rows and the CTC ids wherever the reference's top-2 margin exceeds 1e-3."""
+    g = _load(golden_dir, "large_full_mixed.npz")
+    sd = synthetic_state_dict(LARGE, int(g["seed"]))
+    lens = g["lens"].tolist()
+    xs = synthetic_features(lens, int(g["feat_seed"]))
+    xp = torch.zeros(len(lens), max(lens), 80)
+    for i, t in enumerate(xs):
+        xp[i, : t.shape[0]] = t
+    y, masks = ref.forward_encoder(sd, LARGE, xp, lens, 0, 0, 0)
+    np.testing.assert_array_equal(masks.numpy(), g["mask"])
+    valid = g["mask"][:, 0, :]
+    np.testing.assert_allclose(y.numpy()[valid], g["out"], atol=1e-4, rtol=0)
+    ids = (y[torch.from_numpy(valid)] @ sd["ctc.ctc_lo.weight"].T + sd["ctc.ctc_lo.bias"]).argmax(-1).numpy()
+    sure = g["margin"] > 1e-3
+    np.testing.assert_array_equal(ids[sure], g["ids"][sure])
+
+
 def _stream_steps(g, tag, cfg, seed0, sd):
     from chunkformer_amd.weights import synthetic_features
     from oracle import encoder_ref as ref
