@@ -2,7 +2,9 @@
 
     python tools/graph_destroy_probe.py nosync     # destroy graphs without the device sync (events kept)
     python tools/graph_destroy_probe.py early_ev   # sync, but release the capture events before the graphs
-    python tools/graph_destroy_probe.py both       # neither (round 4's behaviour)
+    python tools/graph_destroy_probe.py both       # neither
+    python tools/graph_destroy_probe.py temp_events   # round 4's capture: the events recorded inside a capture
+                                                      # are not kept (released while the capture still runs)
 
 Each variant monkeypatches streaming.destroy_graphs and then runs tools/endless_seq.py's sequence (three
 models, every endless mode, runners replaced between them) in this process; a segfault ends the process.
@@ -38,8 +40,17 @@ def make(variant):
 
 def main():
     variant = sys.argv[1]
-    assert variant in ("nosync", "early_ev", "both")
-    streaming.destroy_graphs = make(variant)
+    assert variant in ("nosync", "early_ev", "both", "temp_events")
+    if variant == "temp_events":
+        import inspect
+        import textwrap
+        src = textwrap.dedent(inspect.getsource(streaming.EndlessGraphPipeline._run))
+        src = src.replace("keep.append(e)", "pass").replace("keep.extend(gp)", "pass")
+        ns = {}
+        exec(compile(src, streaming.__file__, "exec"), vars(streaming), ns)
+        streaming.EndlessGraphPipeline._run = ns["_run"]
+    else:
+        streaming.destroy_graphs = make(variant)
     import endless_seq
     sys.argv = [sys.argv[0], "m32,mb,m16,g32,gb,g16,g32,gb"]
     endless_seq.main()
