@@ -235,8 +235,17 @@ constexpr int KR_BYTES = RING * 128;            // K ring [384][64] bf16, 16-B c
 constexpr int P_BYTES_ = RING * 128;            // P rows [384][64] bf16, swizzled
 constexpr int VT_PITCH_B = (RING + 8) * 2;      // V^T [64 dims][384 (+8)] bf16
 constexpr int VT_BYTES_ = 64 * VT_PITCH_B;
-constexpr int SCR_PITCH = 49;                   // bf16 per query row of the skew scratch (48-wide band, 4k+1: rel_shift reshape)
-constexpr int SCR_BYTES = 16 * SCR_PITCH * 2;   // per wave
+#ifndef ATTN_SCR_PITCH
+#define ATTN_SCR_PITCH 49   // sheared skew writes: bf16 per query row (read pitch one less, a multiple of 4)
+#endif
+#ifndef ATTN_RD_PITCH
+#define ATTN_RD_PITCH 52    // ATTN_SKEW_RD: unsheared rows (a multiple of 4: aligned ds_write_b64; 52 = 4 mod 8:
+                            // the 16-lane write groups hit 32 distinct banks)
+#endif
+constexpr int SCR_PITCH = ATTN_SCR_PITCH;       // bf16 per query row of the skew scratch (48-wide band, 4k+1: rel_shift reshape)
+constexpr int RD_PITCH = ATTN_RD_PITCH;
+constexpr int SCR_ELEMS = 16 * SCR_PITCH > 16 * RD_PITCH + 8 ? 16 * SCR_PITCH : 16 * RD_PITCH + 8;
+constexpr int SCR_BYTES = (SCR_ELEMS * 2 + 15) / 16 * 16;   // per wave
 constexpr int RING_LDS = KR_BYTES + P_BYTES_ + VT_BYTES_ + 8 * SCR_BYTES + 512;
 }  // namespace
 
@@ -266,9 +275,65 @@ CFM_DEV void attn_static_prio(int half) {
   (void)half;
 }
 #ifndef ATTN_SKEW_RD
-#define ATTN_SKEW_RD 0   // ring kernel rel_shift: 1 = unsheared aligned ds_write_b64 rows and the shear on the read
-                         // side (ds_read2_b32 + ds_read_b32 + two v_alignbit per 4 values); 0 = sheared writes
+#define ATTN_SKEW_RD 1   // ring / dense kernels' rel_shift: 1 = unsheared aligned ds_write_b64 rows at pitch RD_PITCH
+                         // and the shear on the read side (ds_read2_b32 + ds_read_b32 + two v_alignbit per 4 values);
+                         // 0 = sheared ds_write_b16 writes at pitch SCR_PITCH, aligned ds_read_b64 reads
 #endif
+
+// rel_shift of one 32-key half (hh) of a 64-key tile through the wave's bf16 scratch (attention.py:242-266, the
+// reference's pad / reshape trick): b[0..2] = band^T subtiles 2hh .. 2hh+2 (P rows kb0 + 16(2hh+pt) + 4g + rr,
+// query fr); returns in bd[st2] the band of (query fr, keys j0 + 32hh + 16st2 + 4g .. +3) = band column
+// 16st2 + 4g + rr + 15 - fr.  Round 6: with ATTN_SKEW_RD the rows are written unsheared (one aligned
+// ds_write_b64 per subtile) and sheared on the read; the round-5 layout (sheared 2-B writes, pitch 49 / 48)
+// spent a quarter of the kernel's LDS cycles in 2-way bank conflicts (PMC SQ_LDS_BANK_CONFLICT 25% of
+// SQ_LDS_IDX_ACTIVE; a model of the banking: the b16 writes and the pitch-48 b64 reads are 2-way, pitch-52
+// b64 writes conflict-free, the read-side shear's dword reads 2-way): 112 -> 72 LDS cycles per wave and tile
+template <typename E>
+CFM_DEV void skew_half(unsigned scr_base, int fr, int g, const f32x4* b, E (&bd)[2][4]) {
+  typedef E ex4 __attribute__((ext_vector_type(4)));
+  ex4 v[2];
+#pragma unroll
+  for (int pt = 0; pt < 3; ++pt) {
+    const unsigned lo = pack_e2<E>(b[pt][0], b[pt][1]), hi = pack_e2<E>(b[pt][2], b[pt][3]);
+    if constexpr (ATTN_SKEW_RD) {
+      const unsigned waddr = scr_base + 2u * (unsigned)(fr * RD_PITCH + 16 * pt + 4 * g);
+      asm volatile("ds_write_b64 %0, %1" ::"v"(waddr), "v"((u32x2_a){lo, hi}) : "memory");
+    } else {
+      lds_store_4bf16_a2(scr_base + 2u * (unsigned)(fr * SCR_PITCH + 1 + 16 * pt + 4 * g), lo, hi);
+    }
+  }
+  if constexpr (ATTN_SKEW_RD) {
+    // the 4 values start at a 2-B aligned element: three dwords from the 4-B aligned address at or below it,
+    // funnel-shifted by 0 or 16 bits (tools/probe/skew_probe.hip)
+    u32x2_a d01[2];
+    unsigned d2[2], sh[2];
+#pragma unroll
+    for (int st2 = 0; st2 < 2; ++st2) {
+      const unsigned ra = scr_base + 2u * (unsigned)(fr * RD_PITCH + 15 - fr + 16 * st2 + 4 * g);
+      const unsigned al = ra & ~3u;
+      sh[st2] = (ra & 2u) << 3;
+      asm volatile("ds_read2_b32 %0, %1 offset0:0 offset1:1" : "=v"(d01[st2]) : "v"(al) : "memory");
+      asm volatile("ds_read_b32 %0, %1 offset:8" : "=v"(d2[st2]) : "v"(al) : "memory");
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(d01[0]), "+v"(d01[1]), "+v"(d2[0]), "+v"(d2[1])::"memory");
+#pragma unroll
+    for (int st2 = 0; st2 < 2; ++st2)
+      v[st2] = __builtin_bit_cast(ex4, (u32x2_a){__builtin_amdgcn_alignbit(d01[st2].y, d01[st2].x, sh[st2]),
+                                                 __builtin_amdgcn_alignbit(d2[st2], d01[st2].y, sh[st2])});
+  } else {
+#pragma unroll
+    for (int st2 = 0; st2 < 2; ++st2)
+      asm volatile("ds_read_b64 %0, %1"
+                   : "=v"(v[st2])
+                   : "v"(scr_base + 2u * (unsigned)(fr * (SCR_PITCH - 1) + 16 + 16 * st2 + 4 * g))
+                   : "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v[0]), "+v"(v[1])::"memory");
+  }
+#pragma unroll
+  for (int st2 = 0; st2 < 2; ++st2)
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) bd[st2][rr] = v[st2][rr];
+}
 #ifndef ATTN_STAGGER
 #define ATTN_STAGGER 0   // A/B: waves 4-7 store their output rows one pair late (see the ring kernel)
 #endif
@@ -530,55 +595,8 @@ __global__ __launch_bounds__(512, 1) void chunk_attention_ring_kernel(
           }
 #pragma unroll
           for (int hh = 0; hh < 2; ++hh) {
-#pragma unroll
-            for (int pt = 0; pt < 3; ++pt) {
-              const f32x4 a = band[2 * hh + pt];
-              // rel_shift by the reshape trick: row fr is written at pitch 49 (+1) and read back at
-              // pitch 48, so query fr's band for key jj starts 16 - fr elements later: the reads
-              // are aligned 8-B vectors (4 keys), the writes 2-B aligned, as four ds_write_b16
-              const unsigned lo = pack_e2<E>(a[0], a[1]), hi = pack_e2<E>(a[2], a[3]);
-              if constexpr (ATTN_SKEW_RD) {   // unsheared rows at pitch 48: one aligned ds_write_b64
-                const unsigned waddr = scr_base + 2u * (unsigned)(fr * (SCR_PITCH - 1) + 16 * pt + 4 * g);
-                asm volatile("ds_write_b64 %0, %1" ::"v"(waddr), "v"((u32x2_a){lo, hi}) : "memory");
-              } else {
-                const unsigned waddr = scr_base + 2u * (unsigned)(fr * SCR_PITCH + 1 + 16 * pt + 4 * g);
-                if (diag & 16)   // A/B: one unaligned ds_write_b64 (replayed by the LDS)
-                  asm volatile("ds_write_b64 %0, %1" ::"v"(waddr), "v"((u32x2_a){lo, hi}) : "memory");
-                else
-                  lds_store_4bf16_a2(waddr, lo, hi);
-              }
-            }
-            // band of (query fr, key j0+32hh+16st2+4g+rr) = scratch[fr][16st2 + 4g + rr + 15 - fr]
-            typedef E ex4 __attribute__((ext_vector_type(4)));
-            ex4 bdv4[2];
-            if constexpr (ATTN_SKEW_RD) {
-              // the shear on the read side: the 4 values start at a 2-B aligned element, so three dwords
-              // from the 4-B aligned address at or below it, funnel-shifted by 0 or 16 bits
-              // (tools/probe/skew_probe.hip)
-              u32x2_a d01[2];
-              unsigned d2[2], sh[2];
-#pragma unroll
-              for (int st2 = 0; st2 < 2; ++st2) {
-                const unsigned ra = scr_base + 2u * (unsigned)(fr * (SCR_PITCH - 1) + 15 - fr + 16 * st2 + 4 * g);
-                const unsigned al = ra & ~3u;
-                sh[st2] = (ra & 2u) << 3;
-                asm volatile("ds_read2_b32 %0, %1 offset0:0 offset1:1" : "=v"(d01[st2]) : "v"(al) : "memory");
-                asm volatile("ds_read_b32 %0, %1 offset:8" : "=v"(d2[st2]) : "v"(al) : "memory");
-              }
-              asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(d01[0]), "+v"(d01[1]), "+v"(d2[0]), "+v"(d2[1])::"memory");
-#pragma unroll
-              for (int st2 = 0; st2 < 2; ++st2)
-                bdv4[st2] = __builtin_bit_cast(ex4, (u32x2_a){__builtin_amdgcn_alignbit(d01[st2].y, d01[st2].x, sh[st2]),
-                                                             __builtin_amdgcn_alignbit(d2[st2], d01[st2].y, sh[st2])});
-            } else {
-#pragma unroll
-              for (int st2 = 0; st2 < 2; ++st2)
-                asm volatile("ds_read_b64 %0, %1"
-                             : "=v"(bdv4[st2])
-                             : "v"(scr_base + 2u * (unsigned)(fr * (SCR_PITCH - 1) + 16 + 16 * st2 + 4 * g))
-                             : "memory");
-              asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(bdv4[0]), "+v"(bdv4[1])::"memory");
-            }
+            E bdv4[2][4];
+            skew_half<E>(scr_base, fr, g, band + 2 * hh, bdv4);
             // S^T[key 16st + 4g + rr][query fr] = band + K.(q+u)
 #pragma unroll
             for (int st2 = 0; st2 < 2; ++st2) {
@@ -760,6 +778,7 @@ constexpr int FA_KV_BYTES = FA_VT_BYTES > FA_K_BYTES ? FA_VT_BYTES : FA_K_BYTES;
 constexpr int FA_P_BYTES = FA_PROWS * 128;
 constexpr int FA_LDS = FA_KV_BYTES + FA_P_BYTES + 8 * SCR_BYTES + 512;
 static_assert(FA_LDS <= 163840, "full-attention LDS");
+static_assert(RING_LDS <= 163840, "ring-attention LDS");
 }  // namespace
 
 __global__ __launch_bounds__(512, 1) void full_attention_bf16_kernel(
@@ -893,21 +912,8 @@ __global__ __launch_bounds__(512, 1) void full_attention_bf16_kernel(
         const bool tmask = t == NTV - 1 && j0 + 64 > key_hi;   // only the last valid tile can be partial
 #pragma unroll
         for (int hh = 0; hh < 2; ++hh) {
-#pragma unroll
-          for (int pt = 0; pt < 3; ++pt) {
-            const f32x4 a = band[2 * hh + pt];
-            const unsigned waddr = scr_base + 2u * (unsigned)(fr * SCR_PITCH + 1 + 16 * pt + 4 * g);
-            lds_store_4bf16_a2(waddr, pack_bf16x2_a(a[0], a[1]), pack_bf16x2_a(a[2], a[3]));
-          }
-          typedef bf16 bf16x4 __attribute__((ext_vector_type(4)));
-          bf16x4 bdv4[2];
-#pragma unroll
-          for (int st2 = 0; st2 < 2; ++st2)
-            asm volatile("ds_read_b64 %0, %1"
-                         : "=v"(bdv4[st2])
-                         : "v"(scr_base + 2u * (unsigned)(fr * (SCR_PITCH - 1) + 16 + 16 * st2 + 4 * g))
-                         : "memory");
-          asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(bdv4[0]), "+v"(bdv4[1])::"memory");
+          bf16 bdv4[2][4];
+          skew_half<bf16>(scr_base, fr, g, band + 2 * hh, bdv4);
 #pragma unroll
           for (int st2 = 0; st2 < 2; ++st2) {
             const int st = 2 * hh + st2;
