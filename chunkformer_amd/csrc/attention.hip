@@ -754,18 +754,19 @@ int chunk_attention_masked_f16(const f16* q, const f16* kv, int kv_rows, const f
 
 // =====================================================================================
 // Dense path (bf16, dk 64, full attention: forward_encoder with chunk_size -1, BASELINE configs[4];
-// any padded plan without left context): one 512-thread block = two consecutive 64-query
-// descriptors of one utterance x one head (8 waves, two per SIMD), with every key of the
-// utterance (T' <= 384) staged ONCE in LDS for all 8 waves instead of each wave reloading K and P
-// fragments from global memory per 64-key tile (chunk_attention_kernel):
-//   phase 1: K rows (swizzled) and the 64 NT + 127 relative-position rows the block's queries reach;
-//            V rows are loaded into registers at the same time;
+// any padded plan without left context): one 512-thread block = one utterance x one head (8 waves, two
+// per SIMD), every key of the utterance (T' <= 384) staged in LDS for all 8 waves instead of each wave
+// reloading K and P fragments from global memory per 64-key tile (chunk_attention_kernel).  Round 6: the
+// block runs the utterance's query pairs (two 64-query descriptors, one per half of the block) as passes
+// over ONE prologue -- the relative-position rows of every pass (64 NT + 127 + 128 per further pair) by
+// LDS-DMA, the K and V rows into registers, where they stay for all passes -- instead of one block (and
+// one HBM-bound prologue of 160 KB) per pair; per pass:
+//   K rows (swizzled) from the registers into the K / V^T region;
 //   scores:  the ring kernel's compute -- S^T = K.(q+u)^T, band^T = P.(q+v)^T skewed through a bf16
-//            scratch (pitch 49 write, 48 read), exact softmax with all <= 384 scores of a query in
-//            registers;
-//   phase 2: V^T is written over the dead K region, then O^T = V^T.P^T with the score registers as
+//            scratch (skew_half), exact softmax with all <= 384 scores of a query in registers;
+//   V^T from the registers over the dead K region, then O^T = V^T.P^T with the score registers as
 //            the B operand.
-// LDS: max(K 48 KiB, V^T 49 KiB) + P 64 KiB + 8 skew scratches = 126 KiB.
+// LDS: max(K 48 KiB, V^T 49 KiB) + P 96 KiB + 8 skew scratches = 159 KiB.
 // =====================================================================================
 namespace {
 constexpr int FA_KEYS = 384;                        // keys staged (T' <= 384: utterances <= 30.8 s)
@@ -775,7 +776,9 @@ constexpr int FA_K_BYTES = FA_KEYS * 128;
 constexpr int FA_VT_PITCH = (FA_KEYS + 8) * 2;
 constexpr int FA_VT_BYTES = 64 * FA_VT_PITCH;
 constexpr int FA_KV_BYTES = FA_VT_BYTES > FA_K_BYTES ? FA_VT_BYTES : FA_K_BYTES;
-constexpr int FA_P_BYTES = FA_PROWS * 128;
+constexpr int FA_MAXPAIR = (FA_NT + 1) / 2;                      // query pairs of a T' <= 384 utterance
+constexpr int FA_PROWS_ALL = FA_PROWS + 128 * (FA_MAXPAIR - 1);   // P rows of every pass (768)
+constexpr int FA_P_BYTES = FA_PROWS_ALL * 128;
 constexpr int FA_LDS = FA_KV_BYTES + FA_P_BYTES + 8 * SCR_BYTES + 512;
 static_assert(FA_LDS <= 163840, "full-attention LDS");
 static_assert(RING_LDS <= 163840, "ring-attention LDS");
@@ -796,28 +799,24 @@ __global__ __launch_bounds__(512, 1) void full_attention_bf16_kernel(
   const unsigned scr_base = (unsigned)(size_t)(__attribute__((address_space(3))) char*)scr;
   float* uv = reinterpret_cast<float*>(pl + FA_P_BYTES + 8 * SCR_BYTES);
   // XCD-aware order: the dispatcher deals consecutive workgroups round-robin to the 8 XCDs, so the
-  // hardware index is remapped (bijectively) to give each XCD a contiguous run of (head, utterance,
-  // query-pair) items: the query pairs of one utterance x head -- which stage the same K / V rows --
-  // and the utterances of one head -- the same P rows -- share that XCD's L2
-  const int npair = (nd + 1) >> 1, gx = gridDim.x;
-  const int T = gx * gridDim.y, b = blockIdx.y * gx + blockIdx.x, xcd = b & 7, q8 = T >> 3, r8 = T & 7;
+  // hardware index is remapped (bijectively) to give each XCD a contiguous run of (head, utterance)
+  // items: the utterances of one head -- which stage the same P rows -- share that XCD's L2
+  const int nutt = gridDim.x;
+  const int T = nutt * gridDim.y, b = blockIdx.y * nutt + blockIdx.x, xcd = b & 7, q8 = T >> 3, r8 = T & 7;
   const int item = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b >> 3);
-  const int h = item / gx, d = H * 64;
-  const int u = (item - h * gx) / npair, pr2 = (item - h * gx) % npair;
-  const int dix = u * nd + 2 * pr2 + half;
-  const bool has = 2 * pr2 + half < nd;
-  const int32_t* D0 = desc + (size_t)(u * nd + 2 * pr2) * AD_INTS;
-  const int32_t* D = desc + (size_t)(has ? dix : u * nd + 2 * pr2) * AD_INTS;
-  const int kv_row0 = D0[AD_KV_ROW0], key_hi = D0[AD_KEY_HI];   // shared by the pair (one utterance)
-  const int q_row0 = D[AD_Q_ROW0], nq = D[AD_NQ], p_base = D[AD_P_BASE], q_valid = D[AD_Q_VALID];
-  const int pb0 = D0[AD_P_BASE] - 127;   // P row of LDS row 0
+  const int h = item / nutt, u = item - h * nutt, d = H * 64;
+  const int npair = (nd + 1) >> 1;
+  const int32_t* Du = desc + (size_t)u * nd * AD_INTS;
+  const int kv_row0 = Du[AD_KV_ROW0], key_hi = Du[AD_KEY_HI];   // shared by the utterance's descriptors
+  // P_BASE of descriptor k is T' - 1 - 64 k (planner.cpp): the last pair's rows start lowest
+  const int pb0 = Du[(size_t)(2 * (npair - 1)) * AD_INTS + AD_P_BASE] - 127;   // P row of LDS row 0
 
-  // ---- phase 1: the P rows pb0 .. straight into LDS by LDS-DMA (wave w, instruction i fills rows
-  // 8 (8 i + w) .. +7 lane-linearly, the row's 16-B chunk swizzle applied on the source address; rows
-  // outside [0, p_rows) are clamped: they reach masked scores only), then every global load of the
-  // thread (K, and V for phase 2), then the K stores
-#pragma unroll
-  for (int i = 0; i < FA_PROWS / 64; ++i) {
+  // ---- prologue: the P rows pb0 .. of every pass straight into LDS by LDS-DMA (wave w, instruction i
+  // fills rows 8 (8 i + w) .. +7 lane-linearly, the row's 16-B chunk swizzle applied on the source
+  // address; rows outside [0, p_rows) are clamped: they reach masked scores only), then every global
+  // load of the thread (K and V, kept in registers for all passes)
+  const int p_iters = (FA_PROWS + 128 * (npair - 1)) / 64;
+  for (int i = 0; i < p_iters; ++i) {
     const int r = 8 * (8 * i + w) + (lane >> 3), ch = (lane & 7) ^ ((r >> 1) & 7);
     const int prow = min(max(pb0 + r, 0), p_rows - 1);
     __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(P + (size_t)prow * p_ld + h * 64 + ch * 8),
@@ -826,6 +825,7 @@ __global__ __launch_bounds__(512, 1) void full_attention_bf16_kernel(
   if (tid < 128) uv[tid] = (tid < 64 ? pos_u : pos_v)[h * 64 + (tid & 63)];
   constexpr int KIT = FA_KEYS * 8 / 512, VIT = (FA_KEYS / 2) * 8 / 512;
   static_assert(FA_KEYS * 8 % 512 == 0 && FA_PROWS % 64 == 0 && (FA_KEYS / 2) * 8 % 512 == 0, "staging");
+  static_assert(FA_LDS <= 163840, "full-attention LDS");
   u32x4 sk[KIT], sv0[VIT], sv1[VIT];
   const u32x4 z4 = (u32x4){0u, 0u, 0u, 0u};
 #pragma unroll
@@ -845,26 +845,32 @@ __global__ __launch_bounds__(512, 1) void full_attention_bf16_kernel(
                                                            h * 128 + ch * 8)
                         : z4;
   }
-#pragma unroll
-  for (int it = 0; it < KIT; ++it) {
-    const int idx = tid + 512 * it;
-    *reinterpret_cast<u32x4*>(kr + sw128(idx >> 3, idx & 7)) = sk[it];
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the P rows (LDS-DMA) have landed
-  __syncthreads();
 
   const int i0 = wq * 16;
   attn_static_prio(half);
-  const bool active = has && i0 < nq;
   // the block's key tiles (one utterance: uniform), as a compile-time count: the tile loops are
   // straight-line code without per-tile skip branches; only the last tile can need the key mask
   const int ntv = __builtin_amdgcn_readfirstlane((key_hi + 63) >> 6);
   auto body = [&](auto NTVc) {
     constexpr int NTV = decltype(NTVc)::value;
-    f32x4 S[NTV][4];
-    float l = 0.f;
     const int key8 = (fr >> 1) & 7;
     const int frag_lane[2] = {fr * 128 + ((g ^ key8) << 4), fr * 128 + (((4 + g) ^ key8) << 4)};
+    for (int pr2 = 0; pr2 < npair; ++pr2) {
+    const int dix = u * nd + 2 * pr2 + half;
+    const bool has = 2 * pr2 + half < nd;
+    const int32_t* D = desc + (size_t)(has ? dix : u * nd + 2 * pr2) * AD_INTS;
+    const int q_row0 = D[AD_Q_ROW0], nq = D[AD_NQ], p_base = D[AD_P_BASE], q_valid = D[AD_Q_VALID];
+    const bool active = has && i0 < nq;
+    // K rows into the K / V^T region (the previous pass's P.V reads of it are behind the pass-end barrier)
+#pragma unroll
+    for (int it = 0; it < KIT; ++it) {
+      const int idx = tid + 512 * it;
+      *reinterpret_cast<u32x4*>(kr + sw128(idx >> 3, idx & 7)) = sk[it];
+    }
+    if (pr2 == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the P rows (LDS-DMA) have landed
+    __syncthreads();
+    f32x4 S[NTV][4];
+    float l = 0.f;
     if (active) {
       bf16x8 qraw[2];
       {
@@ -960,7 +966,7 @@ __global__ __launch_bounds__(512, 1) void full_attention_bf16_kernel(
       for (int e = 0; e < 8; ++e) *reinterpret_cast<bf16x2_*>(vt + (ch * 8 + e) * FA_VT_PITCH + j * 2) = (bf16x2_){a[e], b[e]};
     }
     __syncthreads();
-    if (!active) return;
+    if (active) {
     const int vt_lane = fr * FA_VT_PITCH + 8 * g;
     f32x4 O[4];
 #pragma unroll
@@ -1004,14 +1010,17 @@ __global__ __launch_bounds__(512, 1) void full_attention_bf16_kernel(
       if (qi < nq) *reinterpret_cast<u32x4*>(op + 32 * pr + 16 * (g & 1) + 8 * (g >> 1)) = (u32x4){r0[0], r1[0], r0[1], r1[1]};
     }
 #else
-    if (qi >= nq) return;
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) {
       typedef bf16 bf16x4 __attribute__((ext_vector_type(4)));
-      *reinterpret_cast<bf16x4*>(op + 16 * nt + 4 * g) =
-          (bf16x4){(bf16)(O[nt][0] * inv), (bf16)(O[nt][1] * inv), (bf16)(O[nt][2] * inv), (bf16)(O[nt][3] * inv)};
+      if (qi < nq)
+        *reinterpret_cast<bf16x4*>(op + 16 * nt + 4 * g) =
+            (bf16x4){(bf16)(O[nt][0] * inv), (bf16)(O[nt][1] * inv), (bf16)(O[nt][2] * inv), (bf16)(O[nt][3] * inv)};
     }
 #endif
+    }   // active
+    __syncthreads();   // every wave is past its V^T reads before the next pass writes K there
+    }   // passes
   };
   switch (ntv) {
     case 0:   // (no key: tile 0 fully masked, output 0)
@@ -1032,7 +1041,8 @@ int full_attention_bf16(const bf16* q, const bf16* kv, int kv_rows, const bf16* 
   if (nutt <= 0 || nd <= 0) return 0;
   if (dk != 64 || t_keys > FA_KEYS || t_keys <= 0) return -1;
   if (p_ld <= 0) p_ld = H * 64;
-  hipLaunchKernelGGL(full_attention_bf16_kernel, dim3(nutt * ((nd + 1) / 2), H), dim3(512), 0, st, q, kv, kv_rows, P,
+  if ((nd + 1) / 2 > FA_MAXPAIR) return -1;
+  hipLaunchKernelGGL(full_attention_bf16_kernel, dim3(nutt, H), dim3(512), 0, st, q, kv, kv_rows, P,
                      p_rows, pos_u, pos_v, desc, H, nd, out, p_ld);
   CFM_CHECK_LAUNCH();
   return 0;
