@@ -261,7 +261,8 @@ CFM_DEV unsigned pack_e2(float a, float b) {
 }
 CFM_DEV int sw128(int row, int ch) { return row * 128 + ((ch ^ ((row >> 1) & 7)) << 4); }
 #ifndef RING_KPF
-#define RING_KPF 1   // ring kernel, interior chunks: next tile's K fragments read before this tile's skew
+#define RING_KPF 0   // ring kernel, interior chunks: next tile's K fragments read before this tile's skew (round 6,
+                     // with the conflict-free skew: off 4.22 vs on 4.30 ms/step, one-process A/B)
 #endif
 #ifndef ATTN_PRIO
 #define ATTN_PRIO 1   // static wave priority: 1 = the second-dispatched half (waves 4-7) at s_setprio 1 (ring attention
