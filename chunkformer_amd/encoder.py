@@ -36,6 +36,17 @@ def calc_length(T: int) -> int:
     return 1 + (int(T) - 15) // 8
 
 
+def reverse_calc_length(out_len: int) -> int:
+    """subsampling.py:290-311: the input length that subsamples to out_len (three kernel-3, stride-2
+    stages without padding: n -> 2 (n - 1) + 3 each, i.e. 8 (out_len - 1) + 15); 0 for out_len <= 0."""
+    if out_len <= 0:
+        return 0
+    n = int(out_len)
+    for _ in range(3):
+        n = (n - 1) * 2 + 3
+    return n
+
+
 class ChunkFormerEncoder:
     subsampling_rate = 8
     right_context = 14
@@ -369,6 +380,38 @@ class ChunkFormerEncoder:
                                           out.data_ptr(), ws.data_ptr(), ws_bytes, self._stream()))
         self._last_plan = (plan, plan_dev)
         return out, None, aco, cco
+
+    @torch.no_grad()
+    def forward_chunk_by_chunk(self, xs: torch.Tensor, xs_lens: torch.Tensor, chunk_size: int = 0,
+                               left_context_size: int = 0, right_context_size: int = 0):
+        """encoder.py:387-459: streaming decode of a padded batch xs [B, T, 80] through forward_chunk, the
+        caches carried: the input is padded so that (T - size) is a multiple of the stride (size =
+        reverse_calc_length(chunk_size) + 8 right_context_size input frames per step, stride 8 chunk_size),
+        every step keeps its first chunk_size rows but the last one keeps its whole output; returns
+        (out [B, T', d], masks [B, 1, T']) with the masks of calc_length(xs_lens + pad) like the reference."""
+        B = xs.size(0)
+        C, L, R = int(chunk_size), int(left_context_size), int(right_context_size)
+        nb, H, dk, d = self.num_blocks, self.cfg.n_heads, self.cfg.head_dim, self.cfg.d_model
+        size = reverse_calc_length(C) + R * self.subsampling_rate
+        stride = C * self.subsampling_rate
+        if stride <= 0:
+            raise ValueError("forward_chunk_by_chunk needs chunk_size > 0")
+        pad = stride - ((xs.size(1) - size) % stride)
+        xs = torch.nn.functional.pad(xs, (0, 0, 0, pad))
+        lens = torch.as_tensor(xs_lens) + pad
+        dev = self.device
+        att = torch.zeros(nb, B, H, L, 2 * dk, device=dev)
+        cnn = torch.zeros(nb, B, d, self.cfg.conv_lorder, device=dev)
+        outs, offset = [], 0
+        for i in range(0, xs.size(1) - size + stride, stride):
+            y, _, att, cnn = self.forward_chunk(xs[:, i: i + size, :], att, cnn, C, L, R, offset)
+            outs.append(y[:, :C, :] if i + size < xs.size(1) else y)
+            offset += C
+        out = torch.cat(outs, dim=1)
+        sub = torch.tensor([calc_length(int(t)) for t in lens.tolist()])
+        n = int(sub.max()) if sub.numel() else 0   # make_pad_mask's max_len (mask.py:203-226)
+        masks = (torch.arange(max(n, 0))[None, :] < sub[:, None]).unsqueeze(1).to(dev)
+        return out, masks
 
     def forward(self, xs, xs_lens, chunk_size: int = 0, left_context_size: int = -1, right_context_size: int = -1,
                 **kwargs):

@@ -389,3 +389,29 @@ def forward_chunk(sd, cfg, xs, att_cache, cnn_cache, C, L, R, offset):
 def ctc_log_softmax(sd, enc):
     """ctc.py:73-81."""
     return F.log_softmax(F.linear(enc, sd["ctc.ctc_lo.weight"], sd["ctc.ctc_lo.bias"]), dim=-1)
+
+
+@torch.no_grad()
+def forward_chunk_by_chunk(sd, cfg, xs, xs_lens, C, L, R):
+    """Restatement of ChunkFormerEncoder.forward_chunk_by_chunk (encoder.py:387-459): xs [B, T, 80] padded by
+    stride - ((T - size) % stride) zero frames (size = 8 (C - 1) + 15 + 8 R input frames per step, the
+    reverse of calc_length, subsampling.py:290-311; stride 8 C), then forward_chunk per step with the caches
+    carried and offset += C; every step keeps its first C rows but the last one its whole output.  Returns
+    (out [B, T', d], masks [B, 1, max calc_length(xs_lens + pad)])."""
+    B = xs.shape[0]
+    nb, H, dk, d = cfg.num_blocks, cfg.n_heads, cfg.head_dim, cfg.d_model
+    size = 8 * (C - 1) + 15 + 8 * R
+    stride = 8 * C
+    pad = stride - ((xs.shape[1] - size) % stride)
+    xs = torch.nn.functional.pad(xs.float(), (0, 0, 0, pad))
+    lens = [int(t) + pad for t in xs_lens]
+    att = torch.zeros(nb, B, H, L, 2 * dk)
+    cnn = torch.zeros(nb, B, d, 7)
+    outs, offset = [], 0
+    for i in range(0, xs.shape[1] - size + stride, stride):
+        y, att, cnn = forward_chunk(sd, cfg, xs[:, i: i + size], att, cnn, C, L, R, offset)
+        outs.append(y[:, :C] if i + size < xs.shape[1] else y)
+        offset += C
+    sub = torch.tensor([calc_length(t) for t in lens])
+    masks = (torch.arange(int(sub.max()))[None, :] < sub[:, None]).unsqueeze(1)
+    return torch.cat(outs, 1), masks

@@ -392,6 +392,25 @@ def gen_stream(path):
     np.savez_compressed(path, **out)
 
 
+def gen_chunk_by_chunk(path, cfg=SMALL, seed=1):
+    """forward_chunk_by_chunk (encoder.py:387-459): the reference's own streaming loop over forward_chunk
+    (input padded to the stride, caches carried, every chunk's first chunk_size rows kept but the last
+    one's whole output), batch of 2 utterances of different lengths, two geometries."""
+    enc, _, sd = build_reference(cfg, seed)
+    out = {"sd_digest": sd_digest(sd), "seed": np.array(seed)}
+    cases = [("a", [1003, 777], 16, 32, 16, 61), ("b", [640, 640], 8, 16, 8, 62)]
+    with torch.no_grad():
+        for tag, lens, C, L, R, fs in cases:
+            xs = feats(lens, fs)
+            xp = torch.zeros(len(lens), max(lens), 80)
+            for i, t in enumerate(xs):
+                xp[i, : t.shape[0]] = t
+            y, masks = enc.forward_chunk_by_chunk(xp, torch.tensor(lens), C, L, R)
+            out.update({f"{tag}_lens": np.array(lens, np.int32), f"{tag}_clr": np.array([C, L, R], np.int32),
+                        f"{tag}_feat_seed": np.array(fs), f"{tag}_out": y.numpy(), f"{tag}_mask": masks.numpy()})
+    np.savez_compressed(path, **out)
+
+
 def gen_endless_tbd(path, cfg=SMALL, seed=1):
     """The small endless input of small.npz decoded again with total_batch_duration 80 (2 segments
     instead of 7): the reference's output depends (slightly) on the segmentation, so the bench's
@@ -769,7 +788,7 @@ def gen_rnnt_memory(path, seed=3, n_steps=64, dir_seed=11):
 if __name__ == "__main__":
     which = sys.argv[1:] or ["masks", "small", "large", "large_4h", "large_endless", "large_full", "text", "stream",
                              "endless_tbd", "rnnt", "rows_neq", "small256", "rnnt_sparse", "rnnt_memory", "autocast", "endless_tail", "tiny_batch", "tiny_padded",
-                             "large_full_mixed"]
+                             "large_full_mixed", "chunk_by_chunk"]
     if "masks" in which:
         gen_masks(os.path.join(HERE, "masks.npz"))
     if "small" in which:
@@ -806,6 +825,8 @@ if __name__ == "__main__":
         gen_tiny_batch(os.path.join(HERE, "tiny_batch.npz"))
     if "tiny_padded" in which:
         gen_tiny_padded(os.path.join(HERE, "tiny_padded.npz"))
+    if "chunk_by_chunk" in which:
+        gen_chunk_by_chunk(os.path.join(HERE, "chunk_by_chunk.npz"))
     if "large_full_mixed" in which:
         gen_large_full_mixed(os.path.join(HERE, "large_full_mixed.npz"))
     print("ok", which)

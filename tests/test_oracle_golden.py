@@ -343,6 +343,23 @@ def test_oracle_forward_chunk_large_4h(golden_dir):
     np.testing.assert_allclose(cnn.numpy(), g["b_cnn"], atol=1e-4, rtol=0)
 
 
+@pytest.mark.parametrize("tag", ["a", "b"])
+def test_oracle_chunk_by_chunk(golden_dir, tag):
+    """forward_chunk_by_chunk (encoder.py:387-459): the oracle's loop over its forward_chunk against the
+    reference's own run (chunk_by_chunk.npz: padded batch of 2, two chunk / context geometries)."""
+    g = _load(golden_dir, "chunk_by_chunk.npz")
+    sd = synthetic_state_dict(SMALL, int(g["seed"]))
+    lens = g[f"{tag}_lens"].tolist()
+    C, L, R = (int(v) for v in g[f"{tag}_clr"])
+    xs = synthetic_features(lens, int(g[f"{tag}_feat_seed"]))
+    xp = torch.zeros(len(lens), max(lens), 80)
+    for i, t in enumerate(xs):
+        xp[i, : t.shape[0]] = t
+    y, masks = ref.forward_chunk_by_chunk(sd, SMALL, xp, lens, C, L, R)
+    np.testing.assert_array_equal(masks.numpy(), g[f"{tag}_mask"])
+    np.testing.assert_allclose(y.numpy(), g[f"{tag}_out"], atol=1e-4, rtol=0)
+
+
 def test_reference_endless_depends_on_segmentation(golden_dir):
     """Reference fixtures only: endless_decode of the same input at tbd 20 (small.npz, 7 segments)
     and tbd 80 (endless_tbd80.npz, 2 segments) agree closely but not exactly, so total_batch_duration
