@@ -288,16 +288,29 @@ CFM_DEV void attn_static_prio(int half) {
 // ds_write_b64 per subtile) and sheared on the read; the round-5 layout (sheared 2-B writes, pitch 49 / 48)
 // spent a quarter of the kernel's LDS cycles in 2-way bank conflicts (PMC SQ_LDS_BANK_CONFLICT 25% of
 // SQ_LDS_IDX_ACTIVE; a model of the banking: the b16 writes and the pitch-48 b64 reads are 2-way, pitch-52
-// b64 writes conflict-free, the read-side shear's dword reads 2-way): 112 -> 72 LDS cycles per wave and tile
+// b64 writes conflict-free, the read-side shear's dword reads 2-way): 112 -> 72 LDS cycles per wave and tile.
+// ATTN_SKEW_PERM: query row fr lives in row slot skew_slot(fr) of the pitch-52 scratch.  With rows in query
+// order the reads' first dwords (2 q(fr) + (15 - fr) / 2 for slot q(fr) in 8-B units) and those 2 banks on (g odd)
+// collide pairwise in the 32-lane groups; a permutation whose slots keep q mod 16 distinct (the writes stay
+// conflict-free) and make those 32 dwords distinct mod 32 removes the reads' conflicts: 72 -> 60 cycles per wave
+// and tile in the model (the permutation is one solution of that search; any slot order keeps the layout valid)
+#ifndef ATTN_SKEW_PERM
+#define ATTN_SKEW_PERM 1
+#endif
+CFM_DEV int skew_slot(int fr) {
+  if constexpr (ATTN_SKEW_PERM && ATTN_SKEW_RD) return (int)((0x9f35c268b17de4a0ull >> (4 * fr)) & 15u);
+  return fr;
+}
 template <typename E>
 CFM_DEV void skew_half(unsigned scr_base, int fr, int g, const f32x4* b, E (&bd)[2][4]) {
   typedef E ex4 __attribute__((ext_vector_type(4)));
   ex4 v[2];
+  const int srow = skew_slot(fr) * RD_PITCH;   // element offset of the lane's scratch row (ATTN_SKEW_RD)
 #pragma unroll
   for (int pt = 0; pt < 3; ++pt) {
     const unsigned lo = pack_e2<E>(b[pt][0], b[pt][1]), hi = pack_e2<E>(b[pt][2], b[pt][3]);
     if constexpr (ATTN_SKEW_RD) {
-      const unsigned waddr = scr_base + 2u * (unsigned)(fr * RD_PITCH + 16 * pt + 4 * g);
+      const unsigned waddr = scr_base + 2u * (unsigned)(srow + 16 * pt + 4 * g);
       asm volatile("ds_write_b64 %0, %1" ::"v"(waddr), "v"((u32x2_a){lo, hi}) : "memory");
     } else {
       lds_store_4bf16_a2(scr_base + 2u * (unsigned)(fr * SCR_PITCH + 1 + 16 * pt + 4 * g), lo, hi);
@@ -310,7 +323,7 @@ CFM_DEV void skew_half(unsigned scr_base, int fr, int g, const f32x4* b, E (&bd)
     unsigned d2[2], sh[2];
 #pragma unroll
     for (int st2 = 0; st2 < 2; ++st2) {
-      const unsigned ra = scr_base + 2u * (unsigned)(fr * RD_PITCH + 15 - fr + 16 * st2 + 4 * g);
+      const unsigned ra = scr_base + 2u * (unsigned)(srow + 15 - fr + 16 * st2 + 4 * g);
       const unsigned al = ra & ~3u;
       sh[st2] = (ra & 2u) << 3;
       asm volatile("ds_read2_b32 %0, %1 offset0:0 offset1:1" : "=v"(d01[st2]) : "v"(al) : "memory");
