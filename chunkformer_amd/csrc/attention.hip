@@ -348,6 +348,48 @@ CFM_DEV void skew_half(unsigned scr_base, int fr, int g, const f32x4* b, E (&bd)
 #pragma unroll
     for (int rr = 0; rr < 4; ++rr) bd[st2][rr] = v[st2][rr];
 }
+// ATTN_SKEW_OVL (ring kernel, ATTN_SKEW_RD): skew_half split in two, so the second half's round trip through
+// the scratch is in flight while the first half's score MFMAs run (the wait names their results, which pins
+// them between the reads' issue and the wait)
+#ifndef ATTN_SKEW_OVL
+#define ATTN_SKEW_OVL 2   // 0: skew_half per half; 1: half 1 in flight under half 0's score MFMAs (ring 4.35 -> 4.26 ms/step); 2: also band subtiles 3-4 under half 0's round trip (4.28 -> 4.22)
+#endif
+#ifndef ATTN_DENSE_OVL
+#define ATTN_DENSE_OVL 0   // the dense kernel's form: 2 = as the ring kernel (rocprof 312 -> 320 us per launch, slower; 4 half-tile K reads in flight)
+#endif
+struct SkewRd {
+  u32x2_a d01[2];
+  unsigned d2[2], sh[2];
+};
+template <typename E>
+CFM_DEV void skew_issue(unsigned scr_base, int fr, int g, const f32x4* b, SkewRd& r) {
+  const int srow = skew_slot(fr) * RD_PITCH;
+#pragma unroll
+  for (int pt = 0; pt < 3; ++pt) {
+    const unsigned lo = pack_e2<E>(b[pt][0], b[pt][1]), hi = pack_e2<E>(b[pt][2], b[pt][3]);
+    const unsigned waddr = scr_base + 2u * (unsigned)(srow + 16 * pt + 4 * g);
+    asm volatile("ds_write_b64 %0, %1" ::"v"(waddr), "v"((u32x2_a){lo, hi}) : "memory");
+  }
+#pragma unroll
+  for (int st2 = 0; st2 < 2; ++st2) {
+    const unsigned ra = scr_base + 2u * (unsigned)(srow + 15 - fr + 16 * st2 + 4 * g);
+    const unsigned al = ra & ~3u;
+    r.sh[st2] = (ra & 2u) << 3;
+    asm volatile("ds_read2_b32 %0, %1 offset0:0 offset1:1" : "=v"(r.d01[st2]) : "v"(al) : "memory");
+    asm volatile("ds_read_b32 %0, %1 offset:8" : "=v"(r.d2[st2]) : "v"(al) : "memory");
+  }
+}
+template <typename E>
+CFM_DEV void skew_finish(const SkewRd& r, E (&bd)[2][4]) {
+  typedef E ex4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+  for (int st2 = 0; st2 < 2; ++st2) {
+    const ex4 v = __builtin_bit_cast(ex4, (u32x2_a){__builtin_amdgcn_alignbit(r.d01[st2].y, r.d01[st2].x, r.sh[st2]),
+                                                   __builtin_amdgcn_alignbit(r.d2[st2], r.d01[st2].y, r.sh[st2])});
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) bd[st2][rr] = v[rr];
+  }
+}
 #ifndef ATTN_STAGGER
 #define ATTN_STAGGER 0   // A/B: waves 4-7 store their output rows one pair late (see the ring kernel)
 #endif
@@ -592,8 +634,10 @@ __global__ __launch_bounds__(512, 1) void chunk_attention_ring_kernel(
           // band^T[P row kb0 + 16pt + 4g + rr][query fr], pt = 0..4 (80 rows for 64 keys + 15 skew); the
           // two 32-key halves use subtiles 0-2 and 2-4 -> scratch[query][band pos] (16 x 48 E per wave)
           f32x4 band[5];
+          // ATTN_SKEW_OVL 2: subtiles 3-4 (half 1 only) are computed while half 0's round trip is in flight
+          constexpr bool BAND_SPLIT = ATTN_SKEW_OVL >= 2 && ATTN_SKEW_RD;
 #pragma unroll
-          for (int pt = 0; pt < 5; ++pt) {
+          for (int pt = 0; pt < (BAND_SPLIT ? 3 : 5); ++pt) {
             if (pt == 0 && carry) {
               band[0] = band_next;
               continue;
@@ -603,10 +647,46 @@ __global__ __launch_bounds__(512, 1) void chunk_attention_ring_kernel(
             for (int s = 0; s < 2; ++s) a = mma16(pf[pt][s], qv[s], a);
             band[pt] = a;
           }
-          band_next = band[4];
+          if constexpr (!BAND_SPLIT) band_next = band[4];
           if constexpr (KPF) {
             if (t + 1 < NTT) load_kf(t + 1, kf_next);
           }
+          if constexpr (ATTN_SKEW_OVL && ATTN_SKEW_RD) {
+            SkewRd r0, r1;
+            skew_issue<E>(scr_base, fr, g, band, r0);
+            if constexpr (BAND_SPLIT) {
+              asm volatile("" : "+v"(qv[0]), "+v"(qv[1]));   // the MFMAs below read qv after the issue
+#pragma unroll
+              for (int pt = 3; pt < 5; ++pt) {
+                f32x4 a = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int s = 0; s < 2; ++s) a = mma16(pf[pt][s], qv[s], a);
+                band[pt] = a;
+              }
+              band_next = band[4];
+              asm volatile("s_waitcnt lgkmcnt(0)"
+                           : "+v"(r0.d01[0]), "+v"(r0.d01[1]), "+v"(r0.d2[0]), "+v"(r0.d2[1]), "+v"(band[3]), "+v"(band[4])::"memory");
+            } else {
+              asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(r0.d01[0]), "+v"(r0.d01[1]), "+v"(r0.d2[0]), "+v"(r0.d2[1])::"memory");
+            }
+            E bd0[2][4], bd1[2][4];
+            skew_finish<E>(r0, bd0);
+            skew_issue<E>(scr_base, fr, g, band + 2, r1);   // the half-0 reads are complete: the rows may be reused
+            auto scores = [&](int hh, const E (&bdv)[2][4]) {
+#pragma unroll
+              for (int st2 = 0; st2 < 2; ++st2) {
+                f32x4 a = (f32x4){(float)bdv[st2][0], (float)bdv[st2][1], (float)bdv[st2][2], (float)bdv[st2][3]};
+#pragma unroll
+                for (int s = 0; s < 2; ++s) a = mma16(kf[2 * hh + st2][s], qu[s], a);
+                S[t][2 * hh + st2] = a;
+              }
+            };
+            scores(0, bd0);
+            asm volatile("s_waitcnt lgkmcnt(0)"
+                         : "+v"(r1.d01[0]), "+v"(r1.d01[1]), "+v"(r1.d2[0]), "+v"(r1.d2[1]), "+v"(S[t][0]), "+v"(S[t][1])::"memory");
+            skew_finish<E>(r1, bd1);
+            scores(1, bd1);
+          } else
 #pragma unroll
           for (int hh = 0; hh < 2; ++hh) {
             E bdv4[2][4];
@@ -915,39 +995,79 @@ __global__ __launch_bounds__(512, 1) void full_attention_bf16_kernel(
         const int j0 = 64 * t;
         // the band first; its skewed values are the C operand of the score MFMAs (no VALU add)
         f32x4 band[5];
-#pragma unroll
-        for (int pt = 0; pt < 5; ++pt) {
-          if (pt == 0 && t > 0) {   // subtile 0 of this tile is subtile 4 of the previous one
-            band[0] = band_next;
-            continue;
-          }
+        const bool tmask = t == NTV - 1 && j0 + 64 > key_hi;   // only the last valid tile can be partial
+        auto band_pt = [&](int pt) {
           f32x4 a = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
           for (int s = 0; s < 2; ++s)
             a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
                 *reinterpret_cast<const bf16x8*>(pl + (lbase + j0 + 16 * pt) * 128 + frag_lane[s]), qv[s], a, 0, 0, 0);
           band[pt] = a;
-        }
-        band_next = band[4];
-        const bool tmask = t == NTV - 1 && j0 + 64 > key_hi;   // only the last valid tile can be partial
+        };
+        // S^T[key 16st + 4g + rr][query fr] = band + K.(q+u), masked past key_hi
+        auto score_st = [&](int st, const bf16 (&bdv)[4], const bf16x8 (&kf)[2]) {
+          f32x4 a = (f32x4){(float)bdv[0], (float)bdv[1], (float)bdv[2], (float)bdv[3]};
 #pragma unroll
-        for (int hh = 0; hh < 2; ++hh) {
-          bf16 bdv4[2][4];
-          skew_half<bf16>(scr_base, fr, g, band + 2 * hh, bdv4);
+          for (int s = 0; s < 2; ++s) a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[s], qu[s], a, 0, 0, 0);
 #pragma unroll
-          for (int st2 = 0; st2 < 2; ++st2) {
-            const int st = 2 * hh + st2;
-            f32x4 a = (f32x4){(float)bdv4[st2][0], (float)bdv4[st2][1], (float)bdv4[st2][2], (float)bdv4[st2][3]};
+          for (int rr = 0; rr < 4; ++rr) {
+            float sv = a[rr];
+            if (tmask && j0 + 16 * st + 4 * g + rr >= key_hi) sv = -INFINITY;
+            S[t][st][rr] = sv;
+            mx = fmaxf(mx, sv);
+          }
+        };
+        auto kfrag = [&](int st, bf16x8 (&kf)[2]) {
 #pragma unroll
-            for (int s = 0; s < 2; ++s)
-              a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                  *reinterpret_cast<const bf16x8*>(kr + (j0 + 16 * st) * 128 + frag_lane[s]), qu[s], a, 0, 0, 0);
+          for (int s = 0; s < 2; ++s) kf[s] = *reinterpret_cast<const bf16x8*>(kr + (j0 + 16 * st) * 128 + frag_lane[s]);
+        };
+        if constexpr (ATTN_DENSE_OVL >= 2 && ATTN_SKEW_RD) {
+          // as the ring kernel: band subtiles 3-4 under half 0's scratch round trip, half 1's round trip under
+          // half 0's score MFMAs (K fragments read before the first scratch access)
+          bf16x8 kf[4][2];   // half 1's fragments are read behind half 1's scratch accesses (registers)
 #pragma unroll
-            for (int rr = 0; rr < 4; ++rr) {
-              float sv = a[rr];
-              if (tmask && j0 + 32 * hh + 16 * st2 + 4 * g + rr >= key_hi) sv = -INFINITY;
-              S[t][st][rr] = sv;
-              mx = fmaxf(mx, sv);
+          for (int st = 0; st < 2; ++st) kfrag(st, kf[st]);
+#pragma unroll
+          for (int pt = 0; pt < 3; ++pt) {
+            if (pt == 0 && t > 0) band[0] = band_next;   // subtile 0 of this tile is subtile 4 of the previous one
+            else band_pt(pt);
+          }
+          SkewRd r0, r1;
+          skew_issue<bf16>(scr_base, fr, g, band, r0);
+          asm volatile("" : "+v"(qv[0]), "+v"(qv[1]));
+          band_pt(3);
+          band_pt(4);
+          band_next = band[4];
+          asm volatile("s_waitcnt lgkmcnt(0)"
+                       : "+v"(r0.d01[0]), "+v"(r0.d01[1]), "+v"(r0.d2[0]), "+v"(r0.d2[1]), "+v"(band[3]), "+v"(band[4])::"memory");
+          bf16 bd0[2][4], bd1[2][4];
+          skew_finish<bf16>(r0, bd0);
+          skew_issue<bf16>(scr_base, fr, g, band + 2, r1);
+          kfrag(2, kf[2]);
+          kfrag(3, kf[3]);
+          score_st(0, bd0[0], kf[0]);
+          score_st(1, bd0[1], kf[1]);
+          asm volatile("s_waitcnt lgkmcnt(0)"
+                       : "+v"(r1.d01[0]), "+v"(r1.d01[1]), "+v"(r1.d2[0]), "+v"(r1.d2[1]), "+v"(S[t][0]), "+v"(S[t][1])::"memory");
+          skew_finish<bf16>(r1, bd1);
+          score_st(2, bd1[0], kf[2]);
+          score_st(3, bd1[1], kf[3]);
+        } else {
+#pragma unroll
+          for (int pt = 0; pt < 5; ++pt) {
+            if (pt == 0 && t > 0) band[0] = band_next;   // subtile 0 of this tile is subtile 4 of the previous one
+            else band_pt(pt);
+          }
+          band_next = band[4];
+#pragma unroll
+          for (int hh = 0; hh < 2; ++hh) {
+            bf16 bdv4[2][4];
+            skew_half<bf16>(scr_base, fr, g, band + 2 * hh, bdv4);
+#pragma unroll
+            for (int st2 = 0; st2 < 2; ++st2) {
+              bf16x8 kf[2];
+              kfrag(2 * hh + st2, kf);
+              score_st(2 * hh + st2, bdv4[st2], kf);
             }
           }
         }
