@@ -354,6 +354,9 @@ CFM_DEV void skew_half(unsigned scr_base, int fr, int g, const f32x4* b, E (&bd)
 #ifndef ATTN_SKEW_OVL
 #define ATTN_SKEW_OVL 2   // 0: skew_half per half; 1: half 1 in flight under half 0's score MFMAs (ring 4.35 -> 4.26 ms/step); 2: also band subtiles 3-4 under half 0's round trip (4.28 -> 4.22)
 #endif
+#ifndef ATTN_SKEW_PERMC
+#define ATTN_SKEW_PERMC 1   // ring kernel, bf16: skew_finish_c (v_perm_b32 into the f32 C operand)
+#endif
 #ifndef ATTN_DENSE_OVL
 #define ATTN_DENSE_OVL 0   // the dense kernel's form: 2 = as the ring kernel (rocprof 312 -> 320 us per launch, slower; 4 half-tile K reads in flight)
 #endif
@@ -377,6 +380,21 @@ CFM_DEV void skew_issue(unsigned scr_base, int fr, int g, const f32x4* b, SkewRd
     r.sh[st2] = (ra & 2u) << 3;
     asm volatile("ds_read2_b32 %0, %1 offset0:0 offset1:1" : "=v"(r.d01[st2]) : "v"(al) : "memory");
     asm volatile("ds_read_b32 %0, %1 offset:8" : "=v"(r.d2[st2]) : "v"(al) : "memory");
+  }
+}
+// bf16: the values straight into the f32 C operand -- v_perm_b32 puts an element's two bytes in the high half and
+// zeros below (one VALU op per value instead of the funnel shift plus the bf16 -> f32 shift / mask); the byte
+// offset sh / 8 is a lane constant (the parity of 15 - fr), so are the selectors
+CFM_DEV void skew_finish_c(const SkewRd& r, f32x4 (&c)[2]) {
+  const unsigned o = r.sh[0] >> 3;
+  const unsigned s0 = 0x0c0cu | (o << 16) | ((o + 1) << 24);
+  const unsigned s1 = s0 + 0x02020000u, s2 = s0 + 0x04040000u;
+#pragma unroll
+  for (int st2 = 0; st2 < 2; ++st2) {
+    c[st2][0] = __builtin_bit_cast(float, __builtin_amdgcn_perm(r.d01[st2].y, r.d01[st2].x, s0));
+    c[st2][1] = __builtin_bit_cast(float, __builtin_amdgcn_perm(r.d01[st2].y, r.d01[st2].x, s1));
+    c[st2][2] = __builtin_bit_cast(float, __builtin_amdgcn_perm(r.d01[st2].y, r.d01[st2].x, s2));
+    c[st2][3] = __builtin_bit_cast(float, __builtin_amdgcn_perm(r.d2[st2], r.d01[st2].y, s1));
   }
 }
 template <typename E>
@@ -669,23 +687,35 @@ __global__ __launch_bounds__(512, 1) void chunk_attention_ring_kernel(
             } else {
               asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(r0.d01[0]), "+v"(r0.d01[1]), "+v"(r0.d2[0]), "+v"(r0.d2[1])::"memory");
             }
-            E bd0[2][4], bd1[2][4];
-            skew_finish<E>(r0, bd0);
-            skew_issue<E>(scr_base, fr, g, band + 2, r1);   // the half-0 reads are complete: the rows may be reused
-            auto scores = [&](int hh, const E (&bdv)[2][4]) {
+            // the band as the f32 C operand of half hh's score MFMAs
+            auto finish = [&](const SkewRd& r, f32x4 (&c)[2]) {
+              if constexpr (ATTN_SKEW_PERMC && std::is_same<E, bf16>::value) {
+                skew_finish_c(r, c);
+              } else {
+                E bdv[2][4];
+                skew_finish<E>(r, bdv);
+#pragma unroll
+                for (int st2 = 0; st2 < 2; ++st2)
+                  c[st2] = (f32x4){(float)bdv[st2][0], (float)bdv[st2][1], (float)bdv[st2][2], (float)bdv[st2][3]};
+              }
+            };
+            auto scores = [&](int hh, const f32x4 (&c)[2]) {
 #pragma unroll
               for (int st2 = 0; st2 < 2; ++st2) {
-                f32x4 a = (f32x4){(float)bdv[st2][0], (float)bdv[st2][1], (float)bdv[st2][2], (float)bdv[st2][3]};
+                f32x4 a = c[st2];
 #pragma unroll
                 for (int s = 0; s < 2; ++s) a = mma16(kf[2 * hh + st2][s], qu[s], a);
                 S[t][2 * hh + st2] = a;
               }
             };
-            scores(0, bd0);
+            f32x4 c0[2], c1[2];
+            finish(r0, c0);
+            skew_issue<E>(scr_base, fr, g, band + 2, r1);   // the half-0 reads are complete: the rows may be reused
+            scores(0, c0);
             asm volatile("s_waitcnt lgkmcnt(0)"
                          : "+v"(r1.d01[0]), "+v"(r1.d01[1]), "+v"(r1.d2[0]), "+v"(r1.d2[1]), "+v"(S[t][0]), "+v"(S[t][1])::"memory");
-            skew_finish<E>(r1, bd1);
-            scores(1, bd1);
+            finish(r1, c1);
+            scores(1, c1);
           } else
 #pragma unroll
           for (int hh = 0; hh < 2; ++hh) {
