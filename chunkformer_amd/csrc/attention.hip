@@ -355,10 +355,7 @@ CFM_DEV void skew_half(unsigned scr_base, int fr, int g, const f32x4* b, E (&bd)
 #define ATTN_SKEW_OVL 2   // 0: skew_half per half; 1: half 1 in flight under half 0's score MFMAs (ring 4.35 -> 4.26 ms/step); 2: also band subtiles 3-4 under half 0's round trip (4.28 -> 4.22)
 #endif
 #ifndef ATTN_SKEW_PERMC
-#define ATTN_SKEW_PERMC 1   // ring kernel, bf16: skew_finish_c (v_perm_b32 into the f32 C operand)
-#endif
-#ifndef ATTN_DENSE_OVL
-#define ATTN_DENSE_OVL 0   // the dense kernel's form: 2 = as the ring kernel (rocprof 312 -> 320 us per launch, slower; 4 half-tile K reads in flight)
+#define ATTN_SKEW_PERMC 1   // ring (bf16) and dense kernels: skew_finish_c (v_perm_b32 into the f32 C operand)
 #endif
 struct SkewRd {
   u32x2_a d01[2];
@@ -1036,8 +1033,8 @@ __global__ __launch_bounds__(512, 1) void full_attention_bf16_kernel(
           band[pt] = a;
         };
         // S^T[key 16st + 4g + rr][query fr] = band + K.(q+u), masked past key_hi
-        auto score_st = [&](int st, const bf16 (&bdv)[4], const bf16x8 (&kf)[2]) {
-          f32x4 a = (f32x4){(float)bdv[0], (float)bdv[1], (float)bdv[2], (float)bdv[3]};
+        auto score_st = [&](int st, const f32x4& c, const bf16x8 (&kf)[2]) {
+          f32x4 a = c;
 #pragma unroll
           for (int s = 0; s < 2; ++s) a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[s], qu[s], a, 0, 0, 0);
 #pragma unroll
@@ -1052,54 +1049,32 @@ __global__ __launch_bounds__(512, 1) void full_attention_bf16_kernel(
 #pragma unroll
           for (int s = 0; s < 2; ++s) kf[s] = *reinterpret_cast<const bf16x8*>(kr + (j0 + 16 * st) * 128 + frag_lane[s]);
         };
-        if constexpr (ATTN_DENSE_OVL >= 2 && ATTN_SKEW_RD) {
-          // as the ring kernel: band subtiles 3-4 under half 0's scratch round trip, half 1's round trip under
-          // half 0's score MFMAs (K fragments read before the first scratch access)
-          bf16x8 kf[4][2];   // half 1's fragments are read behind half 1's scratch accesses (registers)
 #pragma unroll
-          for (int st = 0; st < 2; ++st) kfrag(st, kf[st]);
+        for (int pt = 0; pt < 5; ++pt) {
+          if (pt == 0 && t > 0) band[0] = band_next;   // subtile 0 of this tile is subtile 4 of the previous one
+          else band_pt(pt);
+        }
+        band_next = band[4];
 #pragma unroll
-          for (int pt = 0; pt < 3; ++pt) {
-            if (pt == 0 && t > 0) band[0] = band_next;   // subtile 0 of this tile is subtile 4 of the previous one
-            else band_pt(pt);
-          }
-          SkewRd r0, r1;
-          skew_issue<bf16>(scr_base, fr, g, band, r0);
-          asm volatile("" : "+v"(qv[0]), "+v"(qv[1]));
-          band_pt(3);
-          band_pt(4);
-          band_next = band[4];
-          asm volatile("s_waitcnt lgkmcnt(0)"
-                       : "+v"(r0.d01[0]), "+v"(r0.d01[1]), "+v"(r0.d2[0]), "+v"(r0.d2[1]), "+v"(band[3]), "+v"(band[4])::"memory");
-          bf16 bd0[2][4], bd1[2][4];
-          skew_finish<bf16>(r0, bd0);
-          skew_issue<bf16>(scr_base, fr, g, band + 2, r1);
-          kfrag(2, kf[2]);
-          kfrag(3, kf[3]);
-          score_st(0, bd0[0], kf[0]);
-          score_st(1, bd0[1], kf[1]);
-          asm volatile("s_waitcnt lgkmcnt(0)"
-                       : "+v"(r1.d01[0]), "+v"(r1.d01[1]), "+v"(r1.d2[0]), "+v"(r1.d2[1]), "+v"(S[t][0]), "+v"(S[t][1])::"memory");
-          skew_finish<bf16>(r1, bd1);
-          score_st(2, bd1[0], kf[2]);
-          score_st(3, bd1[1], kf[3]);
-        } else {
-#pragma unroll
-          for (int pt = 0; pt < 5; ++pt) {
-            if (pt == 0 && t > 0) band[0] = band_next;   // subtile 0 of this tile is subtile 4 of the previous one
-            else band_pt(pt);
-          }
-          band_next = band[4];
-#pragma unroll
-          for (int hh = 0; hh < 2; ++hh) {
+        for (int hh = 0; hh < 2; ++hh) {
+          f32x4 c[2];
+          if constexpr (ATTN_SKEW_PERMC && ATTN_SKEW_RD) {   // the band straight into the C operand (v_perm_b32)
+            SkewRd r;
+            skew_issue<bf16>(scr_base, fr, g, band + 2 * hh, r);
+            asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(r.d01[0]), "+v"(r.d01[1]), "+v"(r.d2[0]), "+v"(r.d2[1])::"memory");
+            skew_finish_c(r, c);
+          } else {
             bf16 bdv4[2][4];
             skew_half<bf16>(scr_base, fr, g, band + 2 * hh, bdv4);
 #pragma unroll
-            for (int st2 = 0; st2 < 2; ++st2) {
-              bf16x8 kf[2];
-              kfrag(2 * hh + st2, kf);
-              score_st(2 * hh + st2, bdv4[st2], kf);
-            }
+            for (int st2 = 0; st2 < 2; ++st2)
+              c[st2] = (f32x4){(float)bdv4[st2][0], (float)bdv4[st2][1], (float)bdv4[st2][2], (float)bdv4[st2][3]};
+          }
+#pragma unroll
+          for (int st2 = 0; st2 < 2; ++st2) {
+            bf16x8 kf[2];
+            kfrag(2 * hh + st2, kf);
+            score_st(2 * hh + st2, c[st2], kf);
           }
         }
       }
