@@ -72,6 +72,11 @@ template <int EPI> constexpr int wst_depth() { return wst_nslot<EPI>() - wst_bar
 #ifndef DW2_UNPK_SCALAR
 #define DW2_UNPK_SCALAR 0
 #endif
+#ifndef DW2_OFFTAB
+#define DW2_OFFTAB 1  // the rank table also holds each output's element offset (computed once, where `last` is decided:
+                      // no integer division per pass)
+#endif
+constexpr int DW2_TABW = DW2_OFFTAB ? 512 : 256;   // rank table bytes per wave
 #ifndef DW2_DEFER
 #define DW2_DEFER 0  // dw2 outputs staged in LDS and stored at the start of the next phase (A/B)
 #endif
@@ -206,7 +211,7 @@ __global__ __launch_bounds__(256, 1) void gemm_wsp_kernel(const bf16* __restrict
   // + per wave a 16-row x 64-column bf16 output staging tile (144-B rows) for full-row stores
   constexpr int STG_PITCH = 144, STG_BYTES = 16 * STG_PITCH;
   constexpr int NS = wst_nslot<EPI>(), DP = wst_depth<EPI>();
-  constexpr int TAIL = EPI == EPI_DW2 ? DW2_RING + DW2_WB + 4 * 256 + (DW2_DEFER ? 4 * DW2_STG : 0) : 4 * STG_BYTES;
+  constexpr int TAIL = EPI == EPI_DW2 ? DW2_RING + DW2_WB + 4 * DW2_TABW + (DW2_DEFER ? 4 * DW2_STG : 0) : 4 * STG_BYTES;
   __shared__ __attribute__((aligned(16))) char smem[NS * WST_SLOT + 1024 + TAIL];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -614,7 +619,7 @@ __global__ __launch_bounds__(256, 1) void gemm_wsp_kernel(const bf16* __restrict
   // (position k of 8 in flight, 8 channels); the same f32 taps and FMA order as fe_dw2_kernel.
   // DW2_DEFER: the previous phase's outputs (npend passes) leave from the LDS staging area here, so
   // their store acknowledgements overlap this phase's arithmetic instead of the next DMA waits
-  const unsigned dstg = dww + DW2_WB + 4 * 256 + (unsigned)wv * DW2_STG;
+  const unsigned dstg = dww + DW2_WB + 4 * DW2_TABW + (unsigned)wv * DW2_STG;
   int npend = 0;
   auto dw2_flush = [&]() {
     if constexpr (EPI == EPI_DW2 && DW2_DEFER) {
@@ -641,16 +646,23 @@ __global__ __launch_bounds__(256, 1) void gemm_wsp_kernel(const bf16* __restrict
       const int wrows = ep.t2n * 19;
       const int R = rtp * WST_MT + lane;
       bool last = false;
+      unsigned ooff = 0;   // DW2_OFFTAB: the output's element offset (without the lane's channels)
       if (R < M) {
         const int w_ = R / wrows, rem = R - w_ * wrows, t2 = rem / 19, f2 = rem - t2 * 19;
         last = t2 >= 2 && !(t2 & 1) && f2 >= 2 && !(f2 & 1);
+        ooff = (unsigned)(((w_ * ep.t3n + ((t2 - 2) >> 1)) * 9 + ((f2 - 2) >> 1)) * ep.ldo + ct * 256);
       }
       const unsigned long long mask = __builtin_amdgcn_ballot_w64(last);
       const int n = __builtin_popcountll(mask);
-      const unsigned tab = dww + DW2_WB + (unsigned)wv * 256;
+      const unsigned tab = dww + DW2_WB + (unsigned)wv * DW2_TABW;
       if (last) {
         const int rank = __builtin_amdgcn_mbcnt_hi((unsigned)(mask >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)mask, 0u));
-        asm volatile("ds_write_b32 %0, %1" ::"v"(tab + 4u * rank), "v"(lane) : "memory");
+        if constexpr (DW2_OFFTAB) {
+          typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
+          asm volatile("ds_write_b64 %0, %1" ::"v"(tab + 8u * rank), "v"((u32x2_t){(unsigned)lane, ooff}) : "memory");
+        } else {
+          asm volatile("ds_write_b32 %0, %1" ::"v"(tab + 4u * rank), "v"(lane) : "memory");
+        }
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       const int cl = wv * 64 + 8 * (lane & 7);   // the lane's 8 channels within the block's 256
@@ -666,8 +678,20 @@ __global__ __launch_bounds__(256, 1) void gemm_wsp_kernel(const bf16* __restrict
           asm volatile("ds_write_b32 %0, %1 offset:1024" ::"v"(dstg + (unsigned)(base >> 3) * 1280 + 4u * lane), "v"(0xffffffffu) : "memory");
         if (k0 >= n) continue;
         int Rl[P];
+        unsigned Ol = 0;   // DW2_OFFTAB, P == 1: the output offset from the table
         f32x4 b0, b1;
-        if constexpr (DW2_PIPE >= 2 && P == 1) {
+        if constexpr (DW2_PIPE >= 2 && P == 1 && DW2_OFFTAB) {
+          // the rank, the output offset and the bias seeds in one LDS round trip
+          typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
+          const unsigned bl = dww + 4u * (unsigned)(9 * 256 + cl);
+          u32x2_t ro;
+          asm volatile("ds_read_b64 %0, %1" : "=v"(ro) : "v"(tab + 8u * min(k0, n - 1)) : "memory");
+          asm volatile("ds_read_b128 %0, %1" : "=v"(b0) : "v"(bl) : "memory");
+          asm volatile("ds_read_b128 %0, %1 offset:16" : "=v"(b1) : "v"(bl) : "memory");
+          asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(ro), "+v"(b0), "+v"(b1)::"memory");
+          Rl[0] = (int)ro[0];
+          Ol = ro[1];
+        } else if constexpr (DW2_PIPE >= 2 && P == 1) {
           // the rank and the bias seeds in one LDS round trip
           const unsigned bl = dww + 4u * (unsigned)(9 * 256 + cl);
           asm volatile("ds_read_b32 %0, %1" : "=v"(Rl[0]) : "v"(tab + 4u * min(k0, n - 1)) : "memory");
@@ -679,7 +703,7 @@ __global__ __launch_bounds__(256, 1) void gemm_wsp_kernel(const bf16* __restrict
           for (int u = 0; u < P; ++u) {
             const int ku = min(k0 + 8 * u, n - 1);
             int rr;
-            asm volatile("ds_read_b32 %0, %1" : "=v"(rr) : "v"(tab + 4u * ku) : "memory");
+            asm volatile("ds_read_b32 %0, %1" : "=v"(rr) : "v"(tab + (DW2_OFFTAB ? 8u : 4u) * ku) : "memory");
             Rl[u] = rr;
           }
           asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -759,20 +783,25 @@ __global__ __launch_bounds__(256, 1) void gemm_wsp_kernel(const bf16* __restrict
 #pragma unroll
         for (int u = 0; u < P; ++u) {
           if (k0 + 8 * u >= n) break;
-          const int R = rtp * WST_MT + Rl[u];
-          const int w_ = R / wrows, rem = R - w_ * wrows, t2 = rem / 19, f2 = rem - t2 * 19;
-          const int t3 = (t2 - 2) >> 1, f3 = (f2 - 2) >> 1;
           u32x4 o8;   // the same conversion as fe_dw2_kernel's store8 (round to nearest even)
 #pragma unroll
           for (int h = 0; h < 4; ++h) o8[h] = pack_h2<FMT>(a[u][h][0], a[u][h][1]);
-          u32x4* dst = reinterpret_cast<u32x4*>(reinterpret_cast<bf16*>(ep.out) + ((size_t)(w_ * ep.t3n + t3) * 9 + f3) * ep.ldo +
-                                                ct * 256 + cl);
+          size_t oel;
+          if constexpr (DW2_OFFTAB && DW2_PIPE >= 2 && P == 1) {
+            oel = (size_t)Ol + cl;
+          } else {
+            const int R = rtp * WST_MT + Rl[u];
+            const int w_ = R / wrows, rem = R - w_ * wrows, t2 = rem / 19, f2 = rem - t2 * 19;
+            const int t3 = (t2 - 2) >> 1, f3 = (f2 - 2) >> 1;
+            oel = ((size_t)(w_ * ep.t3n + t3) * 9 + f3) * ep.ldo + ct * 256 + cl;
+          }
+          u32x4* dst = reinterpret_cast<u32x4*>(reinterpret_cast<bf16*>(ep.out) + oel);
           if constexpr (DW2_DIAG != 1) {
             if (defer) {
               const unsigned sb = dstg + (unsigned)(base >> 3) * 1280;
               asm volatile("ds_write_b128 %0, %1 offset:0" ::"v"(sb + 16u * lane), "v"(o8) : "memory");
               asm volatile("ds_write_b32 %0, %1 offset:1024" ::"v"(sb + 4u * lane),
-                           "v"((unsigned)(((size_t)(w_ * ep.t3n + t3) * 9 + f3) * ep.ldo + ct * 256 + cl)) : "memory");
+                           "v"((unsigned)oel) : "memory");
             } else if constexpr (DW2_NT) {
               __builtin_nontemporal_store(o8, dst);
             } else {
