@@ -32,7 +32,7 @@ def fixture(golden_dir):
     from chunkformer_amd.weights import synthetic_features, synthetic_state_dict
     g = np.load(os.path.join(golden_dir, "autocast.npz"))
     sd = synthetic_state_dict(LARGE, int(g["seed"]))
-    np.testing.assert_allclose(np.array([float(v.double().sum()) for v in sd.values()]), g["sd_digest"], rtol=0, atol=0)
+    np.testing.assert_allclose(np.array([float(v.double().sum()) for v in sd.values()]), g["sd_digest"], rtol=1e-12, atol=0)  # double sums: order differs by thread count
     lens = g["lens"].tolist()
     return g, sd, synthetic_features(lens, int(g["feat_seed"])), torch.tensor(lens, dtype=torch.int32)
 

@@ -42,7 +42,7 @@ def small(golden_dir):
     g = _load(golden_dir, "small.npz")
     sd = synthetic_state_dict(SMALL, int(g["seed"]))
     dig = np.array([float(v.double().sum()) for v in sd.values()])
-    np.testing.assert_allclose(dig, g["sd_digest"], rtol=0, atol=0)
+    np.testing.assert_allclose(dig, g["sd_digest"], rtol=1e-12, atol=0)  # double sums: order differs by thread count
     return g, sd
 
 
@@ -161,7 +161,7 @@ def test_small256_matches_reference(golden_dir):
     from chunkformer_amd.config import SMALL256
     g = _load(golden_dir, "small256.npz")
     sd = synthetic_state_dict(SMALL256, int(g["seed"]))
-    np.testing.assert_allclose(np.array([float(v.double().sum()) for v in sd.values()]), g["sd_digest"], rtol=0, atol=0)
+    np.testing.assert_allclose(np.array([float(v.double().sum()) for v in sd.values()]), g["sd_digest"], rtol=1e-12, atol=0)  # double sums: order differs by thread count
     lens = g["lens"].tolist()
     xs = synthetic_features(lens, int(g["feat_seed"]))
     out, olens, nch, _, _, _ = ref.forward_parallel_chunk(sd, SMALL256, xs, lens, 64, 128, 128)
