@@ -102,6 +102,28 @@ CFM_DEV void store8(f16* p, const float* x) {
   *reinterpret_cast<f16x8*>(p) = v;
 }
 
+// front-end dw2 (depthwise 3x3 stride 2) on 16-bit activations, shared by fe_dw2_kernel and the fused pw1 + dw2
+// GEMM epilogue so that both compute bit-identical sums: a channel pair's activations stay one packed dword and each
+// channel's tap is ONE dot2 against a weight dword holding (w, 0) or (0, w) in the same 16-bit format -- the weights
+// rounded to that format, as the reference's autocast conv2d casts them (FMT 0 = bf16, 1 = f16)
+#ifndef DW2_DOT2
+#define DW2_DOT2 1
+#endif
+template <int FMT> CFM_DEV float dw2_dot(unsigned x, unsigned wd, float c) {
+  typedef __bf16 bf2_ __attribute__((ext_vector_type(2)));
+  typedef _Float16 h2_ __attribute__((ext_vector_type(2)));
+  if constexpr (FMT == 1)
+    return __builtin_amdgcn_fdot2(__builtin_bit_cast(h2_, x), __builtin_bit_cast(h2_, wd), c, false);
+  else
+    return __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf2_, x), __builtin_bit_cast(bf2_, wd), c, false);
+}
+// the weight dword of channel c: w in the 16-bit half that holds channel c's activation (c & 1), zero in the other
+template <int FMT> CFM_DEV unsigned dw2_wpack(float w, int c) {
+  unsigned short b;
+  if constexpr (FMT == 1) b = __builtin_bit_cast(unsigned short, (f16)w);
+  else b = __builtin_bit_cast(unsigned short, (bf16)w);
+  return (unsigned)b << (16 * (c & 1));
+}
 template <typename T> CFM_DEV typename Frag<T>::type zero8() {
   typename Frag<T>::type z;
 #pragma unroll

@@ -16,6 +16,7 @@
 // become -mean*istd).
 #include <algorithm>
 #include <cstdlib>
+#include <type_traits>
 #include "cfm_common.h"
 #include "cfm_kernels.h"
 
@@ -554,6 +555,48 @@ __global__ __launch_bounds__(256) void fe_dw2_kernel(const T* __restrict__ in, i
   const size_t r = idx / d8;
   const int f3 = r % FE_F3;
   const size_t wn = r / FE_F3;
+  if constexpr (sizeof(T) == 2 && DW2_DOT2) {
+    // 16-bit activations: channel pairs kept packed, one dw2_dot per channel and tap (cfm_common.h), the same
+    // taps in the same order as the fused pw1 + dw2 kernel (gemm_wst_impl.h), so the two agree bit for bit
+    constexpr int FMT = std::is_same<T, f16>::value ? 1 : 0;
+    typedef unsigned u4_ __attribute__((ext_vector_type(4)));
+    unsigned wd[9][8];
+    float bias[8];
+#pragma unroll
+    for (int e = 0; e < 9; ++e)
+#pragma unroll
+      for (int q = 0; q < 8; ++q) wd[e][q] = dw2_wpack<FMT>(w[(size_t)e * d + c + q], q);
+    load8(b + c, bias);
+    const T* ib = in + (wn * T2 * FE_F2 + 2 * f3) * d + c;
+    T* ob = out + (wn * T3 * FE_F3 + f3) * d + c;
+    u4_ top[3];
+#pragma unroll
+    for (int v = 0; v < 3; ++v) top[v] = *reinterpret_cast<const u4_*>(ib + (size_t)(2 * t3a) * FE_F2 * d + (size_t)v * d);
+    for (int t3 = t3a; t3 < t3b; ++t3) {
+      u4_ mid[3], bot[3];
+      const T* rb = ib + (size_t)(2 * t3 + 1) * FE_F2 * d;
+#pragma unroll
+      for (int v = 0; v < 3; ++v) {
+        mid[v] = *reinterpret_cast<const u4_*>(rb + (size_t)v * d);
+        bot[v] = *reinterpret_cast<const u4_*>(rb + (size_t)(FE_F2 + v) * d);
+      }
+      float a[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) a[q] = bias[q];
+#pragma unroll
+      for (int v = 0; v < 3; ++v) {
+        const u4_* rows[3] = {&top[v], &mid[v], &bot[v]};
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+          for (int q = 0; q < 8; ++q) a[q] = dw2_dot<FMT>((*rows[i])[q >> 1], wd[3 * i + v][q], a[q]);
+      }
+      store8(ob + (size_t)t3 * FE_F3 * d, a);
+#pragma unroll
+      for (int v = 0; v < 3; ++v) top[v] = bot[v];
+    }
+    return;
+  }
   float wt[9][8], bias[8];
 #pragma unroll
   for (int e = 0; e < 9; ++e) load8(w + (size_t)e * d + c, wt[e]);

@@ -274,7 +274,10 @@ __global__ __launch_bounds__(256, 1) void gemm_wsp_kernel(const bf16* __restrict
     float* dwl = reinterpret_cast<float*>(smem + NS * WST_SLOT + 1024 + DW2_RING);
     for (int idx = tid; idx < 10 * 256; idx += 256) {
       const int e = idx >> 8, j = idx & 255;
-      dwl[idx] = e < 9 ? ep.dw_w[(size_t)e * N + ct * 256 + j] : ep.dw_b[ct * 256 + j];
+      if (DW2_DOT2 && e < 9)   // tap weights as dw2_dot dwords (cfm_common.h); the bias stays f32
+        reinterpret_cast<unsigned*>(dwl)[idx] = dw2_wpack<FMT>(ep.dw_w[(size_t)e * N + ct * 256 + j], j);
+      else
+        dwl[idx] = e < 9 ? ep.dw_w[(size_t)e * N + ct * 256 + j] : ep.dw_b[ct * 256 + j];
     }
   }
   if (tid < 64)
@@ -671,6 +674,7 @@ __global__ __launch_bounds__(256, 1) void gemm_wsp_kernel(const bf16* __restrict
       // DW2_PPL positions per lane (k, k + 8, ..): each tap's 8 f32 weights are read from LDS once for
       // all of them; packed f32 FMAs (v_pk_fma_f32: per-element fma, the same rounding as fmaf)
       constexpr int P = DW2_PPL;
+      static_assert(!DW2_DOT2 || (DW2_PIPE >= 2 && DW2_PPL == 1), "DW2_DOT2 weights serve the pipelined P = 1 path only");
       const bool defer = DW2_DEFER && P == 1 && n <= 24;
       for (int base = 0; base < n; base += 8 * P) {
         const int k0 = base + (lane >> 3);
@@ -753,11 +757,22 @@ __global__ __launch_bounds__(256, 1) void gemm_wsp_kernel(const bf16* __restrict
               asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(xs[sl]), "+v"(ws[sl][0]), "+v"(ws[sl][1])::"memory");
             const f32x4 w0 = ws[sl][0], w1 = ws[sl][1];
             const u32x4 x = xs[sl];
-            const f32x2 wq[4] = {(f32x2){w0[0], w0[1]}, (f32x2){w0[2], w0[3]}, (f32x2){w1[0], w1[1]}, (f32x2){w1[2], w1[3]}};
+            if constexpr (DW2_DOT2) {
+              // channel pair h: one dot2 per channel against its (w, 0) / (0, w) weight dword
+              const u32x4 d0 = __builtin_bit_cast(u32x4, w0), d1 = __builtin_bit_cast(u32x4, w1);
+              const unsigned wd[8] = {d0[0], d0[1], d0[2], d0[3], d1[0], d1[1], d1[2], d1[3]};
 #pragma unroll
-            for (int h = 0; h < 4; ++h) {
-              const f32x2 xv = dw2_unpk2<FMT>(x[h]);
-              a[0][h] = __builtin_elementwise_fma(wq[h], xv, a[0][h]);
+              for (int h = 0; h < 4; ++h) {
+                a[0][h][0] = dw2_dot<FMT>(x[h], wd[2 * h], a[0][h][0]);
+                a[0][h][1] = dw2_dot<FMT>(x[h], wd[2 * h + 1], a[0][h][1]);
+              }
+            } else {
+              const f32x2 wq[4] = {(f32x2){w0[0], w0[1]}, (f32x2){w0[2], w0[3]}, (f32x2){w1[0], w1[1]}, (f32x2){w1[2], w1[3]}};
+#pragma unroll
+              for (int h = 0; h < 4; ++h) {
+                const f32x2 xv = dw2_unpk2<FMT>(x[h]);
+                a[0][h] = __builtin_elementwise_fma(wq[h], xv, a[0][h]);
+              }
             }
             if constexpr (t + 2 < 9) issue(std::integral_constant<int, t + 2>{});
           });
