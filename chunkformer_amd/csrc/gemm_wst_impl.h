@@ -668,6 +668,7 @@ __global__ __launch_bounds__(256, 1) void gemm_wsp_kernel(const bf16* __restrict
         }
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if constexpr (DW2_DIAG == 3) return;   // timing only: the phase's setup (output rows, rank table) alone
       const int cl = wv * 64 + 8 * (lane & 7);   // the lane's 8 channels within the block's 256
       const float* dwl = reinterpret_cast<const float*>(smem + NS * WST_SLOT + 1024 + DW2_RING);
       const char* ring = smem + NS * WST_SLOT + 1024 + 128 * wv + 16 * (lane & 7);
