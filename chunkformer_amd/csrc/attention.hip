@@ -264,6 +264,9 @@ CFM_DEV int sw128(int row, int ch) { return row * 128 + ((ch ^ ((row >> 1) & 7))
 #define RING_KPF 0   // ring kernel, interior chunks: next tile's K fragments read before this tile's skew (round 6,
                      // with the conflict-free skew: off 4.22 vs on 4.30 ms/step, one-process A/B)
 #endif
+#ifndef RING_V4
+#define RING_V4 1   // next-pair staging in row quads (8-B V^T stores, half the store instructions; C % 4 == 0)
+#endif
 #ifndef ATTN_PRIO
 #define ATTN_PRIO 1   // static wave priority: 1 = the second-dispatched half (waves 4-7) at s_setprio 1 (ring attention
                       // 4.82 -> 4.74 ms/step, tools/ab_prio.sh); 2 = waves 0-3 instead (4.77); 0 = none
@@ -463,6 +466,17 @@ __global__ __launch_bounds__(512, 1) void chunk_attention_ring_kernel(
 #pragma unroll
     for (int e = 0; e < 8; ++e) *reinterpret_cast<ex2_*>(vt + (ch * 8 + e) * VT_PITCH_B + rr * 2) = (ex2_){a[e], b[e]};
   };
+  // RING_V4: four consecutive rows (frow % 4 == 0) x one 16-B chunk: each V^T dim row gets one 8-B store
+  auto stage_quad = [&](int frow, int ch, const u32x4 (&k)[4], const u32x4 (&v)[4]) {
+    const int rr = frow % RING;   // multiple of 4; rr + 3 < RING
+#pragma unroll
+    for (int i = 0; i < 4; ++i) *reinterpret_cast<u32x4*>(kr + sw128(rr + i, ch)) = k[i];
+    typedef E ex4_ __attribute__((ext_vector_type(4)));
+    const ex8 a = __builtin_bit_cast(ex8, v[0]), b = __builtin_bit_cast(ex8, v[1]), c_ = __builtin_bit_cast(ex8, v[2]),
+              d_ = __builtin_bit_cast(ex8, v[3]);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) *reinterpret_cast<ex4_*>(vt + (ch * 8 + e) * VT_PITCH_B + rr * 2) = (ex4_){a[e], b[e], c_[e], d_[e]};
+  };
   auto load_pair = [&](int frow, int ch, u32x4& k0, u32x4& v0, u32x4& k1, u32x4& v1) {
     const E* s0 = KV + (size_t)min(frow, kv_rows - 1) * (2 * d) + h * 128 + ch * 8;
     const E* s1 = KV + (size_t)min(frow + 1, kv_rows - 1) * (2 * d) + h * 128 + ch * 8;
@@ -556,6 +570,17 @@ __global__ __launch_bounds__(512, 1) void chunk_attention_ring_kernel(
     const int pf_pairs = n_new / 2;
     u32x4 pk0[2], pv0[2], pk1[2], pv1[2];
     int pf_row[2], pf_ch[2];
+    if constexpr (RING_V4) {
+      // quads: 2C / 4 <= 32 row quads x 8 chunks <= 256 items, one per thread of the first half
+      const int pf_quads = n_new / 4;
+      pf_row[0] = pf_row[1] = -1;
+      if (pf_quads > 0 && tid < pf_quads * 8) {
+        pf_ch[0] = tid / pf_quads;
+        pf_row[0] = kvp + W + C + 4 * (tid % pf_quads);
+        load_pair(pf_row[0], pf_ch[0], pk0[0], pv0[0], pk1[0], pv1[0]);
+        load_pair(pf_row[0] + 2, pf_ch[0], pk0[1], pv0[1], pk1[1], pv1[1]);
+      }
+    } else {
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
       const int idx = tid + 512 * q;
@@ -565,6 +590,7 @@ __global__ __launch_bounds__(512, 1) void chunk_attention_ring_kernel(
         pf_row[q] = kvp + W + C + 2 * (idx % pf_pairs);
         load_pair(pf_row[q], pf_ch[q], pk0[q], pv0[q], pk1[q], pv1[q]);
       }
+    }
     }
     if (active) {
       const int q_row0 = c * C;
@@ -813,9 +839,16 @@ __global__ __launch_bounds__(512, 1) void chunk_attention_ring_kernel(
     }
     // ---- the prefetched rows replace the first 2C rows of this pair's windows (no longer needed)
     if ((diag & 15) != 7) __syncthreads();
+    if constexpr (RING_V4) {
+      if (pf_row[0] >= 0) {
+        const u32x4 kq[4] = {pk0[0], pk1[0], pk0[1], pk1[1]}, vq[4] = {pv0[0], pv1[0], pv0[1], pv1[1]};
+        stage_quad(pf_row[0], pf_ch[0], kq, vq);
+      }
+    } else {
 #pragma unroll
-    for (int q = 0; q < 2; ++q)
-      if (pf_row[q] >= 0) stage_pair(pf_row[q], pf_ch[q], pk0[q], pv0[q], pk1[q], pv1[q]);
+      for (int q = 0; q < 2; ++q)
+        if (pf_row[q] >= 0) stage_pair(pf_row[q], pf_ch[q], pk0[q], pv0[q], pk1[q], pv1[q]);
+    }
     if ((diag & 15) != 7) __syncthreads();
   }
   if (ATTN_STAGGER && opd) store_out(Od, invd, opd);
