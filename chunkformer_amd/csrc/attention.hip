@@ -570,22 +570,7 @@ __global__ __launch_bounds__(512, 1) void chunk_attention_ring_kernel(
     const int pf_pairs = n_new / 2;
     u32x4 pk0[2], pv0[2], pk1[2], pv1[2];
     int pf_row[2], pf_ch[2];
-    if constexpr (RING_V4 == 2) {
-      // quads, K and V split: threads 0-255 stage the K rows of item tid, threads 256-511 the V rows of item tid - 256
-      const int pf_quads = n_new / 4, it = tid & 255, vh = tid >> 8;
-      pf_row[0] = pf_row[1] = -1;
-      if (pf_quads > 0 && it < pf_quads * 8) {
-        pf_ch[0] = it / pf_quads;
-        pf_row[0] = kvp + W + C + 4 * (it % pf_quads);
-        const u32x4 z4 = (u32x4){0u, 0u, 0u, 0u};
-        (void)z4;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const E* sp = KV + (size_t)min(pf_row[0] + i, kv_rows - 1) * (2 * d) + h * 128 + 64 * vh + pf_ch[0] * 8;
-          (i < 2 ? (i == 0 ? pk0[0] : pk1[0]) : (i == 2 ? pk0[1] : pk1[1])) = *reinterpret_cast<const u32x4*>(sp);
-        }
-      }
-    } else if constexpr (RING_V4) {
+    if constexpr (RING_V4) {
       // quads: 2C / 4 <= 32 row quads x 8 chunks <= 256 items, one per thread of the first half
       const int pf_quads = n_new / 4;
       pf_row[0] = pf_row[1] = -1;
@@ -854,23 +839,7 @@ __global__ __launch_bounds__(512, 1) void chunk_attention_ring_kernel(
     }
     // ---- the prefetched rows replace the first 2C rows of this pair's windows (no longer needed)
     if ((diag & 15) != 7) __syncthreads();
-    if constexpr (RING_V4 == 2) {
-      if (pf_row[0] >= 0) {
-        const int rr = pf_row[0] % RING, ch = pf_ch[0];
-        const u32x4 q4[4] = {pk0[0], pk1[0], pk0[1], pk1[1]};
-        if ((tid >> 8) == 0) {
-#pragma unroll
-          for (int i = 0; i < 4; ++i) *reinterpret_cast<u32x4*>(kr + sw128(rr + i, ch)) = q4[i];
-        } else {
-          typedef E ex4_ __attribute__((ext_vector_type(4)));
-          const ex8 a = __builtin_bit_cast(ex8, q4[0]), b = __builtin_bit_cast(ex8, q4[1]), c_ = __builtin_bit_cast(ex8, q4[2]),
-                    d_ = __builtin_bit_cast(ex8, q4[3]);
-#pragma unroll
-          for (int e = 0; e < 8; ++e)
-            *reinterpret_cast<ex4_*>(vt + (ch * 8 + e) * VT_PITCH_B + rr * 2) = (ex4_){a[e], b[e], c_[e], d_[e]};
-        }
-      }
-    } else if constexpr (RING_V4) {
+    if constexpr (RING_V4) {
       if (pf_row[0] >= 0) {
         const u32x4 kq[4] = {pk0[0], pk1[0], pk0[1], pk1[1]}, vq[4] = {pv0[0], pv1[0], pv0[1], pv1[1]};
         stage_quad(pf_row[0], pf_ch[0], kq, vq);
